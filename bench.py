@@ -1,0 +1,226 @@
+#!/usr/bin/env python
+"""Training-throughput benchmark: KITTI 192x640 multi-frame self-supervised.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Workload (BASELINE.json configs[1]): SelfSupModelMF +
+DepthPoseNet('it8-seq4-inter-out', min_depth 0.5, max_depth 80), Adam lr 2e-4,
+B=2 target frames per GPU, 2 context frames, 192x640, photometric loss with
+automask + min reduction, flip_lr_prob 0.5 (the default).  Synthetic data of
+that shape (smooth random textures, shifted context frames), random init.
+A step = zero_grad -> forward -> loss -> backward -> RCCL all-reduce -> Adam.
+
+Prints ONE JSON line on rank 0; `value` = images/s over all ranks (weak
+scaling: per-GPU batch fixed).  Also reports the roofline of the dominant
+kernel (HIP events) and the CPU-oracle baseline on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "training images/sec (KITTI 192x640 mf self-sup)"
+VERSION = "it8-seq4-inter-out"
+H, W, NREF, MIN_D, MAX_D = 192, 640, 2, 0.5, 80.0
+KITTI_K = [[371.8, 0.0, 314.1], [0.0, 369.4, 88.5], [0.0, 0.0, 1.0]]
+LOSS_KW = dict(ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
+               photometric_reduce_op="min", disp_norm=True, clip_loss=0.0, progressive_scaling=0.0,
+               padding_mode="zeros", automask_loss=True, num_scales=4, rotation_mode="euler",
+               upsample_depth_maps=True, min_depth=MIN_D, max_depth=MAX_D)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def smooth_images(n, gen, device):
+    lo = torch.rand(n, 3, H // 8, W // 8, generator=gen, device=device)
+    up = torch.nn.functional.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False)
+    return (up + 0.1 * torch.rand(n, 3, H, W, generator=gen, device=device)).clamp(0, 1)
+
+
+def make_batch(B, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    img = smooth_images(B, g, device)
+    refs = []
+    for j in range(NREF):
+        shift = (-1) ** j * (2 + j)
+        refs.append((0.97 * torch.roll(img, shift, 3) + 0.03 * smooth_images(B, g, device)).clamp(0, 1))
+    K = torch.tensor(KITTI_K, device=device).unsqueeze(0).repeat(B, 1, 1)
+    return {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
+            "intrinsics": K, "_K0": K.clone()}
+
+
+def build_model(device, flip_prob):
+    from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF
+    from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
+    model = SelfSupModelMF(flip_lr_prob=flip_prob, **LOSS_KW)
+    model.add_depth_net(DepthPoseNet(version=VERSION, min_depth=MIN_D, max_depth=MAX_D))
+    return model.to(device)
+
+
+# ----------------------------------------------------------------------------- roofline
+def roofline_photometric(B, device, iters=20):
+    """Dominant custom kernel pair: the fused photometric loss (forward + backward)
+    at the metric shape.  Algorithmic bytes per forward+backward launch pair (each
+    input read once, each output written once):
+      fwd: image 12 + context 12N + inv 4n + sel n   bytes/px
+      bwd: image 12 + context 12N + inv 4n + sel n + grad_inv 4n bytes/px."""
+    import dro_sfm_amd.hip as hip
+    n = 9
+    g = torch.Generator(device=device)
+    g.manual_seed(5)
+    img = smooth_images(B, g, device)
+    ctx = torch.stack([smooth_images(B, g, device) for _ in range(NREF)])
+    invs = (0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g, device=device)).requires_grad_(True)
+    pose = torch.cat([0.1 * torch.randn(NREF, n, B, 3, generator=g, device=device),
+                      0.02 * torch.randn(NREF, n, B, 3, generator=g, device=device)], 3).requires_grad_(True)
+    K = torch.tensor(KITTI_K, device=device).unsqueeze(0).repeat(B, 1, 1)
+    for _ in range(3):
+        loss, _ = hip.photometric_loss(img, ctx, invs, pose, K)
+        loss.backward()
+    torch.cuda.synchronize()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    fwd_ms = bwd_ms = 0.0
+    for _ in range(iters):
+        e0.record()
+        loss, _ = hip.photometric_loss(img, ctx, invs, pose, K)
+        e1.record()
+        loss.backward()
+        e2.record()
+        torch.cuda.synchronize()
+        fwd_ms += e0.elapsed_time(e1)
+        bwd_ms += e1.elapsed_time(e2)
+    fwd_ms, bwd_ms = fwd_ms / iters, bwd_ms / iters
+    HW = H * W
+    fwd_bytes = HW * B * (12 + 12 * NREF) + HW * B * n * 5
+    bwd_bytes = HW * B * (12 + 12 * NREF) + HW * B * n * 9
+    total_bytes = fwd_bytes + bwd_bytes
+    achieved = total_bytes / ((fwd_ms + bwd_ms) * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "photometric fwd+bwd (photo_fwd_kernel + photo_bwd_kernel)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "algorithmic_bytes": int(total_bytes), "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)}
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(model, steps=2):
+    """Reference algorithm on the host cores: the CPU oracle (a restatement of the
+    reference's PyTorch path, pinned to its golden vectors) running the same
+    training step -- forward, loss, backward, Adam -- on the same weights."""
+    from oracle import dro_oracle as O
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    params = {k: v.detach().cpu().clone() for k, v in model.depth_net.state_dict().items()}
+    leaves = []
+    for k, v in params.items():
+        if v.is_floating_point() and "running" not in k:
+            v.requires_grad_(True)
+            leaves.append(v)
+    opt = torch.optim.Adam(leaves, lr=2e-4)
+    batch = make_batch(2, 1234, "cpu")
+    times = []
+    for s in range(steps + 1):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        out = O.train_step_loss(params, VERSION, MIN_D, MAX_D, batch, kind="selfsup", loss_kw={})
+        out["loss"].sum().backward()
+        opt.step()
+        if s > 0:
+            times.append(time.perf_counter() - t0)
+    sec = sum(times) / len(times)
+    return {"value": round(2 / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed steps (+1 warmup) of the full training step, B=2, 192x640, "
+                      f"N=2, {VERSION}, CPU oracle oracle/dro_oracle.py, torch {torch.__version__}",
+            "sec_per_step": round(sec, 3)}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2, help="target frames per GPU")
+    ap.add_argument("--flip-prob", type=float, default=0.5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
+    args = ap.parse_args()
+
+    from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
+                                                  init_distributed)
+    rank, world, local = init_distributed()
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    torch.manual_seed(42)
+    model = build_model(device, args.flip_prob)
+    model.seed(42 + rank)
+    trainer = DataParallelTrainer(model, lr=2e-4, bucket_mb=25.0, capturable=not args.eager)
+    batches = [make_batch(args.batch, 1000 * rank + i, device) for i in range(4)]
+    mode, stepper = "eager", None
+    if not args.eager:
+        try:
+            stepper = GraphedTrainStep(trainer, batches[0], warmup=max(args.warmup, 2))
+            mode = "hipgraph"
+        except Exception as exc:  # keep measuring, but say so
+            print(f"[bench] graph capture failed ({type(exc).__name__}: {exc}); running eager",
+                  file=sys.stderr, flush=True)
+
+    def run(step_i):
+        b = batches[step_i % len(batches)]
+        if stepper is not None:
+            return stepper.step(b)
+        b["intrinsics"].copy_(b["_K0"])      # the data loader hands a fresh K every step
+        return trainer.step(b)
+
+    for i in range(args.warmup):
+        loss, _ = run(i)
+    if not torch.isfinite(loss).all():
+        raise RuntimeError(f"non-finite loss in warmup: {loss}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, _ = run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    images = world * args.batch * args.steps
+    result = {
+        "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "KITTI 192x640 mf self-sup (configs[1])", "model": f"DepthPoseNet {VERSION}",
+                   "global_batch": world * args.batch, "per_gpu_batch": args.batch, "ref_frames": NREF,
+                   "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
+                   "optimizer": "Adam lr 2e-4", "execution": mode},
+        "final_loss": round(float(loss), 6),
+    }
+    if rank == 0 and not args.no_roofline:
+        result["roofline"] = roofline_photometric(args.batch, device)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(model)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

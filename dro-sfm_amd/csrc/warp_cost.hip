@@ -1,0 +1,445 @@
+// Fused inverse warp + squared feature cost for the DRO recurrent optimizer.
+//
+// Replaces the ATen chain of DepthPoseNet.get_cost_each / depth_cost_calc
+// (dro_sfm/networks/depth_pose/DepthPoseNet.py:76-105): Pose.from_vec,
+// 2x Camera.scaled, Kinv, 3 bmm (reconstruct / transform / project), clamp,
+// normalise, grid_sampler_2d, sub, pow, stack, mean -- ~40 launches per call
+// in the reference -- with ONE launch over every reference view.
+//
+// Layout: all maps dense NCHW fp32.  A 256-thread workgroup covers 64
+// consecutive pixels (one per lane, so every per-channel access of a wave is a
+// 256-B coalesced row segment) x 4 channel groups (one per wave); each thread
+// walks CPT channels.  The projection (~60 flops, 6 sincos) is recomputed per
+// wave instead of being staged: it is far cheaper than a round trip.
+//
+// Roofline: HBM/L2 bound.  Algorithmic bytes per forward call:
+//   P * ((N+2) * 4C + 4)   [fmap + N ref maps read once, cost written once,
+//                           depth read once]; backward ~ P * (5*4C + 8) per ref.
+#include <hip/hip_runtime.h>
+
+#include "dro_common.hpp"
+
+namespace dro {
+
+constexpr int kCPT = 8;        // channels per thread
+constexpr int kGroups = 4;     // channel groups (waves) per workgroup
+constexpr int kGeoThreads = 256;
+
+struct WarpArgs {
+  const float* fmap;
+  const float* fmap_ref;
+  const float* depth;
+  const float* K;
+  const float* ref_K;
+  const float* pose;
+  int depth_mode, pose_mode;
+  float min_disp, span;
+  float scale;
+  int do_scale;
+  int B, N, C, h, w;
+  int reduce_mean;
+};
+
+__device__ __forceinline__ void cams(const WarpArgs& a, int b, float ki[9], float kr[9]) {
+  float k[9];
+  scaled_K(a.K + 9 * b, a.scale, a.do_scale, k);
+  K_inverse(k, ki);
+  scaled_K(a.ref_K + 9 * b, a.scale, a.do_scale, kr);
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* __restrict__ cost) {
+  const int P = a.h * a.w;
+  const int p = blockIdx.x * kWave + (threadIdx.x & 63);
+  const int b = blockIdx.z;
+  const int c0 = (blockIdx.y * kGroups + (threadIdx.x >> 6)) * kCPT;
+  if (p >= P || c0 >= a.C) return;
+  const int cn = min(kCPT, a.C - c0);
+
+  float ki[9], kr[9];
+  cams(a, b, ki, kr);
+  float dd;
+  const float depth = decode_depth(a.depth[b * P + p], a.depth_mode, a.min_disp, a.span, &dd);
+  const float u = (float)(p % a.w), v = (float)(p / a.w);
+
+  float f[kCPT], acc[kCPT];
+  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
+#pragma unroll
+  for (int c = 0; c < kCPT; ++c) {
+    f[c] = (c < cn) ? fm[(size_t)c * P] : 0.f;
+    acc[c] = 0.f;
+  }
+  const int ps = pose_stride(a.pose_mode);
+  for (int n = 0; n < a.N; ++n) {
+    float R[9], t[3];
+    load_pose(a.pose + (size_t)(n * a.B + b) * ps, a.pose_mode, R, t);
+    Proj q;
+    project(ki, kr, R, t, u, v, depth, a.h, a.w, q);
+    Taps T;
+    bilinear_taps(q.ix, q.iy, a.h, a.w, T);
+    const float* fr = a.fmap_ref + (((size_t)n * a.B + b) * a.C + c0) * P;
+#pragma unroll
+    for (int c = 0; c < kCPT; ++c) {
+      if (c < cn) {
+        const float* pl = fr + (size_t)c * P;
+        float val = 0.f;
+        if (T.ok[0]) val += pl[T.idx[0]] * T.wgt[0];
+        if (T.ok[1]) val += pl[T.idx[1]] * T.wgt[1];
+        if (T.ok[2]) val += pl[T.idx[2]] * T.wgt[2];
+        if (T.ok[3]) val += pl[T.idx[3]] * T.wgt[3];
+        const float d = f[c] - val;
+        if (a.reduce_mean) {
+          acc[c] += d * d;
+        } else {
+          cost[(((size_t)n * a.B + b) * a.C + c0 + c) * P + p] = d * d;
+        }
+      }
+    }
+  }
+  if (a.reduce_mean) {
+    float* out = cost + ((size_t)b * a.C + c0) * P + p;
+    const float invN = (float)a.N;
+#pragma unroll
+    for (int c = 0; c < kCPT; ++c)
+      if (c < cn) out[(size_t)c * P] = acc[c] / invN;
+  }
+}
+
+// ------------------------------------------------------------------ backward: feature side
+// d/dfmap, d/dfmap_ref (bilinear scatter, fp32 atomics) and the per-pixel
+// sampling-position gradient gxy[n,b,p] = sum_c dL/dwarped * dwarped/d(ix,iy).
+__global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
+    WarpArgs a, const float* __restrict__ gcost, float* __restrict__ gfmap,
+    float* __restrict__ gfref, float* __restrict__ gxy) {
+  const int P = a.h * a.w;
+  const int p = blockIdx.x * kWave + (threadIdx.x & 63);
+  const int b = blockIdx.z;
+  const int c0 = (blockIdx.y * kGroups + (threadIdx.x >> 6)) * kCPT;
+  if (p >= P || c0 >= a.C) return;
+  const int cn = min(kCPT, a.C - c0);
+
+  float ki[9], kr[9];
+  cams(a, b, ki, kr);
+  float dd;
+  const float depth = decode_depth(a.depth[b * P + p], a.depth_mode, a.min_disp, a.span, &dd);
+  const float u = (float)(p % a.w), v = (float)(p / a.w);
+  const float scaleN = a.reduce_mean ? 1.f / (float)a.N : 1.f;
+
+  float f[kCPT], gf[kCPT], g[kCPT];
+  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
+#pragma unroll
+  for (int c = 0; c < kCPT; ++c) {
+    f[c] = (c < cn) ? fm[(size_t)c * P] : 0.f;
+    gf[c] = 0.f;
+  }
+  if (a.reduce_mean) {
+    const float* gp = gcost + ((size_t)b * a.C + c0) * P + p;
+#pragma unroll
+    for (int c = 0; c < kCPT; ++c) g[c] = (c < cn) ? gp[(size_t)c * P] * scaleN : 0.f;
+  }
+  const int ps = pose_stride(a.pose_mode);
+  for (int n = 0; n < a.N; ++n) {
+    if (!a.reduce_mean) {
+      const float* gp = gcost + (((size_t)n * a.B + b) * a.C + c0) * P + p;
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) g[c] = (c < cn) ? gp[(size_t)c * P] : 0.f;
+    }
+    float R[9], t[3];
+    load_pose(a.pose + (size_t)(n * a.B + b) * ps, a.pose_mode, R, t);
+    Proj q;
+    project(ki, kr, R, t, u, v, depth, a.h, a.w, q);
+    Taps T;
+    bilinear_taps(q.ix, q.iy, a.h, a.w, T);
+    const float* fr = a.fmap_ref + (((size_t)n * a.B + b) * a.C + c0) * P;
+    float* gr = gfref ? gfref + (((size_t)n * a.B + b) * a.C + c0) * P : nullptr;
+    const float omy = 1.f - T.ty, omx = 1.f - T.tx;
+    float gix = 0.f, giy = 0.f;
+#pragma unroll
+    for (int c = 0; c < kCPT; ++c) {
+      if (c < cn) {
+        const float* pl = fr + (size_t)c * P;
+        const float v0 = T.ok[0] ? pl[T.idx[0]] : 0.f;
+        const float v1 = T.ok[1] ? pl[T.idx[1]] : 0.f;
+        const float v2 = T.ok[2] ? pl[T.idx[2]] : 0.f;
+        const float v3 = T.ok[3] ? pl[T.idx[3]] : 0.f;
+        const float val = v0 * T.wgt[0] + v1 * T.wgt[1] + v2 * T.wgt[2] + v3 * T.wgt[3];
+        const float gd = 2.f * (f[c] - val) * g[c];  // d cost / d fmap
+        gf[c] += gd;
+        const float gw = -gd;                         // d cost / d warped
+        if (gr) {
+          float* gpl = gr + (size_t)c * P;
+          if (T.ok[0]) atomicAdd(gpl + T.idx[0], gw * T.wgt[0]);
+          if (T.ok[1]) atomicAdd(gpl + T.idx[1], gw * T.wgt[1]);
+          if (T.ok[2]) atomicAdd(gpl + T.idx[2], gw * T.wgt[2]);
+          if (T.ok[3]) atomicAdd(gpl + T.idx[3], gw * T.wgt[3]);
+        }
+        gix += gw * ((v1 - v0) * omy + (v3 - v2) * T.ty);
+        giy += gw * ((v2 - v0) * omx + (v3 - v1) * T.tx);
+      }
+    }
+    if (gxy) {
+      float* dst = gxy + ((size_t)(n * a.B + b) * P + p) * 2;
+      atomicAdd(dst, gix);
+      atomicAdd(dst + 1, giy);
+    }
+  }
+  if (gfmap) {
+    float* out = gfmap + ((size_t)b * a.C + c0) * P + p;
+#pragma unroll
+    for (int c = 0; c < kCPT; ++c)
+      if (c < cn) out[(size_t)c * P] = gf[c];
+  }
+}
+
+// ------------------------------------------------------------------ backward: geometry side
+// One thread per (b, pixel): chain gxy through the projection to the depth
+// input (summed over refs, no atomics) and to per-workgroup pose partials.
+__global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
+    WarpArgs a, const float* __restrict__ gxy, float* __restrict__ gdepth,
+    float* __restrict__ partial) {
+  __shared__ float scratch[12 * (kGeoThreads / kWave)];
+  const int P = a.h * a.w;
+  const int p = blockIdx.x * kGeoThreads + threadIdx.x;
+  const int b = blockIdx.y;
+  const bool live = p < P;
+  float ki[9], kr[9];
+  cams(a, b, ki, kr);
+  float dd = 0.f, depth = 0.f;
+  if (live) depth = decode_depth(a.depth[b * P + p], a.depth_mode, a.min_disp, a.span, &dd);
+  const float u = live ? (float)(p % a.w) : 0.f, v = live ? (float)(p / a.w) : 0.f;
+  const int ps = pose_stride(a.pose_mode);
+  float gd_total = 0.f;
+  for (int n = 0; n < a.N; ++n) {
+    float R[9], t[3];
+    load_pose(a.pose + (size_t)(n * a.B + b) * ps, a.pose_mode, R, t);
+    float acc[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+    if (live) {
+      Proj q;
+      project(ki, kr, R, t, u, v, depth, a.h, a.w, q);
+      const float* g = gxy + ((size_t)(n * a.B + b) * P + p) * 2;
+      gd_total += project_backward(q, kr, R, g[0], g[1], acc, acc + 9);
+    }
+    if (partial) {
+      block_sum<12>(acc, scratch);
+      if (threadIdx.x == 0) {
+        float* dst = partial + (((size_t)n * a.B + b) * gridDim.x + blockIdx.x) * 12;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) dst[k] = acc[k];
+      }
+    }
+  }
+  if (gdepth && live) gdepth[b * P + p] = gd_total * dd;
+}
+
+__global__ void pose_finalize_kernel(const float* __restrict__ partial, int nblk, int npose,
+                                     const float* __restrict__ pose, int pose_mode,
+                                     float* __restrict__ gpose) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npose) return;
+  float s[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) s[k] = 0.f;
+  for (int j = 0; j < nblk; ++j) {
+    const float* src = partial + ((size_t)i * nblk + j) * 12;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s[k] += src[k];
+  }
+  const int ps = pose_stride(pose_mode);
+  store_pose_grad(pose + (size_t)i * ps, pose_mode, s, s + 9, gpose + (size_t)i * ps);
+}
+
+// ------------------------------------------------------------------ plane sweep (forward only)
+__global__ __launch_bounds__(256) void plane_sweep_kernel(WarpArgs a, const float* __restrict__ disp,
+                                                          int D, float* __restrict__ cost) {
+  const int P = a.h * a.w;
+  const int p = blockIdx.x * kWave + (threadIdx.x & 63);
+  const int b = blockIdx.z / D, d = blockIdx.z % D;
+  const int c0 = (blockIdx.y * kGroups + (threadIdx.x >> 6)) * kCPT;
+  if (p >= P || c0 >= a.C) return;
+  const int cn = min(kCPT, a.C - c0);
+  float ki[9], kr[9];
+  cams(a, b, ki, kr);
+  float dd;
+  const float depth = decode_depth(disp[d], DRO_DEPTH_DISP, a.min_disp, a.span, &dd);
+  float R[9], t[3];
+  load_pose(a.pose + (size_t)b * pose_stride(a.pose_mode), a.pose_mode, R, t);
+  Proj q;
+  project(ki, kr, R, t, (float)(p % a.w), (float)(p / a.w), depth, a.h, a.w, q);
+  Taps T;
+  bilinear_taps(q.ix, q.iy, a.h, a.w, T);
+  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
+  const float* fr = a.fmap_ref + ((size_t)b * a.C + c0) * P;
+  float* out = cost + (((size_t)b * D + d) * a.C + c0) * P + p;
+#pragma unroll
+  for (int c = 0; c < kCPT; ++c) {
+    if (c < cn) {
+      const float* pl = fr + (size_t)c * P;
+      float val = 0.f;
+      if (T.ok[0]) val += pl[T.idx[0]] * T.wgt[0];
+      if (T.ok[1]) val += pl[T.idx[1]] * T.wgt[1];
+      if (T.ok[2]) val += pl[T.idx[2]] * T.wgt[2];
+      if (T.ok[3]) val += pl[T.idx[3]] * T.wgt[3];
+      const float df = fm[(size_t)c * P] - val;
+      out[(size_t)c * P] = df * df;
+    }
+  }
+}
+
+int launch_pose_finalize(const float* partial, int nblk, int npose, const float* pose,
+                         int pose_mode, float* gpose, hipStream_t s) {
+  hipLaunchKernelGGL(pose_finalize_kernel, dim3((npose + 63) / 64), dim3(64), 0, s, partial, nblk,
+                     npose, pose, pose_mode, gpose);
+  return launch_status("pose_finalize_kernel launch failed");
+}
+
+static int check_common(const float* fmap, const float* fmap_ref, const float* K,
+                        const float* ref_K, const float* pose, int pose_mode, int B, int N, int C,
+                        int h, int w) {
+  if (!fmap || !fmap_ref || !K || !ref_K || !pose) {
+    set_error("warp_cost: NULL input pointer");
+    return DRO_E_NULL;
+  }
+  if (B < 1 || N < 1 || C < 1 || h < 2 || w < 2 || (long long)h * w > (1LL << 30)) {
+    set_error("warp_cost: sizes out of range (need B,N,C >= 1, h,w >= 2)");
+    return DRO_E_SHAPE;
+  }
+  if (pose_mode != DRO_POSE_EULER && pose_mode != DRO_POSE_MATRIX) {
+    set_error("warp_cost: unknown pose_mode");
+    return DRO_E_MODE;
+  }
+  return DRO_OK;
+}
+
+static WarpArgs make_args(const float* fmap, const float* fmap_ref, const float* depth,
+                          int depth_mode, float min_disp, float max_disp, const float* K,
+                          const float* ref_K, float scale, const float* pose, int pose_mode, int B,
+                          int N, int C, int h, int w, int reduce_mean) {
+  WarpArgs a;
+  a.fmap = fmap;
+  a.fmap_ref = fmap_ref;
+  a.depth = depth;
+  a.K = K;
+  a.ref_K = ref_K;
+  a.pose = pose;
+  a.depth_mode = depth_mode;
+  a.pose_mode = pose_mode;
+  a.min_disp = min_disp;
+  a.span = max_disp - min_disp;
+  a.scale = scale;
+  a.do_scale = scale != 1.0f;
+  a.B = B;
+  a.N = N;
+  a.C = C;
+  a.h = h;
+  a.w = w;
+  a.reduce_mean = reduce_mean;
+  return a;
+}
+
+}  // namespace dro
+
+using namespace dro;
+
+extern "C" size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w) {
+  const size_t P = (size_t)h * w;
+  const size_t nblk = (P + kGeoThreads - 1) / kGeoThreads;
+  return ((size_t)N * B * P * 2 + (size_t)N * B * nblk * 12) * sizeof(float);
+}
+
+extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, const float* depth,
+                                     int depth_mode, float min_disp, float max_disp,
+                                     const float* K, const float* ref_K, float scale,
+                                     const float* pose, int pose_mode, int B, int N, int C, int h,
+                                     int w, int reduce_mean, float* cost, void* stream) {
+  int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, N, C, h, w);
+  if (st) return st;
+  if (!depth || !cost) {
+    set_error("warp_cost_forward: NULL depth/cost");
+    return DRO_E_NULL;
+  }
+  if (depth_mode < DRO_DEPTH_METRIC || depth_mode > DRO_DEPTH_DISP) {
+    set_error("warp_cost_forward: unknown depth_mode");
+    return DRO_E_MODE;
+  }
+  WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
+                         pose, pose_mode, B, N, C, h, w, reduce_mean);
+  const int P = h * w;
+  dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
+  hipLaunchKernelGGL(warp_cost_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, cost);
+  return launch_status("warp_cost_fwd_kernel launch failed");
+}
+
+extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float* depth,
+                                      int depth_mode, float min_disp, float max_disp,
+                                      const float* K, const float* ref_K, float scale,
+                                      const float* pose, int pose_mode, int B, int N, int C,
+                                      int h, int w, int reduce_mean, const float* grad_cost,
+                                      float* grad_fmap, float* grad_fmap_ref, float* grad_depth,
+                                      float* grad_pose, void* workspace, void* stream) {
+  int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, N, C, h, w);
+  if (st) return st;
+  if (!depth || !grad_cost) {
+    set_error("warp_cost_backward: NULL depth/grad_cost");
+    return DRO_E_NULL;
+  }
+  const bool geo = grad_depth || grad_pose;
+  if (geo && !workspace) {
+    set_error("warp_cost_backward: workspace required for depth/pose gradients");
+    return DRO_E_NULL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
+                         pose, pose_mode, B, N, C, h, w, reduce_mean);
+  const int P = h * w;
+  float* gxy = geo ? (float*)workspace : nullptr;
+  const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
+  float* partial = (geo && grad_pose) ? gxy + (size_t)N * B * P * 2 : nullptr;
+  if (grad_fmap_ref) {
+    hipError_t e = hipMemsetAsync(grad_fmap_ref, 0, sizeof(float) * (size_t)N * B * C * P, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (gxy) {
+    hipError_t e = hipMemsetAsync(gxy, 0, sizeof(float) * (size_t)N * B * P * 2, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (grad_fmap || grad_fmap_ref || gxy) {
+    dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
+    hipLaunchKernelGGL(warp_cost_bwd_feat_kernel, grid, dim3(256), 0, s, a, grad_cost, grad_fmap,
+                       grad_fmap_ref, gxy);
+    if ((st = launch_status("warp_cost_bwd_feat_kernel launch failed"))) return st;
+  }
+  if (geo) {
+    hipLaunchKernelGGL(warp_cost_bwd_geo_kernel, dim3(nblk, B), dim3(kGeoThreads), 0, s, a, gxy,
+                       grad_depth, partial);
+    if ((st = launch_status("warp_cost_bwd_geo_kernel launch failed"))) return st;
+  }
+  if (grad_pose) {
+    if ((st = launch_pose_finalize(partial, nblk, N * B, pose, pose_mode, grad_pose, s))) return st;
+  }
+  return DRO_OK;
+}
+
+extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref, const float* disp,
+                                       int D, float min_disp, float max_disp, const float* K,
+                                       const float* ref_K, float scale, const float* pose,
+                                       int pose_mode, int B, int C, int h, int w, float* cost,
+                                       void* stream) {
+  int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, 1, C, h, w);
+  if (st) return st;
+  if (!disp || !cost) {
+    set_error("plane_sweep_forward: NULL disp/cost");
+    return DRO_E_NULL;
+  }
+  if (D < 1 || (long long)B * D > 65535) {
+    set_error("plane_sweep_forward: D out of range");
+    return DRO_E_SHAPE;
+  }
+  WarpArgs a = make_args(fmap, fmap_ref, nullptr, DRO_DEPTH_DISP, min_disp, max_disp, K, ref_K,
+                         scale, pose, pose_mode, B, 1, C, h, w, 0);
+  const int P = h * w;
+  dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B * D);
+  hipLaunchKernelGGL(plane_sweep_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D, cost);
+  return launch_status("plane_sweep_kernel launch failed");
+}

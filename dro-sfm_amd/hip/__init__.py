@@ -1,0 +1,11 @@
+"""Autograd-aware wrappers of the gfx950 kernels (libdro_amd.so).
+
+Every op launches on torch's current HIP stream, allocates only through the
+PyTorch caching allocator and never synchronises, so whole training steps can
+be captured into a hipGraph.
+"""
+from .ops import (DEPTH_DISP, DEPTH_INV, DEPTH_METRIC, POSE_EULER, POSE_MATRIX,
+                  convex_upsample, photometric_loss, plane_sweep_cost, warp_cost)
+
+__all__ = ["warp_cost", "plane_sweep_cost", "photometric_loss", "convex_upsample",
+           "POSE_EULER", "POSE_MATRIX", "DEPTH_METRIC", "DEPTH_INV", "DEPTH_DISP"]

@@ -1,0 +1,86 @@
+"""ctypes binding of libdro_amd.so (C ABI: include/dro_amd.h).
+
+The library is loaded AFTER torch so that its NEEDED libamdhip64.so.7 resolves
+to the HIP runtime torch already mapped (one runtime, one device context).
+There is deliberately no fallback: if the library is missing, or the tensors
+are not on a ROCm device, the ops raise.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "libdro_amd.so"))
+
+_c_float_p = ctypes.c_void_p
+_lib = None
+
+
+def _sig(fn, *argtypes, restype=ctypes.c_int):
+    fn.argtypes = list(argtypes)
+    fn.restype = restype
+
+
+def load():
+    """Load and type the library once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"dro_sfm_amd: native library not found at {LIB_PATH}; build it with "
+            "`make -C dro-sfm_amd/csrc` (or __graft_entry__.build()).  There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P, I, F, S, Z = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+    _sig(lib.dro_last_error, restype=ctypes.c_char_p)
+    _sig(lib.dro_abi_version)
+    _sig(lib.dro_warp_cost_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, P, S)
+    _sig(lib.dro_warp_cost_workspace_bytes, I, I, I, I, restype=Z)
+    _sig(lib.dro_warp_cost_backward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I,
+         P, P, P, P, P, P, S)
+    _sig(lib.dro_plane_sweep_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, P, S)
+    _sig(lib.dro_photometric_workspace_bytes, I, I, I, I, I, restype=Z)
+    _sig(lib.dro_photometric_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I,
+         P, P, S)
+    _sig(lib.dro_photometric_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I,
+         P, P, P, P, S)
+    _sig(lib.dro_convex_upsample_forward, P, P, I, I, I, I, P, S)
+    _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, P, P, S)
+    _lib = lib
+    return lib
+
+
+# names every consumer can check against include/dro_amd.h
+EXPORTED = (
+    "dro_last_error", "dro_abi_version",
+    "dro_warp_cost_forward", "dro_warp_cost_workspace_bytes", "dro_warp_cost_backward",
+    "dro_plane_sweep_forward",
+    "dro_photometric_workspace_bytes", "dro_photometric_forward", "dro_photometric_backward",
+    "dro_convex_upsample_forward", "dro_convex_upsample_backward",
+)
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().dro_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors, what="op"):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(f"dro_sfm_amd.{what}: tensors must live on a ROCm device "
+                               "(no CPU fallback)")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"dro_sfm_amd.{what}: expected float32, got {t.dtype}")

@@ -1,0 +1,228 @@
+"""torch.autograd.Function wrappers over the C ABI of libdro_amd.so.
+
+Each Function checks dtype/device/shape up front (RuntimeError, as the
+reference's ATen ops would raise), allocates outputs through the caching
+allocator, and launches on the current stream.
+"""
+import torch
+
+from . import _lib
+from ._lib import check, ptr, require_device, stream_of
+
+POSE_EULER, POSE_MATRIX = 0, 1
+DEPTH_METRIC, DEPTH_INV, DEPTH_DISP = 0, 1, 2
+
+
+def _pose_layout(pose, lead):
+    """Return (flat pose [*lead, 6|12] contiguous, mode, restore-fn for its grad)."""
+    if pose.shape[-1] == 6 and pose.dim() == len(lead) + 1:
+        return pose.contiguous(), POSE_EULER, lambda g: g
+    if pose.shape[-2:] in ((3, 4), (4, 4)) and pose.dim() == len(lead) + 2:
+        rows = pose.shape[-2]
+        flat = pose[..., :3, :].contiguous().view(*lead, 12)
+
+        def restore(g):
+            g = g.view(*lead, 3, 4)
+            if rows == 4:
+                g = torch.cat([g, g.new_zeros(*lead, 1, 4)], dim=-2)
+            return g
+        return flat, POSE_MATRIX, restore
+    raise RuntimeError(f"pose must be [...,6] (euler) or [...,3|4,4] matrices, got {tuple(pose.shape)}")
+
+
+def _disp_range(min_depth, max_depth):
+    if min_depth is None or max_depth is None:
+        return 0.0, 0.0
+    return 1.0 / max_depth, 1.0 / min_depth
+
+
+# ------------------------------------------------------------------------- warp + feature cost
+class _WarpCost(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale,
+                reduce_mean):
+        lib = _lib.load()
+        require_device(fmap, fmap_ref, depth, K, ref_K, what="warp_cost")
+        B, C, h, w = fmap.shape
+        N = fmap_ref.shape[0]
+        if fmap_ref.shape != (N, B, C, h, w) or depth.shape != (B, 1, h, w) or K.shape != (B, 3, 3):
+            raise RuntimeError("warp_cost: shape mismatch (fmap [B,C,h,w], fmap_ref [N,B,C,h,w], "
+                               "depth [B,1,h,w], K [B,3,3])")
+        pose_flat, pose_mode, restore = _pose_layout(pose, (N, B))
+        require_device(pose_flat, what="warp_cost")
+        fmap, fmap_ref, depth = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous()
+        K, ref_K = K.contiguous(), ref_K.contiguous()
+        out_shape = (B, C, h, w) if reduce_mean else (N, B, C, h, w)
+        cost = torch.empty(out_shape, device=fmap.device, dtype=torch.float32)
+        check(lib.dro_warp_cost_forward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode,
+                                        min_disp, max_disp, ptr(K), ptr(ref_K), scale,
+                                        ptr(pose_flat), pose_mode, B, N, C, h, w, int(reduce_mean),
+                                        ptr(cost), stream_of(fmap)), "dro_warp_cost_forward")
+        ctx.save_for_backward(fmap, fmap_ref, depth, pose_flat, K, ref_K)
+        ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode, int(reduce_mean))
+        ctx.restore = restore
+        return cost
+
+    @staticmethod
+    def backward(ctx, gcost):
+        lib = _lib.load()
+        fmap, fmap_ref, depth, pose_flat, K, ref_K = ctx.saved_tensors
+        depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean = ctx.cfg
+        B, C, h, w = fmap.shape
+        N = fmap_ref.shape[0]
+        need = ctx.needs_input_grad
+        gcost = gcost.contiguous()
+        g_f = torch.empty_like(fmap) if need[0] else None
+        g_r = torch.empty_like(fmap_ref) if need[1] else None
+        g_d = torch.empty_like(depth) if need[2] else None
+        g_p = torch.empty_like(pose_flat) if need[3] else None
+        ws = None
+        if g_d is not None or g_p is not None:
+            nbytes = lib.dro_warp_cost_workspace_bytes(B, N, h, w)
+            ws = torch.empty(nbytes // 4 + 1, device=fmap.device, dtype=torch.float32)
+        check(lib.dro_warp_cost_backward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode,
+                                         min_disp, max_disp, ptr(K), ptr(ref_K), scale,
+                                         ptr(pose_flat), pose_mode, B, N, C, h, w, reduce_mean,
+                                         ptr(gcost), ptr(g_f), ptr(g_r), ptr(g_d), ptr(g_p),
+                                         ptr(ws), stream_of(fmap)), "dro_warp_cost_backward")
+        if g_p is not None:
+            g_p = ctx.restore(g_p)
+        return g_f, g_r, g_d, g_p, None, None, None, None, None, None, None
+
+
+def warp_cost(fmap, fmap_ref, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_METRIC,
+              min_depth=None, max_depth=None, scale=1.0 / 8, reduce_mean=True):
+    """Fused get_cost_each / depth_cost_calc (DepthPoseNet.py:76-105).
+
+    fmap [B,C,h,w]; fmap_ref [N,B,C,h,w]; depth [B,1,h,w] encoded per depth_mode
+    (DEPTH_DISP applies disp_to_depth(min_depth, max_depth) then inv2depth);
+    pose [N,B,6] euler vectors or [N,B,3|4,4] matrices; K/ref_K full-res [B,3,3].
+    Returns the mean cost over refs [B,C,h,w] (reduce_mean) or [N,B,C,h,w].
+    """
+    if fmap_ref.dim() == 4:
+        fmap_ref = fmap_ref.unsqueeze(0)
+        pose = pose.unsqueeze(0)
+    min_disp, max_disp = _disp_range(min_depth, max_depth)
+    if depth_mode == DEPTH_DISP and (min_depth is None or max_depth is None):
+        raise RuntimeError("warp_cost: DEPTH_DISP needs min_depth and max_depth")
+    return _WarpCost.apply(fmap, fmap_ref, depth, pose, K, K if ref_K is None else ref_K,
+                           depth_mode, float(min_disp), float(max_disp), float(scale), reduce_mean)
+
+
+def plane_sweep_cost(fmap, fmap_ref, disp, pose, K, ref_K=None, *, min_depth, max_depth,
+                     scale=1.0 / 8):
+    """Cost of D fronto-parallel planes (disp [D] in sigmoid space): [B,D,C,h,w]."""
+    lib = _lib.load()
+    require_device(fmap, fmap_ref, disp, K, what="plane_sweep_cost")
+    B, C, h, w = fmap.shape
+    D = disp.numel()
+    pose_flat, pose_mode, _ = _pose_layout(pose, (B,))
+    ref_K = K if ref_K is None else ref_K
+    min_disp, max_disp = _disp_range(min_depth, max_depth)
+    fmap, fmap_ref, disp = fmap.contiguous(), fmap_ref.contiguous(), disp.contiguous()
+    K, ref_K = K.contiguous(), ref_K.contiguous()
+    cost = torch.empty(B, D, C, h, w, device=fmap.device, dtype=torch.float32)
+    check(lib.dro_plane_sweep_forward(ptr(fmap), ptr(fmap_ref), ptr(disp), D, float(min_disp),
+                                      float(max_disp), ptr(K), ptr(ref_K), float(scale),
+                                      ptr(pose_flat), pose_mode, B, C, h, w, ptr(cost),
+                                      stream_of(fmap)), "dro_plane_sweep_forward")
+    return cost
+
+
+# ------------------------------------------------------------------------- photometric loss
+class _Photometric(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, image, context, inv_depths, pose, K, ref_K, opts):
+        lib = _lib.load()
+        require_device(image, context, inv_depths, K, ref_K, what="photometric_loss")
+        n, B, _, H, W = inv_depths.shape
+        N = context.shape[0]
+        if image.shape != (B, 3, H, W) or context.shape != (N, B, 3, H, W):
+            raise RuntimeError("photometric_loss: image [B,3,H,W], context [N,B,3,H,W] and "
+                               "inv_depths [n,B,1,H,W] must share B,H,W (full-res predictions)")
+        pose_flat, pose_mode, restore = _pose_layout(pose, (N, n, B))
+        ssim_w, C1, C2, smooth_w, automask, reduce_min = opts
+        image, context, inv_depths = image.contiguous(), context.contiguous(), inv_depths.contiguous()
+        K, ref_K = K.contiguous(), ref_K.contiguous()
+        nbytes = lib.dro_photometric_workspace_bytes(B, N, n, H, W)
+        ws = torch.empty(nbytes, device=image.device, dtype=torch.uint8)
+        out = torch.empty(3, device=image.device, dtype=torch.float32)
+        check(lib.dro_photometric_forward(ptr(image), ptr(context), ptr(inv_depths), ptr(K),
+                                          ptr(ref_K), ptr(pose_flat), pose_mode, B, N, n, H, W,
+                                          ssim_w, C1, C2, smooth_w, automask, reduce_min,
+                                          ptr(out), ptr(ws), stream_of(image)),
+              "dro_photometric_forward")
+        ctx.save_for_backward(image, context, inv_depths, pose_flat, K, ref_K, ws)
+        ctx.cfg = (pose_mode, opts)
+        ctx.restore = restore
+        metrics = out[1:].detach()
+        ctx.mark_non_differentiable(metrics)
+        return out[0:1], metrics
+
+    @staticmethod
+    def backward(ctx, gloss, _gmetrics):
+        lib = _lib.load()
+        image, context, inv_depths, pose_flat, K, ref_K, ws = ctx.saved_tensors
+        pose_mode, (ssim_w, C1, C2, smooth_w, automask, reduce_min) = ctx.cfg
+        n, B, _, H, W = inv_depths.shape
+        N = context.shape[0]
+        gloss = gloss.contiguous()
+        g_inv = torch.empty_like(inv_depths)
+        g_pose = torch.empty_like(pose_flat) if ctx.needs_input_grad[3] else None
+        check(lib.dro_photometric_backward(ptr(image), ptr(context), ptr(inv_depths), ptr(K),
+                                           ptr(ref_K), ptr(pose_flat), pose_mode, B, N, n, H, W,
+                                           ssim_w, C1, C2, smooth_w, automask, reduce_min,
+                                           ptr(gloss), ptr(g_inv), ptr(g_pose), ptr(ws),
+                                           stream_of(image)), "dro_photometric_backward")
+        if g_pose is not None:
+            g_pose = ctx.restore(g_pose)
+        return None, None, g_inv if ctx.needs_input_grad[2] else None, g_pose, None, None, None
+
+
+def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=0.85, C1=1e-4,
+                     C2=9e-4, smooth_w=0.001, automask=True, reduce_min=True):
+    """Fused MultiViewPhotometricDecayLoss (multiview_photometric_loss_mf.py:303-361).
+
+    image [B,3,H,W]; context [N,B,3,H,W]; inv_depths [n,B,1,H,W];
+    pose [N,n,B,6] euler vectors or [N,n,B,3|4,4] matrices.
+    Returns (loss [1], detached metrics [2] = (photometric_loss, smoothness_loss)).
+    """
+    opts = (float(ssim_w), float(C1), float(C2), float(smooth_w), int(bool(automask)),
+            int(bool(reduce_min)))
+    return _Photometric.apply(image, context, inv_depths, pose, K, K if ref_K is None else ref_K,
+                              opts)
+
+
+# ------------------------------------------------------------------------- convex upsample
+class _ConvexUpsample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, inv, mask, ratio):
+        lib = _lib.load()
+        require_device(inv, mask, what="convex_upsample")
+        B, _, h, w = inv.shape
+        if mask.shape != (B, 9 * ratio * ratio, h, w):
+            raise RuntimeError("convex_upsample: mask must be [B, 9*r*r, h, w]")
+        inv, mask = inv.contiguous(), mask.contiguous()
+        out = torch.empty(B, 1, h * ratio, w * ratio, device=inv.device, dtype=torch.float32)
+        check(lib.dro_convex_upsample_forward(ptr(inv), ptr(mask), B, h, w, ratio, ptr(out),
+                                              stream_of(inv)), "dro_convex_upsample_forward")
+        ctx.save_for_backward(inv, mask)
+        ctx.ratio = ratio
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        inv, mask = ctx.saved_tensors
+        B, _, h, w = inv.shape
+        g_inv = torch.empty_like(inv) if ctx.needs_input_grad[0] else None
+        g_mask = torch.empty_like(mask)
+        check(lib.dro_convex_upsample_backward(ptr(inv), ptr(mask), ptr(gout.contiguous()), B, h, w,
+                                               ctx.ratio, ptr(g_inv), ptr(g_mask), stream_of(inv)),
+              "dro_convex_upsample_backward")
+        return g_inv, g_mask if ctx.needs_input_grad[1] else None, None
+
+
+def convex_upsample(inv, mask, ratio=8):
+    """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74): [B,1,h,w] -> [B,1,rh,rw]."""
+    return _ConvexUpsample.apply(inv, mask, int(ratio))

@@ -1,0 +1,140 @@
+"""DepthPoseNet -- the DRO recurrent depth/pose optimizer on MI355X.
+
+Drop-in for dro_sfm/networks/depth_pose/DepthPoseNet.py:16-205: same
+constructor (version, min_depth, max_depth), same forward(target_image,
+ref_imgs, intrinsics) and train/eval return conventions, same state_dict keys.
+
+Execution plan (what changes versus the reference, never the math):
+  * every feature cost -- depth cost (mean over refs) and pose cost (per ref) --
+    is ONE fused HIP launch (hip.warp_cost) that builds R from the euler vector,
+    scales K, lifts, projects, bilinearly samples all 128 channels and squares
+    the difference; disp_to_depth + inv2depth are folded in (DEPTH_DISP);
+  * the reference views are processed as one batch: the feature maps of the N
+    refs are a free view of the fnet output [N,B,C,h,w], the initial pose head,
+    and the whole pose update block (cost, encoder, GRU, head) run once over
+    N*B samples instead of N Python iterations;
+  * convex upsampling is one HIP launch (hip.convex_upsample);
+  * no host synchronisation anywhere: the step can be captured in a hipGraph.
+"""
+import logging
+
+import torch
+import torch.nn as nn
+
+from ... import hip
+from ..optim.extractor import ResNetEncoder
+from ..optim.update import (BasicUpdateBlockDepth, BasicUpdateBlockPose, DepthHead, PoseHead,
+                            UpMaskNet)
+
+
+def parse_version(version):
+    """'it{I}[-h][-seq{S}][-inter][-out]' (DepthPoseNet.py:22-34)."""
+    assert version and "it" in version, f"bad DepthPoseNet version {version!r}"
+    fields = version.split("-")
+    total = int(fields[0].split("it")[1])
+    seq = next((int(f.split("seq")[1]) for f in fields if "seq" in f), 4)
+    return {"outer": total // seq, "seq": seq, "high": "h" in version,
+            "out_norm": "out" in version, "inter": "inter" in version}
+
+
+class DepthPoseNet(nn.Module):
+    def __init__(self, version=None, min_depth=0.1, max_depth=100, **kwargs):
+        super().__init__()
+        cfg = parse_version(version)
+        self.version = version
+        self.min_depth, self.max_depth = min_depth, max_depth
+        self.iters, self.seq_len = cfg["outer"], cfg["seq"]
+        self.is_high, self.out_normalize, self.inter_sup = cfg["high"], cfg["out_norm"], cfg["inter"]
+        logging.info("DepthPoseNet(%s): outer=%d seq=%d inter=%s high=%s out_norm=%s", version,
+                     self.iters, self.seq_len, self.inter_sup, self.is_high, self.out_normalize)
+        self.foutput_dim, self.feat_ratio = 128, 8
+        self.hdim, self.cdim = (128 if self.is_high else 64), 32
+        C, r, hd, cd = self.foutput_dim, self.feat_ratio, self.hdim, self.cdim
+        # registration order == reference state_dict order
+        self.fnet = ResNetEncoder(out_chs=C, stride=r)
+        self.depth_head = DepthHead(input_dim=C, hidden_dim=C, scale=False)
+        self.pose_head = PoseHead(input_dim=2 * C, hidden_dim=C)
+        self.upmask_net = UpMaskNet(hidden_dim=C, ratio=r)
+        self.update_block_depth = BasicUpdateBlockDepth(hidden_dim=hd, cost_dim=C, ratio=r, context_dim=cd)
+        self.update_block_pose = BasicUpdateBlockPose(hidden_dim=hd, cost_dim=C, context_dim=cd)
+        # `cnet` is constructed but never used by the reference forward (DepthPoseNet.py:58
+        # vs :107-205); it is kept only so reference checkpoints load.
+        self.cnet = ResNetEncoder(out_chs=C, stride=r)
+        self.cnet_depth = ResNetEncoder(out_chs=hd + cd, stride=r, num_input_images=1)
+        self.cnet_pose = ResNetEncoder(out_chs=hd + cd, stride=r, num_input_images=2)
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def depth_mode(self):
+        return hip.DEPTH_DISP if self.out_normalize else hip.DEPTH_INV
+
+    def scale_inv_depth(self, disp):
+        """disp_to_depth(...)[0] when 'out' is in the version, else identity."""
+        if not self.out_normalize:
+            return disp
+        lo, hi = 1.0 / self.max_depth, 1.0 / self.min_depth
+        return lo + (hi - lo) * disp
+
+    def upsample_depth(self, depth, mask, ratio=8):
+        """Convex upsampling (DepthPoseNet.py:63-74), one HIP launch."""
+        return hip.convex_upsample(depth, mask, ratio)
+
+    def _cost(self, fmap1, frefs, disp, poses, K, reduce_mean):
+        return hip.warp_cost(fmap1, frefs, disp, poses, K, depth_mode=self.depth_mode,
+                             min_depth=self.min_depth, max_depth=self.max_depth,
+                             scale=1.0 / self.feat_ratio, reduce_mean=reduce_mean)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, target_image, ref_imgs, intrinsics):
+        B, N = target_image.shape[0], len(ref_imgs)
+        C, hd, cd = self.foutput_dim, self.hdim, self.cdim
+        K = intrinsics.float().contiguous()
+
+        fmaps = self.fnet(torch.cat([target_image] + list(ref_imgs), 0))
+        assert target_image.shape[2] // fmaps.shape[2] == self.feat_ratio
+        h, w = fmaps.shape[2:]
+        fmap1 = fmaps[:B]
+        frefs = fmaps[B:].view(N, B, C, h, w)           # free view: all refs, one tensor
+
+        # initial poses of all refs in one pass: cat([fmap1, fmap_ref_j]) per ref j
+        pair = torch.cat([fmap1.unsqueeze(0).expand(N, B, C, h, w), frefs], 2).view(N * B, 2 * C, h, w)
+        poses = self.pose_head(pair).view(N, B, 6)
+
+        disp = self.depth_head(fmap1, act_fn=torch.sigmoid)
+        inv_preds = [self.scale_inv_depth(self.upsample_depth(disp, self.upmask_net(fmap1),
+                                                              self.feat_ratio))]
+        pose_preds = [poses]
+
+        if self.iters > 0:
+            ctx_d = self.cnet_depth(target_image)
+            h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
+            pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
+                               torch.stack(list(ref_imgs))], 2).flatten(0, 1)
+            ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
+            h_p, x_p = torch.tanh(ctx_p[:, :hd]), torch.relu(ctx_p[:, hd:hd + cd])
+
+        for _ in range(self.iters):
+            disp = disp.detach()
+            poses = poses.detach()
+            frozen_poses = poses
+            depth_cost = lambda d: self._cost(fmap1, frefs, d, frozen_poses, K, True)
+            h_d, masks, disps = self.update_block_depth(h_d, depth_cost, disp, x_d,
+                                                        seq_len=self.seq_len)
+            keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
+            for k in keep:
+                inv_preds.append(self.scale_inv_depth(
+                    self.upsample_depth(disps[k], masks[k], self.feat_ratio)))
+
+            # pose block over all N refs at once; depth frozen at this outer step
+            frozen_disp = disp
+            pose_cost = lambda q: self._cost(fmap1, frefs, frozen_disp, q.view(N, B, 6), K,
+                                             False).view(N * B, C, h, w)
+            h_p, seq = self.update_block_pose(h_p, pose_cost, poses.reshape(N * B, 6), x_p,
+                                              seq_len=self.seq_len)
+            seq = seq if self.inter_sup else [seq[-1]]
+            pose_preds.extend(q.view(N, B, 6) for q in seq)
+            disp, poses = disps[-1], seq[-1].view(N, B, 6)
+
+        if not self.training:
+            return inv_preds[-1], pose_preds[-1].permute(1, 0, 2)          # [B,N,6]
+        return inv_preds, torch.stack(pose_preds, 2).permute(1, 0, 2, 3)  # [B,N,n_pred,6]

@@ -1,0 +1,88 @@
+"""ResNet-18 trunk (layers 1-3) with the stride-8 fusion head.
+
+State-dict compatible with the reference ResNetEncoder
+(dro_sfm/networks/optim/extractor.py:7-107): conv1/bn1, layer1..layer3 of
+BasicBlocks (conv1/bn1/conv2/bn2[/downsample.0,1]), upconv1.0,
+upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  The convolutions run on
+MIOpen (SURVEY.md §8(f) ranks a fused encoder as the next step); pretrained
+ImageNet weights are never downloaded -- load a checkpoint instead.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
+                                            nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        y = self.bn2(self.conv2(y))
+        skip = x if self.downsample is None else self.downsample(x)
+        return F.relu(y + skip, inplace=True)
+
+
+def _stage(cin, cout, stride):
+    return nn.Sequential(BasicBlock(cin, cout, stride), BasicBlock(cout, cout, 1))
+
+
+class ResNetEncoder(nn.Module):
+    """Feature/context encoder; input [B, 3*num_input_images, H, W] or a list
+    of such tensors (batched along dim 0, split back on return)."""
+
+    def __init__(self, num_layers=18, num_input_images=1, pretrained=False, out_chs=32, stride=8):
+        super().__init__()
+        if num_layers != 18:
+            raise NotImplementedError("only the ResNet-18 trunk is used by DepthPoseNet")
+        if stride not in (4, 8):
+            raise NotImplementedError("stride must be 4 or 8 (extractor.py:28-41)")
+        self.stride = stride
+        self.conv1 = nn.Conv2d(3 * num_input_images, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = _stage(64, 64, 1)
+        self.layer2 = _stage(64, 128, 2)
+        self.layer3 = _stage(128, 256, 2)
+        self.upconv1 = nn.Sequential(nn.Conv2d(256, 128, 3, 1, 1), nn.ReLU(inplace=True))
+        self.upconv1_fusion = nn.Sequential(nn.Conv2d(256, 128, 3, 1, 1), nn.ReLU(inplace=True))
+        if stride == 4:
+            self.upconv2 = nn.Sequential(nn.Conv2d(128, 64, 3, 1, 1), nn.ReLU(inplace=True))
+            self.upconv2_fusion = nn.Sequential(nn.Conv2d(128, 64, 3, 1, 1), nn.ReLU(inplace=True))
+            self.out_conv = nn.Conv2d(64, out_chs, 3, 1, 1)
+        else:
+            self.out_conv = nn.Conv2d(128, out_chs, 3, 1, 1)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        chunks = None
+        if isinstance(x, (list, tuple)):
+            chunks = len(x)
+            x = torch.cat(list(x), 0)
+        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x)), inplace=True), 3, 2, 1)
+        s4 = self.layer1(x)
+        s8 = self.layer2(s4)
+        x = self.layer3(s8)
+        x = self.upconv1(F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False))
+        x = self.upconv1_fusion(torch.cat([x, s8], 1))
+        if self.stride == 4:
+            x = self.upconv2(F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False))
+            x = self.upconv2_fusion(torch.cat([x, s4], 1))
+        x = self.out_conv(x)
+        if chunks is not None:
+            return torch.chunk(x, chunks, 0)
+        return x

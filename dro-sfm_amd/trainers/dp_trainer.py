@@ -1,0 +1,230 @@
+"""Data-parallel training over RCCL (replaces the reference's Horovod path).
+
+Reference: HorovodTrainer (dro_sfm/trainers/horovod_trainer.py:14-127) with
+hvd.DistributedOptimizer commented out (:67-69) and world_size pinned to 1
+(:40-50) -- data parallelism is dormant there.  This module
+provides it MI355X-first:
+
+  * one process per GPU (torchrun), backend "nccl" == RCCL over xGMI;
+  * every gradient lives in ONE flat fp32 buffer (param.grad are views into
+    it), cut into ~bucket_mb buckets in reverse registration order -- the order
+    backward produces them;
+  * a post-accumulate hook per parameter counts arrivals per bucket; a full
+    bucket's all-reduce is issued immediately (async), so communication of
+    late layers overlaps backward of early ones;
+  * parameters that never receive a gradient (DepthPoseNet.cnet, dead in the
+    reference forward) are discovered on the first step and left out;
+  * initial parameters and buffers are broadcast from rank 0 (BatchNorm keeps
+    per-replica batch statistics, as the reference: no SyncBN).
+
+The step order matches HorovodTrainer.train: zero_grad -> forward -> loss ->
+backward -> (all-reduce) -> Adam step.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_distributed(backend=None):
+    """Initialise the default process group from torchrun's env (no-op for 1 rank).
+    Returns (rank, world_size, local_rank)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local
+
+
+class GradBuckets:
+    """Flat gradient storage + bucketed, backward-overlapped all-reduce."""
+
+    def __init__(self, params, bucket_mb=25.0, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.params = [p for p in params if p.requires_grad]
+        if any(p.dtype != torch.float32 for p in self.params):
+            raise RuntimeError("GradBuckets: fp32 parameters only")
+        self.flat = torch.zeros(sum(p.numel() for p in self.params), device=self.params[0].device)
+        self.offsets, off = {}, 0
+        for p in self.params:
+            self.offsets[p] = off
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.bucket_bytes = int(bucket_mb * 1024 * 1024)
+        self.active = None            # params that receive gradients (learned on step 1)
+        self.buckets, self._pending, self._seen = [], [], set()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def _build(self, active):
+        self.active = [p for p in self.params if p in active]
+        self.buckets, cur, nbytes = [], [], 0
+        for p in reversed(self.active):                     # the order backward finishes them
+            cur.append(p)
+            nbytes += p.numel() * 4
+            if nbytes >= self.bucket_bytes:
+                self.buckets.append(cur)
+                cur, nbytes = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b}
+        self._need = [len(b) for b in self.buckets]
+
+    def _slice(self, bucket):
+        """One contiguous flat slice covering a bucket (slots of inactive params
+        inside it are zeros and reduce harmlessly)."""
+        lo = min(self.offsets[p] for p in bucket)
+        hi = max(self.offsets[p] + p.numel() for p in bucket)
+        return self.flat[lo:hi]
+
+    def _on_grad(self, p):
+        if self.active is None:
+            self._seen.add(p)
+            return
+        b = self._bucket_of.get(p)
+        if b is None:
+            return
+        self._left[b] -= 1
+        if self._left[b] == 0 and self.world > 1:
+            self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
+                                                 group=self.group, async_op=True))
+
+    def zero(self):
+        self.flat.zero_()
+        self._pending = []
+        if self.active is not None:
+            self._left = list(self._need)
+
+    def finish(self):
+        """Complete every bucket's all-reduce and average over ranks."""
+        if self.active is None:
+            seen = self._seen
+            if self.world > 1:
+                flags = torch.tensor([float(p in seen) for p in self.params], device=self.flat.device)
+                dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
+                seen = {p for p, f in zip(self.params, flags.tolist()) if f > 0}
+            self._build(seen)
+            if self.world > 1:                               # step 1: reduce synchronously
+                for b in self.buckets:
+                    dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            for work in self._pending:
+                work.wait()
+            self._pending = []
+        if self.world > 1:
+            self.flat.div_(self.world)
+
+
+def broadcast_module(module, src=0, group=None):
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
+class DataParallelTrainer:
+    """fit()-less step driver: `loss, metrics = trainer.step(batch)`.
+
+    `model(batch)` must return a dict with a 'loss' tensor (the SfmModelMF
+    family does).  Adam with the reference's lr (configs/*.yaml: 2e-4).
+    `capturable=True` keeps Adam's step counters on the device so the whole
+    step can be replayed from a hipGraph (GraphedTrainStep)."""
+
+    def __init__(self, model, lr=2e-4, bucket_mb=25.0, group=None, betas=(0.9, 0.999), eps=1e-8,
+                 capturable=False):
+        self.model = model
+        broadcast_module(model, 0, group)
+        self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb, group=group)
+        self.optimizer = torch.optim.Adam(self.grads.params, lr=lr, betas=betas, eps=eps,
+                                          foreach=True, capturable=capturable)
+
+    def _step_inner(self, batch, **fwd_kw):
+        self.grads.zero()
+        out = self.model(batch, **fwd_kw)
+        loss = out["loss"]
+        loss.sum().backward()
+        self.grads.finish()
+        self.optimizer.step()
+        return loss.detach(), out.get("metrics", {})
+
+    def step(self, batch, **fwd_kw):
+        self.model.train()
+        return self._step_inner(batch, **fwd_kw)
+
+
+def _clone_batch(batch):
+    out = {}
+    for k, v in batch.items():
+        if torch.is_tensor(v):
+            out[k] = v.clone()
+        elif isinstance(v, (list, tuple)) and v and torch.is_tensor(v[0]):
+            out[k] = [t.clone() for t in v]
+        else:
+            out[k] = v
+    return out
+
+
+def _copy_batch(dst, src):
+    for k, v in src.items():
+        if k not in dst:
+            continue
+        if torch.is_tensor(v):
+            dst[k].copy_(v, non_blocking=True)
+        elif isinstance(v, (list, tuple)) and v and torch.is_tensor(v[0]):
+            for d, s_ in zip(dst[k], v):
+                d.copy_(s_, non_blocking=True)
+
+
+class GraphedTrainStep:
+    """The whole training step -- zero -> forward -> loss -> backward -> RCCL
+    all-reduce -> Adam -- captured once into a hipGraph per branch of the
+    random left-right flip (SfmModelMF.py:110), then replayed: no Python
+    dispatch and no launch gaps in the steady state.
+
+    The batch is copied into static device buffers before each replay; the
+    intrinsics are restored from `intrinsics_ref` INSIDE the graph because the
+    flip branch mutates them in place (as the reference does).
+    The first eager steps (bucket discovery, MIOpen algorithm selection) run
+    before capture on a side stream and are real training steps.
+    """
+
+    def __init__(self, trainer, example_batch, warmup=3, flips=(False, True)):
+        self.tr = trainer
+        self.model = trainer.model
+        self.static = _clone_batch(example_batch)
+        self.static["intrinsics_ref"] = example_batch["intrinsics"].clone()
+        self.model.train()
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for i in range(max(warmup, len(flips))):
+                self._body(flips[i % len(flips)])
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs = {}
+        for f in flips:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                out = self._body(f)
+            self.graphs[f] = (g, out)
+        torch.cuda.synchronize()
+
+    def _body(self, flip):
+        self.static["intrinsics"].copy_(self.static["intrinsics_ref"])
+        return self.tr._step_inner(self.static, flip=flip)
+
+    def step(self, batch, flip=None):
+        _copy_batch(self.static, {k: v for k, v in batch.items() if k != "intrinsics"})
+        self.static["intrinsics_ref"].copy_(batch["intrinsics"], non_blocking=True)
+        if flip is None:
+            flip = self.model._rng.random() < self.model.flip_lr_prob
+        g, out = self.graphs[bool(flip)]
+        g.replay()
+        return out

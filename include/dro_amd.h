@@ -1,0 +1,139 @@
+/*
+ * dro_amd.h -- C ABI of the MI355X (gfx950) hot-path library libdro_amd.so.
+ *
+ * The reference (xyang9527/dro-sfm) is pure Python/PyTorch; every hot-path op
+ * there is a chain of stock ATen kernels.  Each entry point below replaces one
+ * such chain with hand-written HIP for CDNA4 and is bound from Python by
+ * dro-sfm_amd/hip/_lib.py (ctypes).  Conventions shared by every function:
+ *
+ *   * plain device pointers (fp32, dense NCHW / row-major, caller allocated);
+ *     the library never allocates or frees; outputs are fully overwritten;
+ *   * `stream` is a hipStream_t passed as void* (NULL = default stream); all
+ *     work is enqueued asynchronously on it and is hipGraph-capturable (no
+ *     host synchronisation, no allocation, memsets are async on `stream`);
+ *   * return value: 0 on success, a negative DRO_E_* code for an invalid
+ *     argument (nothing is launched), or a positive hipError_t from the launch.
+ *     dro_last_error() returns a static message for the last failure on the
+ *     calling thread.
+ *
+ * Pose encodings (pose_mode):
+ *   DRO_POSE_EULER  : 6 floats per pose  [tx,ty,tz, rx,ry,rz], R = Rx*Ry*Rz
+ *                     (geometry/pose_utils.py:40-85, Pose.from_vec pose.py:38-45)
+ *   DRO_POSE_MATRIX : 12 floats per pose, row-major [R | t] (the top 3 rows of
+ *                     a Pose.mat [4,4], geometry/pose.py:7-98)
+ * Depth encodings (depth_mode) for the target depth map:
+ *   DRO_DEPTH_METRIC  : metric depth as given
+ *   DRO_DEPTH_INV     : inverse depth; depth = inv2depth(x) (utils/depth.py:102-121)
+ *   DRO_DEPTH_DISP    : sigmoid disparity; depth = inv2depth(disp_to_depth(x)[0])
+ *                       (networks/layers/resnet/layers.py:11-20), using min_disp/max_disp
+ */
+#ifndef DRO_AMD_H
+#define DRO_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRO_POSE_EULER 0
+#define DRO_POSE_MATRIX 1
+
+#define DRO_DEPTH_METRIC 0
+#define DRO_DEPTH_INV 1
+#define DRO_DEPTH_DISP 2
+
+#define DRO_OK 0
+#define DRO_E_NULL (-1)     /* a required pointer is NULL            */
+#define DRO_E_SHAPE (-2)    /* a size is out of the supported range  */
+#define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
+
+const char* dro_last_error(void);
+int dro_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * Inverse warp + feature cost.
+ * Replaces DepthPoseNet.get_cost_each (networks/depth_pose/DepthPoseNet.py:76-96)
+ * and, with reduce_mean=1 over N refs, DepthPoseNet.depth_cost_calc (:98-105):
+ *   Camera(K).scaled(scale).reconstruct(depth) -> Camera(ref_K, Tcw=pose)
+ *   .scaled(scale).project(normalize=True) -> grid_sample(bilinear, zeros,
+ *   align_corners=True) -> (fmap - warped)^2
+ *   fmap [B,C,h,w]; fmap_ref [N,B,C,h,w]; depth [B,1,h,w]; K, ref_K [B,3,3];
+ *   pose [N,B,6|12]; cost [B,C,h,w] (reduce_mean) or [N,B,C,h,w].
+ * scale == 1.0f leaves K untouched (Camera.scaled returns self, camera.py:103-104).
+ * ---------------------------------------------------------------------- */
+int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, const float* depth,
+                          int depth_mode, float min_disp, float max_disp,
+                          const float* K, const float* ref_K, float scale,
+                          const float* pose, int pose_mode,
+                          int B, int N, int C, int h, int w, int reduce_mean,
+                          float* cost, void* stream);
+
+size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w);
+
+/* Gradients of sum(cost * grad_cost).  Any grad_* may be NULL (not computed).
+ * grad_depth is w.r.t. the depth input in its depth_mode encoding; grad_pose
+ * is w.r.t. the pose input in its pose_mode encoding.  `workspace` must hold
+ * dro_warp_cost_workspace_bytes() bytes when grad_depth or grad_pose is set. */
+int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float* depth,
+                           int depth_mode, float min_disp, float max_disp,
+                           const float* K, const float* ref_K, float scale,
+                           const float* pose, int pose_mode,
+                           int B, int N, int C, int h, int w, int reduce_mean,
+                           const float* grad_cost, float* grad_fmap, float* grad_fmap_ref,
+                           float* grad_depth, float* grad_pose, void* workspace, void* stream);
+
+/* D fronto-parallel hypothesis planes (SURVEY.md §8(d) measurement extension):
+ * for each plane d, depth = inv2depth(disp_to_depth(disp[d])) everywhere and
+ * cost[b,d] = get_cost_each(pose, fmap, fmap_ref, depth).  disp [D] (device);
+ * pose [B,6|12]; cost [B,D,C,h,w]. */
+int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref, const float* disp, int D,
+                            float min_disp, float max_disp, const float* K, const float* ref_K,
+                            float scale, const float* pose, int pose_mode,
+                            int B, int C, int h, int w, float* cost, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Multi-view photometric decay loss + edge-aware smoothness.
+ * Replaces MultiViewPhotometricDecayLoss.forward
+ * (losses/multiview_photometric_loss_mf.py:303-361) with clip_loss == 0 and
+ * padding_mode 'zeros': view_synthesis (geometry/camera_utils.py:23-56), SSIM
+ * (:15-54), L1, automask (:346-351), min/mean reduce and 0.85^(n-i-1) decay
+ * (:231-269), calc_smoothness (utils/depth.py:166-199) (:273-299).
+ *   image [B,3,H,W]; context [N,B,3,H,W]; inv_depths [n,B,1,H,W];
+ *   K, ref_K [B,3,3] (scaled by DW/W = 1 -> unscaled); pose [N,n,B,6|12].
+ *   out [3] = {loss, photometric_loss metric, smoothness_loss metric}.
+ * `workspace` (dro_photometric_workspace_bytes) carries the forward state the
+ * backward needs; keep it alive and unmodified in between. */
+size_t dro_photometric_workspace_bytes(int B, int N, int n, int H, int W);
+
+int dro_photometric_forward(const float* image, const float* context, const float* inv_depths,
+                            const float* K, const float* ref_K, const float* pose, int pose_mode,
+                            int B, int N, int n, int H, int W,
+                            float ssim_w, float C1, float C2, float smooth_w,
+                            int automask, int reduce_min,
+                            float* out, void* workspace, void* stream);
+
+/* grad_out: device pointer to d(total)/d(loss) (1 float).  Writes
+ * grad_inv_depths [n,B,1,H,W] and (if non-NULL) grad_pose [N,n,B,6|12]. */
+int dro_photometric_backward(const float* image, const float* context, const float* inv_depths,
+                             const float* K, const float* ref_K, const float* pose, int pose_mode,
+                             int B, int N, int n, int H, int W,
+                             float ssim_w, float C1, float C2, float smooth_w,
+                             int automask, int reduce_min,
+                             const float* grad_out, float* grad_inv_depths, float* grad_pose,
+                             void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Convex 8x upsampling: DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74).
+ *   inv [B,1,h,w]; mask [B,9*r*r,h,w] -> out [B,1,h*r,w*r]
+ * ---------------------------------------------------------------------- */
+int dro_convex_upsample_forward(const float* inv, const float* mask, int B, int h, int w,
+                                int ratio, float* out, void* stream);
+int dro_convex_upsample_backward(const float* inv, const float* mask, const float* grad_out,
+                                 int B, int h, int w, int ratio,
+                                 float* grad_inv, float* grad_mask, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRO_AMD_H */

@@ -1,0 +1,433 @@
+"""CPU ORACLE for the DRO-SfM hot path -- TEST INFRASTRUCTURE ONLY.
+
+A functional fp32 restatement, in plain PyTorch CPU ops, of the reference's
+algorithms on the hot path.  Every function cites the
+reference file:line it restates.  It is pinned against the golden vectors in
+tests/golden/*.npz, which were produced by running the reference itself
+(tests/golden/gen_golden.py) -- see tests/test_oracle_golden.py.
+
+Who may import this module: tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg -- as the CHECKER / CPU baseline only.  The product package
+(dro-sfm_amd/) never imports it and has no CPU path.
+
+Networks are expressed over a flat parameter dict keyed exactly like the
+reference DepthPoseNet.state_dict(), so any implementation
+that keeps those keys can be compared weight-for-weight.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+# ============================================================================ geometry
+def euler_to_matrix(vec):
+    """pose_vec2mat(mode='euler') (geometry/pose_utils.py:40-85): [B,6] -> R [B,3,3], t [B,3].
+
+    R = Rx(rx) @ Ry(ry) @ Rz(rz) with vec = [tx, ty, tz, rx, ry, rz].
+    """
+    t = vec[:, :3]
+    rx, ry, rz = vec[:, 3], vec[:, 4], vec[:, 5]
+    one, zero = torch.ones_like(rx), torch.zeros_like(rx)
+
+    def m(*rows):
+        return torch.stack([torch.stack(r, -1) for r in rows], -2)
+
+    cx, sx, cy, sy, cz, sz = rx.cos(), rx.sin(), ry.cos(), ry.sin(), rz.cos(), rz.sin()
+    Rx = m((one, zero, zero), (zero, cx, -sx), (zero, sx, cx))
+    Ry = m((cy, zero, sy), (zero, one, zero), (-sy, zero, cy))
+    Rz = m((cz, -sz, zero), (sz, cz, zero), (zero, zero, one))
+    return Rx @ Ry @ Rz, t
+
+
+def pose_to_rt(pose):
+    """Accept an euler vector [B,6] or a transform [B,3|4,4]; return (R, t)."""
+    if pose.dim() == 2 and pose.shape[-1] == 6:
+        return euler_to_matrix(pose)
+    return pose[:, :3, :3], pose[:, :3, 3]
+
+
+def vec_to_transform(vec):
+    """Pose.from_vec (geometry/pose.py:38-45): [B,6] -> [B,4,4]."""
+    R, t = euler_to_matrix(vec)
+    T = torch.eye(4, dtype=vec.dtype).repeat(vec.shape[0], 1, 1)
+    T = torch.cat([torch.cat([R, t.unsqueeze(-1)], -1), T[:, 3:]], 1)
+    return T
+
+
+def scale_K(K, s):
+    """Camera.scaled -> scale_intrinsics (geometry/camera.py:83-107, camera_utils.py:13-19)."""
+    if s == 1.0:
+        return K
+    K = K.clone()
+    K[:, 0, 0] = K[:, 0, 0] * s
+    K[:, 1, 1] = K[:, 1, 1] * s
+    K[:, 0, 2] = (K[:, 0, 2] + 0.5) * s - 0.5
+    K[:, 1, 2] = (K[:, 1, 2] + 0.5) * s - 0.5
+    return K
+
+
+def invert_K(K):
+    """Camera.Kinv (geometry/camera.py:70-79): K.clone() with the pinhole entries inverted."""
+    Ki = K.clone()
+    Ki[:, 0, 0] = 1.0 / K[:, 0, 0]
+    Ki[:, 1, 1] = 1.0 / K[:, 1, 1]
+    Ki[:, 0, 2] = -1.0 * K[:, 0, 2] / K[:, 0, 0]
+    Ki[:, 1, 2] = -1.0 * K[:, 1, 2] / K[:, 1, 1]
+    return Ki
+
+
+def inv2depth(inv):
+    """utils/depth.py:102-121: 1/clamp(inv, 1e-6), zero where inv <= 0."""
+    d = 1.0 / inv.clamp(min=1e-6)
+    return torch.where(inv <= 0.0, torch.zeros_like(d), d)
+
+
+def disp_to_depth(disp, min_depth, max_depth):
+    """networks/layers/resnet/layers.py:11-20 -> scaled disparity (first output)."""
+    lo, hi = 1.0 / max_depth, 1.0 / min_depth
+    return lo + (hi - lo) * disp
+
+
+def sample_grid(depth, K, ref_K, pose, scale):
+    """Camera.reconstruct -> Camera(ref_K, Tcw=pose).project(normalize=True)
+    (geometry/camera.py:111-194) as a grid_sample grid [B,h,w,2]."""
+    B, _, h, w = depth.shape
+    Kt, Kr = scale_K(K.to(depth.dtype), scale), scale_K(ref_K.to(depth.dtype), scale)
+    ys, xs = torch.meshgrid(torch.arange(h, dtype=depth.dtype), torch.arange(w, dtype=depth.dtype),
+                            indexing="ij")
+    pix = torch.stack([xs, ys, torch.ones_like(xs)], 0).reshape(1, 3, -1).expand(B, 3, h * w)
+    rays = invert_K(Kt).bmm(pix)                     # [B,3,hw]
+    X = rays * depth.reshape(B, 1, h * w)            # identity Tcw -> world == camera
+    R, t = pose_to_rt(pose)
+    P = R.bmm(X) + t.unsqueeze(-1)
+    x = Kr.bmm(P)
+    Z = x[:, 2].clamp(min=1e-5)
+    u = 2 * (x[:, 0] / Z) / (w - 1) - 1.0
+    v = 2 * (x[:, 1] / Z) / (h - 1) - 1.0
+    return torch.stack([u, v], -1).reshape(B, h, w, 2)
+
+
+def get_cost_each(pose, fmap, fmap_ref, depth, K, ref_K, scale):
+    """DepthPoseNet.get_cost_each (networks/depth_pose/DepthPoseNet.py:76-96)."""
+    grid = sample_grid(depth, K, ref_K, pose, scale)
+    warped = F.grid_sample(fmap_ref, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+    return (fmap - warped) ** 2
+
+
+def depth_cost_calc(inv_scaled, fmap, fmaps_ref, poses, K, ref_K, scale):
+    """DepthPoseNet.depth_cost_calc (DepthPoseNet.py:98-105): mean over refs."""
+    depth = inv2depth(inv_scaled)
+    costs = [get_cost_each(p, fmap, f, depth, K, ref_K, scale) for p, f in zip(poses, fmaps_ref)]
+    return torch.stack(costs, 1).mean(1)
+
+
+def view_synthesis(ref_image, depth, pose, K, ref_K):
+    """geometry/camera_utils.py:23-56 at full resolution (scale 1)."""
+    grid = sample_grid(depth, K, ref_K, pose, 1.0)
+    return F.grid_sample(ref_image, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+
+
+def convex_upsample(inv, mask, r=8):
+    """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74)."""
+    B, _, h, w = inv.shape
+    wts = torch.softmax(mask.reshape(B, 9, r, r, h, w), dim=1)
+    taps = F.unfold(inv, [3, 3], padding=1).reshape(B, 9, 1, 1, h, w)
+    up = (wts * taps).sum(1)                         # [B,r,r,h,w]
+    return up.permute(0, 3, 1, 4, 2).reshape(B, 1, h * r, w * r)
+
+
+# ============================================================================ losses
+def ssim(x, y, C1=1e-4, C2=9e-4):
+    """SSIM with 3x3 mean pooling over a reflection-padded image
+    (losses/multiview_photometric_loss_mf.py:15-54)."""
+    x, y = F.pad(x, (1, 1, 1, 1), mode="reflect"), F.pad(y, (1, 1, 1, 1), mode="reflect")
+    pool = lambda z: F.avg_pool2d(z, 3, stride=1)
+    mx, my = pool(x), pool(y)
+    mxy, mxx, myy = mx * my, mx.pow(2), my.pow(2)
+    sx, sy, sxy = pool(x.pow(2)) - mxx, pool(y.pow(2)) - myy, pool(x * y) - mxy
+    num = (2 * mxy + C1) * (2 * sxy + C2)
+    den = (mxx + myy + C1) * (sx + sy + C2)
+    return num / den
+
+
+def photometric_map(est, tgt, ssim_w, C1, C2):
+    """calc_photometric_loss (multiview_photometric_loss_mf.py:194-229), clip_loss == 0."""
+    l1 = (est - tgt).abs()
+    if ssim_w <= 0.0:
+        return l1
+    s = torch.clamp((1.0 - ssim(est, tgt, C1, C2)) / 2.0, 0.0, 1.0)
+    return ssim_w * s.mean(1, True) + (1 - ssim_w) * l1.mean(1, True)
+
+
+def smoothness(inv_depths, image, smooth_w):
+    """calc_smoothness_loss (multiview_photometric_loss_mf.py:273-299; utils/depth.py:147-199)."""
+    n = len(inv_depths)
+    wx = torch.exp(-(image[..., :-1] - image[..., 1:]).abs().mean(1, True))
+    wy = torch.exp(-(image[..., :-1, :] - image[..., 1:, :]).abs().mean(1, True))
+    total = 0.0
+    for i, d in enumerate(inv_depths):
+        dn = d / d.mean(2, True).mean(3, True).clamp(min=1e-6)
+        sx = (dn[..., :-1] - dn[..., 1:]) * wx
+        sy = (dn[..., :-1, :] - dn[..., 1:, :]) * wy
+        total = total + (sx.abs().mean() + sy.abs().mean()) / 2 ** i
+    return smooth_w * (total / n)
+
+
+def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_w=0.85, C1=1e-4,
+                           C2=9e-4, smooth_w=0.001, automask=True, reduce="min"):
+    """MultiViewPhotometricDecayLoss.forward (multiview_photometric_loss_mf.py:303-361).
+
+    context: list of N [B,3,H,W]; inv_depths: list of n [B,1,H,W] (full res);
+    poses[j][i]: euler [B,6] or transform [B,4,4] for ref j, prediction i.
+    """
+    n = len(inv_depths)
+    per_pred = [[] for _ in range(n)]
+    for j, ref in enumerate(context):
+        for i in range(n):
+            est = view_synthesis(ref, inv2depth(inv_depths[i]), poses[j][i], K, ref_K)
+            per_pred[i].append(photometric_map(est, image, ssim_w, C1, C2))
+        if automask:
+            unwarped = photometric_map(ref, image, ssim_w, C1, C2)
+            for i in range(n):
+                per_pred[i].append(unwarped)
+    photo = 0.0
+    for i in range(n):
+        maps = per_pred[i]
+        if reduce == "min":
+            li = torch.cat(maps, 1).min(1, True)[0].mean()
+        else:
+            li = sum(m.mean() for m in maps) / len(maps)
+        photo = photo + 0.85 ** (n - i - 1) * li
+    if smooth_w > 0:
+        smooth = smoothness(inv_depths, image, smooth_w)
+        loss = photo + smooth
+        # reference quirk: the stored metric is a detached ALIAS of the loss that
+        # the in-place `loss += smoothness` then mutates (:268, :356), so the
+        # 'photometric_loss' metric reports the total loss.
+        photo_metric = loss.detach()
+    else:
+        smooth, loss, photo_metric = torch.zeros(()), photo, photo.detach()
+    return {"loss": loss.reshape(1), "photometric_loss": photo_metric,
+            "smoothness_loss": smooth.detach()}
+
+
+def supervised_depth_pose_loss(inv_depths, gt_inv, gt_poses, poses, K, ref_K, min_depth,
+                               max_depth):
+    """SupervisedDepthPoseLoss.forward (losses/supervised_loss.py:244-371), sparse-l1."""
+    n = len(inv_depths)
+    lo, hi = 1.0 / max_depth, 1.0 / min_depth
+    # depth term (:244-277)
+    tl, tw = 0.0, 0.0
+    for i in range(n):
+        wgt = 0.85 ** (n - i - 1)
+        tw += wgt
+        valid = ((gt_inv > lo) & (gt_inv < hi)).squeeze(1)
+        tl = tl + wgt * torch.mean(valid * (gt_inv - inv_depths[i]).abs().squeeze(1))
+    depth_loss = tl / tw
+    # pose term (:279-325): reprojection of gt depth under gt vs predicted pose
+    gt_depth = inv2depth(gt_inv)
+    dmask = ((gt_depth > min_depth) & (gt_depth < max_depth / 4.0)).permute(0, 2, 3, 1)
+    pl, pw = 0.0, 0.0
+    for i in range(n):
+        wgt = 0.85 ** (n - i - 1)
+        pw += wgt
+        li = 0.0
+        for j, gtp in enumerate(gt_poses):
+            cg = sample_grid(gt_depth, K, ref_K, gtp, 1.0)
+            cp = sample_grid(gt_depth, K, ref_K, poses[j][i], 1.0)
+            valid = ((cg >= -1) & (cg <= 1)) * ((cp >= -1) & (cp <= 1)) * dmask
+            li = li + torch.mean(valid * (cp - cg).abs().clamp(-1, 1))
+        pl = pl + (li / len(gt_poses)) * wgt
+    pose_loss = pl / pw
+    loss = depth_loss + pose_loss
+    return {"loss": loss.reshape(1), "depth_loss": depth_loss.detach(),
+            "pose_loss": pose_loss.detach(), "all_loss": loss.detach()}
+
+
+# ============================================================================ network (functional)
+def _conv(p, name, x, stride=1, padding=0):
+    return F.conv2d(x, p[name + ".weight"], p.get(name + ".bias"), stride=stride, padding=padding)
+
+
+def _bn(p, name, x, training):
+    return F.batch_norm(x, p[name + ".running_mean"], p[name + ".running_var"], p[name + ".weight"],
+                        p[name + ".bias"], training=training, momentum=0.1, eps=1e-5)
+
+
+def resnet_encoder(p, pre, x, training, stride=8):
+    """ResNetEncoder.forward (networks/optim/extractor.py:67-107) on torchvision's
+    ResNet-18 layout (layer1..layer3, BasicBlocks) with the stride-8 fusion head."""
+    x = F.relu(_bn(p, pre + "bn1", _conv(p, pre + "conv1", x, 2, 3), training))
+    x = F.max_pool2d(x, 3, 2, 1)
+    feats = {}
+    for li, s in ((1, 1), (2, 2), (3, 2)):
+        for bi in range(2):
+            b = f"{pre}layer{li}.{bi}."
+            st = s if bi == 0 else 1
+            out = F.relu(_bn(p, b + "bn1", _conv(p, b + "conv1", x, st, 1), training))
+            out = _bn(p, b + "bn2", _conv(p, b + "conv2", out, 1, 1), training)
+            idt = x
+            if b + "downsample.0.weight" in p:
+                idt = _bn(p, b + "downsample.1", _conv(p, b + "downsample.0", x, st, 0), training)
+            x = F.relu(out + idt)
+        feats[li] = x
+    x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+    x = F.relu(_conv(p, pre + "upconv1.0", x, 1, 1))
+    x = F.relu(_conv(p, pre + "upconv1_fusion.0", torch.cat([x, feats[2]], 1), 1, 1))
+    if stride == 4:
+        x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+        x = F.relu(_conv(p, pre + "upconv2.0", x, 1, 1))
+        x = F.relu(_conv(p, pre + "upconv2_fusion.0", torch.cat([x, feats[1]], 1), 1, 1))
+    return _conv(p, pre + "out_conv", x, 1, 1)
+
+
+def sep_conv_gru(p, pre, h, x):
+    """SepConvGRU (networks/optim/update.py:47-74): 1x5 then 5x1 gated update."""
+    for sfx, pad in (("1", (0, 2)), ("2", (2, 0))):
+        hx = torch.cat([h, x], 1)
+        z = torch.sigmoid(_conv(p, pre + "convz" + sfx, hx, 1, pad))
+        r = torch.sigmoid(_conv(p, pre + "convr" + sfx, hx, 1, pad))
+        q = torch.tanh(_conv(p, pre + "convq" + sfx, torch.cat([r * h, x], 1), 1, pad))
+        h = (1 - z) * h + z * q
+    return h
+
+
+def depth_head(p, pre, x, act=torch.tanh):
+    """DepthHead (update.py:5-14)."""
+    return act(_conv(p, pre + "conv2", F.relu(_conv(p, pre + "conv1", x, 1, 1)), 1, 1))
+
+
+def pose_head(p, pre, x):
+    """PoseHead (update.py:16-28): spatial mean, rotation scaled by 0.01."""
+    o = _conv(p, pre + "conv2_pose", F.relu(_conv(p, pre + "conv1_pose", x, 1, 1)), 1, 1)
+    o = o.mean(3).mean(2)
+    return torch.cat([o[:, :3], 0.01 * o[:, 3:]], 1)
+
+
+def mask_head(p, pre, x):
+    """.25 * mask(x): 3x3 -> relu -> 1x1 to 9*r*r (update.py:150-153, :128-139)."""
+    return 0.25 * _conv(p, pre + "2", F.relu(_conv(p, pre + "0", x, 1, 1)), 1, 0)
+
+
+def projection_depth(p, pre, inv, cost):
+    """ProjectionInputDepth (update.py:77-99)."""
+    cor = F.relu(_conv(p, pre + "convc2", F.relu(_conv(p, pre + "convc1", cost)), 1, 1))
+    dfm = F.relu(_conv(p, pre + "convd2", F.relu(_conv(p, pre + "convd1", inv, 1, 3)), 1, 1))
+    out = F.relu(_conv(p, pre + "convd", torch.cat([cor, dfm], 1), 1, 1))
+    return torch.cat([out, inv], 1)
+
+
+def projection_pose(p, pre, pose, cost):
+    """ProjectionInputPose (update.py:102-124): pose broadcast to a constant map."""
+    B, _, h, w = cost.shape
+    pm = pose.reshape(B, 6, 1, 1).expand(B, 6, h, w)
+    cor = F.relu(_conv(p, pre + "convc2", F.relu(_conv(p, pre + "convc1", cost)), 1, 1))
+    pfm = F.relu(_conv(p, pre + "convp2", F.relu(_conv(p, pre + "convp1", pm, 1, 3)), 1, 1))
+    out = F.relu(_conv(p, pre + "convp", torch.cat([cor, pfm], 1), 1, 1))
+    return torch.cat([out, pm], 1)
+
+
+def update_block_depth(p, pre, net, cost_fn, inv, ctx, S, scale):
+    """BasicUpdateBlockDepth.forward (update.py:155-173)."""
+    invs, masks = [], []
+    for _ in range(S):
+        feat = projection_depth(p, pre + "encoder.", inv, cost_fn(scale(inv)))
+        net = sep_conv_gru(p, pre + "depth_gru.", net, torch.cat([ctx, feat], 1))
+        inv = inv + depth_head(p, pre + "depth_head.", net)
+        invs.append(inv)
+        masks.append(mask_head(p, pre + "mask.", net))
+    return net, masks, invs
+
+
+def update_block_pose(p, pre, net, cost_fn, pose, ctx, S):
+    """BasicUpdateBlockPose.forward (update.py:184-199)."""
+    seqs = []
+    for _ in range(S):
+        feat = projection_pose(p, pre + "encoder.", pose, cost_fn(pose))
+        net = sep_conv_gru(p, pre + "pose_gru.", net, torch.cat([ctx, feat], 1))
+        pose = pose + pose_head(p, pre + "pose_head.", net)
+        seqs.append(pose)
+    return net, seqs
+
+
+def parse_version(version):
+    """DepthPoseNet.__init__ version string (DepthPoseNet.py:22-34)."""
+    parts = version.split("-")
+    iters = int(parts[0].split("it")[1])
+    seq = 4
+    for s in parts:
+        if "seq" in s:
+            seq = int(s.split("seq")[1])
+    return dict(outer=iters // seq, seq=seq, hdim=128 if "h" in version else 64,
+                out_norm="out" in version, inter="inter" in version)
+
+
+def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=True):
+    """DepthPoseNet.forward (DepthPoseNet.py:107-205)."""
+    cfg = parse_version(version)
+    hd, cd, S = cfg["hdim"], 32, cfg["seq"]
+    scale = (lambda x: disp_to_depth(x, min_depth, max_depth)) if cfg["out_norm"] else (lambda x: x)
+    B, N = image.shape[0], len(refs)
+    fm = resnet_encoder(p, "fnet.", torch.cat([image] + refs, 0), training)
+    fmap1, frefs = fm[:B], [fm[B * (j + 1):B * (j + 2)] for j in range(N)]
+    poses = [pose_head(p, "pose_head.", torch.cat([fmap1, f], 1)) for f in frefs]
+    inv = depth_head(p, "depth_head.", fmap1, torch.sigmoid)
+    up = convex_upsample(inv, 0.25 * _conv(p, "upmask_net.mask.2",
+                                            F.relu(_conv(p, "upmask_net.mask.0", fmap1, 1, 1))), 8)
+    inv_preds, pose_preds = [scale(up)], [[q.clone() for q in poses]]
+    ctx_d = resnet_encoder(p, "cnet_depth.", image, training)
+    h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
+    ctx_p = resnet_encoder(p, "cnet_pose.", torch.cat([torch.cat([image, r], 1) for r in refs], 0),
+                           training)
+    h_p = [torch.tanh(ctx_p[B * j:B * (j + 1), :hd]) for j in range(N)]
+    x_p = [torch.relu(ctx_p[B * j:B * (j + 1), hd:hd + cd]) for j in range(N)]
+    for _ in range(cfg["outer"]):
+        inv = inv.detach()
+        poses = [q.detach() for q in poses]
+        depth_fixed = inv2depth(scale(inv))
+        cost_d = lambda x, ps=poses: depth_cost_calc(x, fmap1, frefs, ps, K, K, 1.0 / 8)
+        h_d, masks, invs = update_block_depth(p, "update_block_depth.", h_d, cost_d, inv, x_d, S,
+                                              scale)
+        sel = range(S) if cfg["inter"] else [S - 1]
+        for k in sel:
+            inv_preds.append(scale(convex_upsample(invs[k], masks[k], 8)))
+        inv = invs[-1]
+        new_poses = []
+        for j in range(N):
+            cost_p = lambda q, j=j: get_cost_each(q, fmap1, frefs[j], depth_fixed, K, K, 1.0 / 8)
+            h_p[j], seqs = update_block_pose(p, "update_block_pose.", h_p[j], cost_p, poses[j],
+                                             x_p[j], S)
+            new_poses.append(seqs if cfg["inter"] else [seqs[-1]])
+        for k in range(len(new_poses[0])):
+            pose_preds.append([new_poses[j][k].clone() for j in range(N)])
+        poses = [new_poses[j][-1] for j in range(N)]
+    if not training:
+        return inv_preds[-1], torch.stack(pose_preds[-1], 1)
+    return inv_preds, torch.stack([torch.stack(pr, 1) for pr in pose_preds], 2)
+
+
+def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", loss_kw=None):
+    """SelfSupModelMF / SupModelMF .forward in training mode with flip disabled
+    (models/SfmModelMF.py:140-189, SelfSupModelMF.py:63-99, SupModelMF.py:78-119)."""
+    loss_kw = loss_kw or {}
+    invs, pvec = depth_pose_net(p, version, min_depth, max_depth, batch["rgb"], batch["rgb_context"],
+                                batch["intrinsics"], training=True)
+    N, n = pvec.shape[1], pvec.shape[2]
+    poses = [[pvec[:, j, i] for i in range(n)] for j in range(N)]
+    K = batch["intrinsics"]
+    if kind == "selfsup":
+        return photometric_decay_loss(batch["rgb_original"], batch["rgb_context_original"], invs, K,
+                                      K, poses, **loss_kw)
+    gt_inv = torch.where(batch["depth"] <= 0, torch.zeros_like(batch["depth"]),
+                         1.0 / batch["depth"].clamp(min=1e-6))
+    return supervised_depth_pose_loss(invs, gt_inv, batch["pose_context"], poses, K, K, min_depth,
+                                      max_depth)
+
+
+def rel_err(a, b):
+    """max |a-b| / max(|b|) -- the relative metric the parity tests quote."""
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("math", "torch", "F")]

@@ -1,0 +1,81 @@
+"""C ABI checks that need no GPU: the library loads, exports exactly what
+include/dro_amd.h declares, and rejects bad arguments before launching."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dro_amd.h")
+LIB = os.path.join(ROOT, "dro-sfm_amd", "libdro_amd.so")
+
+
+def declared():
+    txt = open(HEADER).read()
+    return set(re.findall(r"\b(dro_[a-z0-9_]+)\s*\(", txt))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        pytest.fail("libdro_amd.so not built: run `make -C dro-sfm_amd/csrc`")
+    import torch  # noqa: F401  (HIP runtime of torch first, as the product does)
+    from dro_sfm_amd.hip import _lib
+    return _lib.load()
+
+
+def test_header_matches_exports(lib):
+    from dro_sfm_amd.hip import _lib
+    names = declared()
+    assert names == set(_lib.EXPORTED)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_abi_version(lib):
+    assert lib.dro_abi_version() == 1
+
+
+def test_null_arguments_rejected(lib):
+    NULL = None
+    st = lib.dro_warp_cost_forward(NULL, NULL, NULL, 0, 0.0, 0.0, NULL, NULL, 0.125, NULL, 0,
+                                   1, 1, 1, 2, 2, 1, NULL, NULL)
+    assert st == -1
+    assert b"NULL" in lib.dro_last_error()
+    st = lib.dro_photometric_forward(NULL, NULL, NULL, NULL, NULL, NULL, 0, 1, 1, 1, 8, 8, 0.85,
+                                     1e-4, 9e-4, 1e-3, 1, 1, NULL, NULL, NULL)
+    assert st == -1
+    st = lib.dro_convex_upsample_forward(NULL, NULL, 1, 2, 2, 8, NULL, NULL)
+    assert st == -1
+
+
+def test_bad_sizes_and_modes_rejected(lib):
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    # h = 1 is out of range (normalisation divides by h-1)
+    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 0, 1, 1, 1, 1, 4, 1,
+                                     p, None) == -2
+    # unknown pose mode
+    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 7, 1, 1, 1, 2, 2, 1,
+                                     p, None) == -3
+    # automask needs the min reduction
+    assert lib.dro_photometric_forward(p, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.85, 1e-4, 9e-4, 1e-3,
+                                       1, 0, p, p, None) == -3
+    assert lib.dro_convex_upsample_forward(p, p, 1, 2, 2, 9, p, None) == -2
+
+
+def test_workspace_sizes(lib):
+    assert lib.dro_warp_cost_workspace_bytes(2, 2, 24, 80) >= 2 * 2 * 24 * 80 * 2 * 4
+    assert lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640) >= 9 * 2 * 192 * 640
+
+
+def test_no_cpu_fallback():
+    """Product ops refuse CPU tensors (there is no CPU path)."""
+    import torch
+    import dro_sfm_amd.hip as H
+    x = torch.zeros(1, 4, 2, 2)
+    with pytest.raises(RuntimeError):
+        H.warp_cost(x, x.unsqueeze(0), torch.ones(1, 1, 2, 2), torch.zeros(1, 6), torch.eye(3).unsqueeze(0))
+    with pytest.raises(RuntimeError):
+        H.convex_upsample(torch.zeros(1, 1, 2, 2), torch.zeros(1, 576, 2, 2))

@@ -1,0 +1,308 @@
+"""GPU parity: the HIP kernels (through the C ABI, via dro_sfm_amd.hip) against
+the reference golden vectors and the CPU oracle on identical inputs.
+
+Tolerance: 1e-4 relative (max|a-b| / max|b|) for outputs and input gradients
+(BASELINE.json north_star); recurrent full-network outputs 1e-3 (fp32
+rounding amplified through 8-12 GRU steps, stated per test).
+"""
+import os
+
+import pytest
+import torch
+
+from common import kitti_K, load_fixture, load_spec, params_from_spec, smooth_images
+from oracle import dro_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-4
+DEV = "cuda"
+
+
+def fx(name):
+    return {k: v.to(DEV) for k, v in load_fixture(os.path.join(G, name + ".npz")).items()}
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import dro_sfm_amd.hip as H
+    from dro_sfm_amd.hip import _lib
+    _lib.load()
+    return H
+
+
+def rel(a, b):
+    return O.rel_err(a.cpu(), b.cpu())
+
+
+# ------------------------------------------------------------------ warp + feature cost
+@pytest.mark.parametrize("name", ["cost_each_small", "cost_each_edge", "cost_each_kitti"])
+@pytest.mark.parametrize("as_matrix", [False, True])
+def test_warp_cost_single_ref(hip, name, as_matrix):
+    d = fx(name)
+    pose = d["pose"]
+    if as_matrix:  # same pose as a [B,4,4] transform; chain its grad back to euler via the oracle
+        pose_in = O.vec_to_transform(pose.cpu()).to(DEV)
+    else:
+        pose_in = pose
+    pose_in = pose_in.clone().requires_grad_(True)
+    fmap, fref, depth = (d[k].clone().requires_grad_(True) for k in ("fmap", "fmap_ref", "depth"))
+    cost = hip.warp_cost(fmap, fref, depth, pose_in, d["K"], depth_mode=hip.DEPTH_METRIC,
+                         reduce_mean=False).squeeze(0)
+    assert rel(cost, d["cost"]) < TOL
+    (cost * d["G"]).sum().backward()
+    assert rel(fmap.grad, d["g_fmap"]) < TOL
+    assert rel(fref.grad, d["g_fmap_ref"]) < TOL
+    assert rel(depth.grad, d["g_depth"]) < TOL
+    if as_matrix:
+        vec = pose.cpu().clone().requires_grad_(True)
+        T = O.vec_to_transform(vec)
+        (T * pose_in.grad.cpu()).sum().backward()
+        assert rel(vec.grad, d["g_pose"]) < TOL
+    else:
+        assert rel(pose_in.grad, d["g_pose"]) < TOL
+
+
+@pytest.mark.parametrize("name", ["depth_cost_n2", "depth_cost_n4"])
+def test_warp_cost_depth_mean(hip, name):
+    d = fx(name)
+    disp = d["disp"].clone().requires_grad_(True)
+    fmap = d["fmap"].clone().requires_grad_(True)
+    fref = d["fmap_ref"].clone().requires_grad_(True)
+    cost = hip.warp_cost(fmap, fref, disp, d["poses"], d["K"], depth_mode=hip.DEPTH_DISP,
+                         min_depth=float(d["min_depth"]), max_depth=float(d["max_depth"]),
+                         reduce_mean=True)
+    assert rel(cost, d["cost"]) < TOL
+    (cost * d["G"]).sum().backward()
+    assert rel(disp.grad, d["g_disp"]) < TOL
+    assert rel(fmap.grad, d["g_fmap"]) < TOL
+    assert rel(fref.grad, d["g_fmap_ref"]) < TOL
+
+
+def test_plane_sweep(hip):
+    d = fx("plane_sweep_d64")
+    vol = hip.plane_sweep_cost(d["fmap"], d["fmap_ref"], d["disp"], d["pose"], d["K"],
+                               min_depth=float(d["min_depth"]), max_depth=float(d["max_depth"]))
+    assert rel(vol, d["cost"]) < TOL
+
+
+def test_warp_cost_kitti_size_vs_oracle(hip):
+    """Metric-config size: B=2, C=128, 24x80, N=2 refs, depth mean + per-ref pose cost."""
+    g = torch.Generator().manual_seed(7)
+    B, C, h, w, N = 2, 128, 24, 80, 2
+    K = kitti_K(B)
+    fmap, frefs = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    disp = torch.rand(B, 1, h, w, generator=g)
+    poses = torch.cat([0.1 * torch.randn(N, B, 3, generator=g), 0.02 * torch.randn(N, B, 3, generator=g)], 2)
+    Gm, Gp = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    # oracle
+    dc = disp.clone().requires_grad_(True)
+    fc = fmap.clone().requires_grad_(True)
+    rc = frefs.clone().requires_grad_(True)
+    pc = poses.clone().requires_grad_(True)
+    inv = O.disp_to_depth(dc, 0.5, 80.0)
+    cm = O.depth_cost_calc(inv, fc, list(rc), list(poses), K, K, 1 / 8)
+    depth_fixed = O.inv2depth(O.disp_to_depth(disp, 0.5, 80.0))
+    cp = torch.stack([O.get_cost_each(pc[j], fc, rc[j], depth_fixed, K, K, 1 / 8) for j in range(N)])
+    ((cm * Gm).sum() + (cp * Gp).sum()).backward()
+    # HIP
+    dg, fg, rg, pg = (t.to(DEV).requires_grad_(True) for t in (disp, fmap, frefs, poses))
+    Kd = K.to(DEV)
+    hm = hip.warp_cost(fg, rg, dg, poses.to(DEV), Kd, depth_mode=hip.DEPTH_DISP, min_depth=0.5,
+                       max_depth=80.0, reduce_mean=True)
+    hp = hip.warp_cost(fg, rg, disp.to(DEV), pg, Kd, depth_mode=hip.DEPTH_DISP, min_depth=0.5,
+                       max_depth=80.0, reduce_mean=False)
+    ((hm * Gm.to(DEV)).sum() + (hp * Gp.to(DEV)).sum()).backward()
+    assert rel(hm, cm) < TOL and rel(hp, cp) < TOL
+    assert rel(dg.grad, dc.grad) < TOL
+    assert rel(fg.grad, fc.grad) < TOL
+    assert rel(rg.grad, rc.grad) < TOL
+    assert rel(pg.grad, pc.grad) < TOL
+
+
+def test_warp_cost_forward_deterministic(hip):
+    d = fx("cost_each_small")
+    a = hip.warp_cost(d["fmap"], d["fmap_ref"], d["depth"], d["pose"], d["K"], reduce_mean=False)
+    b = hip.warp_cost(d["fmap"], d["fmap_ref"], d["depth"], d["pose"], d["K"], reduce_mean=False)
+    assert torch.equal(a, b)
+
+
+def test_warp_cost_rejects_bad_input(hip):
+    d = fx("cost_each_small")
+    with pytest.raises(RuntimeError):
+        hip.warp_cost(d["fmap"].cpu(), d["fmap_ref"], d["depth"], d["pose"], d["K"])
+    with pytest.raises(RuntimeError):
+        hip.warp_cost(d["fmap"], d["fmap_ref"][:, :, :5], d["depth"], d["pose"], d["K"])
+    with pytest.raises(RuntimeError):
+        hip.warp_cost(d["fmap"].double(), d["fmap_ref"], d["depth"], d["pose"], d["K"])
+
+
+# ------------------------------------------------------------------ photometric loss
+def _fp64_photometric(d):
+    """fp64 oracle gradients on the fixture inputs: the yardstick for how far the
+    reference's own fp32 reductions sit from the exact result."""
+    dt = torch.float64
+    invs = [i.cpu().to(dt).requires_grad_(True) for i in d["inv_depths"]]
+    vecs = d["poses"].cpu().to(dt).requires_grad_(True)
+    N, n = vecs.shape[1], vecs.shape[2]
+    poses = [[vecs[:, j, i] for i in range(n)] for j in range(N)]
+    out = O.photometric_decay_loss(d["image"].cpu().to(dt), [c.cpu().to(dt) for c in d["context"]], invs,
+                                   d["K"].cpu().to(dt), d["K"].cpu().to(dt), poses,
+                                   automask=bool(int(d["automask"])),
+                                   reduce="min" if int(d["reduce_min"]) else "mean")
+    out["loss"].sum().backward()
+    return torch.stack([i.grad for i in invs]), vecs.grad
+
+
+@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean"])
+def test_photometric_loss_golden(hip, name):
+    """Loss scalar: 1e-4 vs the reference.  Gradients: 1e-4, or 4x the distance
+    of the reference's own fp32 gradient from the fp64 result when that is
+    larger (the pose gradient is a 2*H*W-term reduction with cancellation; the
+    min-selection flips a few near-tied pixels between any two fp32 orders)."""
+    d = fx(name)
+    invs = d["inv_depths"].clone().requires_grad_(True)           # [n,B,1,H,W]
+    vec = d["poses"].clone().requires_grad_(True)                 # [B,N,n,6]
+    pose = vec.permute(1, 2, 0, 3)                                # [N,n,B,6]
+    loss, metrics = hip.photometric_loss(d["image"], d["context"], invs, pose, d["K"],
+                                         automask=bool(int(d["automask"])),
+                                         reduce_min=bool(int(d["reduce_min"])))
+    assert rel(loss, d["loss"]) < TOL
+    assert rel(metrics[1], d["smoothness_loss"]) < TOL
+    loss.sum().backward()
+    g_inv64, g_pose64 = _fp64_photometric(d)
+    tol_inv = max(TOL, 4 * rel(d["g_inv_depths"].double(), g_inv64))
+    tol_pose = max(TOL, 4 * rel(d["g_poses"].double(), g_pose64))
+    assert rel(invs.grad, d["g_inv_depths"]) < tol_inv
+    assert rel(vec.grad, d["g_poses"]) < tol_pose
+    assert rel(vec.grad.double(), g_pose64) < tol_pose
+
+
+def test_photometric_loss_kitti_size_vs_oracle(hip):
+    """Metric-config loss: B=2, 192x640, n_pred=9, N=2, automask + min."""
+    g = torch.Generator().manual_seed(9)
+    B, H, W, n, N = 2, 192, 640, 9, 2
+    K = kitti_K(B)
+    image = smooth_images(B, H, W, 41)
+    ctx = torch.stack([smooth_images(B, H, W, 42 + j) for j in range(N)])
+    invs = 0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g)
+    vec = torch.cat([0.1 * torch.randn(B, N, n, 3, generator=g), 0.02 * torch.randn(B, N, n, 3, generator=g)], 3)
+    ic, vc = invs.clone().requires_grad_(True), vec.clone().requires_grad_(True)
+    poses = [[vc[:, j, i] for i in range(n)] for j in range(N)]
+    out = O.photometric_decay_loss(image, list(ctx), list(ic), K, K, poses)
+    out["loss"].sum().backward()
+    ig, vg = invs.to(DEV).requires_grad_(True), vec.to(DEV).requires_grad_(True)
+    loss, metrics = hip.photometric_loss(image.to(DEV), ctx.to(DEV), ig, vg.permute(1, 2, 0, 3), K.to(DEV))
+    loss.sum().backward()
+    assert rel(loss, out["loss"]) < TOL
+    assert rel(metrics[1], out["smoothness_loss"]) < TOL
+    assert rel(ig.grad, ic.grad) < TOL
+    assert rel(vg.grad, vc.grad) < TOL
+
+
+# ------------------------------------------------------------------ convex upsample
+def test_convex_upsample(hip):
+    d = fx("upsample")
+    inv, mask = d["inv"].clone().requires_grad_(True), d["mask"].clone().requires_grad_(True)
+    up = hip.convex_upsample(inv, mask, 8)
+    assert rel(up, d["up"]) < TOL
+    (up * d["G"]).sum().backward()
+    assert rel(inv.grad, d["g_inv"]) < TOL
+    assert rel(mask.grad, d["g_mask"]) < TOL
+
+
+def test_convex_upsample_kitti_size(hip):
+    g = torch.Generator().manual_seed(3)
+    inv, mask = torch.rand(2, 1, 24, 80, generator=g), torch.randn(2, 576, 24, 80, generator=g)
+    ic, mc = inv.clone().requires_grad_(True), mask.clone().requires_grad_(True)
+    ref = O.convex_upsample(ic, mc, 8)
+    Gr = torch.randn(ref.shape, generator=g)
+    (ref * Gr).sum().backward()
+    ig, mg = inv.to(DEV).requires_grad_(True), mask.to(DEV).requires_grad_(True)
+    up = hip.convex_upsample(ig, mg, 8)
+    (up * Gr.to(DEV)).sum().backward()
+    assert rel(up, ref) < TOL and rel(ig.grad, ic.grad) < TOL and rel(mg.grad, mc.grad) < TOL
+
+
+# ------------------------------------------------------------------ network level
+def _load_net(tag, version, mind, maxd):
+    from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
+    net = DepthPoseNet(version=version, min_depth=mind, max_depth=maxd)
+    net.load_state_dict(params_from_spec(load_spec(os.path.join(G, f"depthposenet_{tag}_keys.json"))))
+    return net.to(DEV)
+
+
+@pytest.mark.parametrize("tag,version", [("it8", "it8-seq4-inter-out"), ("it12h", "it12-h-out")])
+def test_depth_pose_net_golden(hip, tag, version):
+    """Full forward (train + eval mode) against the reference; 1e-3 (recurrent)."""
+    d = fx(f"depthposenet_{tag}")
+    net = _load_net(tag, version, float(d["min_depth"]), float(d["max_depth"]))
+    net.train()
+    with torch.no_grad():
+        invs, poses = net(d["image"], list(d["refs"]), d["K"])
+        assert rel(torch.stack(invs), d["inv_depths"]) < 1e-3
+        assert rel(poses, d["poses"]) < 1e-3
+        net.eval()
+        inv_e, pose_e = net(d["image"], list(d["refs"]), d["K"])
+        assert rel(inv_e, d["inv_eval"]) < 1e-3
+        assert rel(pose_e, d["poses_eval"]) < 1e-3
+
+
+@pytest.mark.parametrize("tag,version,kind", [("it8", "it8-seq4-inter-out", "selfsup"),
+                                              ("it12h", "it12-h-out", "sup")])
+def test_train_step_golden(hip, tag, version, kind):
+    """SelfSupModelMF / SupModelMF loss and parameter gradients vs the reference."""
+    from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF
+    from dro_sfm_amd.models.SupModelMF import SupModelMF
+    d = fx(f"train_step_{tag}")
+    dn = fx(f"depthposenet_{tag}")
+    mind, maxd = float(dn["min_depth"]), float(dn["max_depth"])
+    kw = dict(ssim_loss_weight=0.85, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
+              photometric_reduce_op="min", clip_loss=0.0, automask_loss=True, flip_lr_prob=0.0,
+              min_depth=mind, max_depth=maxd)
+    model = (SelfSupModelMF if kind == "selfsup" else SupModelMF)(**kw)
+    model.add_depth_net(_load_net(tag, version, mind, maxd))
+    model.train()
+    N = d["refs"].shape[0]
+    batch = {"rgb": d["image"], "rgb_context": list(d["refs"]), "rgb_original": d["image"],
+             "rgb_context_original": list(d["refs"]), "intrinsics": d["K"].clone(),
+             "depth": d["gt_depth"], "pose_context": [d["gt_poses"][:, j] for j in range(N)]}
+    out = model(batch)
+    assert rel(out["loss"], d["loss"]) < 1e-3
+    out["loss"].sum().backward()
+    worst = 0.0
+    for k, v in model.depth_net.named_parameters():
+        key = "gsum." + k
+        if key in d and v.grad is not None:
+            ref = d[key].cpu()
+            worst = max(worst, abs(float(v.grad.double().sum()) - float(ref[0])) / (float(ref[1]) + 1e-12))
+    assert worst < 1e-2
+
+
+def test_train_step_kitti_metric_config(hip):
+    """Metric config (KITTI 192x640, it8-seq4-inter-out, B=2, N=2): product step vs oracle step
+    on the same weights and inputs -- loss and the summed-|grad| of every parameter."""
+    from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF
+    B, N, H, W = 2, 2, 192, 640
+    spec = load_spec(os.path.join(G, "depthposenet_it8_keys.json"))
+    p = params_from_spec(spec)
+    img = smooth_images(B, H, W, 51)
+    refs = [torch.roll(img, 3 * (j + 1), 3) * 0.97 + 0.03 * smooth_images(B, H, W, 52 + j) for j in range(N)]
+    K = kitti_K(B)
+    batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
+             "intrinsics": K}
+    pc = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+          for k, v in p.items()}
+    ref = O.train_step_loss(pc, "it8-seq4-inter-out", 0.5, 80.0, batch, kind="selfsup")
+    ref["loss"].sum().backward()
+    model = SelfSupModelMF(ssim_loss_weight=0.85, smooth_loss_weight=0.001, photometric_reduce_op="min",
+                           clip_loss=0.0, automask_loss=True, flip_lr_prob=0.0, min_depth=0.5, max_depth=80.0)
+    model.add_depth_net(_load_net("it8", "it8-seq4-inter-out", 0.5, 80.0))
+    model.train()
+    gb = {k: (v.to(DEV) if torch.is_tensor(v) else [t.to(DEV) for t in v]) for k, v in batch.items()}
+    out = model(gb)
+    out["loss"].sum().backward()
+    assert rel(out["loss"], ref["loss"]) < 1e-3
+    for k, v in model.depth_net.named_parameters():
+        if k in pc and pc[k].grad is not None:
+            assert rel(v.grad.abs().sum(), pc[k].grad.abs().sum()) < 2e-2, k

@@ -1,0 +1,227 @@
+"""Pin the CPU oracle (oracle/dro_oracle.py) to the reference's golden vectors.
+
+The fixtures were produced by running the reference code itself
+(tests/golden/gen_golden.py).  Tolerance: 1e-5 relative (max|a-b| / max|b|)
+for single ops, looser where a recurrent network amplifies fp32 rounding.
+"""
+import os
+
+import pytest
+import torch
+
+from common import load_fixture, load_spec, params_from_spec  # tests/golden on sys.path
+from oracle import dro_oracle as O
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-5
+
+
+def fx(name):
+    return load_fixture(os.path.join(G, name + ".npz"))
+
+
+@pytest.mark.parametrize("name", ["cost_each_small", "cost_each_edge", "cost_each_kitti"])
+def test_cost_each(name):
+    d = fx(name)
+    pose, fmap, fref, depth = (d[k].clone().requires_grad_(True) for k in ("pose", "fmap", "fmap_ref", "depth"))
+    cost = O.get_cost_each(pose, fmap, fref, depth, d["K"], d["K"], 1.0 / 8)
+    assert O.rel_err(cost, d["cost"]) < TOL
+    (cost * d["G"]).sum().backward()
+    assert O.rel_err(fmap.grad, d["g_fmap"]) < TOL
+    assert O.rel_err(fref.grad, d["g_fmap_ref"]) < TOL
+    assert O.rel_err(depth.grad, d["g_depth"]) < 1e-4
+    assert O.rel_err(pose.grad, d["g_pose"]) < 1e-4
+
+
+@pytest.mark.parametrize("name", ["depth_cost_n2", "depth_cost_n4"])
+def test_depth_cost(name):
+    d = fx(name)
+    disp = d["disp"].clone().requires_grad_(True)
+    fmap = d["fmap"].clone().requires_grad_(True)
+    frefs = [f.clone().requires_grad_(True) for f in d["fmap_ref"]]
+    poses = list(d["poses"])
+    inv = O.disp_to_depth(disp, float(d["min_depth"]), float(d["max_depth"]))
+    cost = O.depth_cost_calc(inv, fmap, frefs, poses, d["K"], d["K"], 1.0 / 8)
+    assert O.rel_err(cost, d["cost"]) < TOL
+    (cost * d["G"]).sum().backward()
+    assert O.rel_err(disp.grad, d["g_disp"]) < 1e-4
+    assert O.rel_err(fmap.grad, d["g_fmap"]) < TOL
+    assert O.rel_err(torch.stack([f.grad for f in frefs]), d["g_fmap_ref"]) < TOL
+
+
+def test_plane_sweep():
+    d = fx("plane_sweep_d64")
+    B, C, h, w = d["fmap"].shape
+    vol = []
+    for v in d["disp"]:
+        inv = O.disp_to_depth(torch.full((B, 1, h, w), float(v)), float(d["min_depth"]), float(d["max_depth"]))
+        vol.append(O.get_cost_each(d["pose"], d["fmap"], d["fmap_ref"], O.inv2depth(inv), d["K"], d["K"], 1 / 8))
+    assert O.rel_err(torch.stack(vol, 1), d["cost"]) < TOL
+
+
+def test_view_synthesis():
+    d = fx("view_synthesis")
+    depth, pose = d["depth"].clone().requires_grad_(True), d["pose"].clone().requires_grad_(True)
+    out = O.view_synthesis(d["ref"], depth, pose, d["K"], d["K"])
+    assert O.rel_err(out, d["warped"]) < TOL
+    (out * d["G"]).sum().backward()
+    assert O.rel_err(depth.grad, d["g_depth"]) < 1e-4
+    assert O.rel_err(pose.grad, d["g_pose"]) < 1e-4
+
+
+def test_ssim():
+    d = fx("ssim")
+    x = d["x"].clone().requires_grad_(True)
+    s = O.ssim(x, d["y"])
+    assert O.rel_err(s, d["ssim"]) < TOL
+    (s * d["G"]).sum().backward()
+    assert O.rel_err(x.grad, d["g_x"]) < 1e-4
+
+
+@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean"])
+def test_photometric_loss(name):
+    d = fx(name)
+    invs = [i.clone().requires_grad_(True) for i in d["inv_depths"]]
+    vecs = d["poses"].clone().requires_grad_(True)  # [B,N,n,6]
+    N, n = vecs.shape[1], vecs.shape[2]
+    poses = [[vecs[:, j, i] for i in range(n)] for j in range(N)]
+    out = O.photometric_decay_loss(d["image"], list(d["context"]), invs, d["K"], d["K"], poses,
+                                   automask=bool(d["automask"]),
+                                   reduce="min" if int(d["reduce_min"]) else "mean")
+    assert O.rel_err(out["loss"], d["loss"]) < TOL
+    assert O.rel_err(out["photometric_loss"], d["photometric_loss"]) < TOL
+    assert O.rel_err(out["smoothness_loss"], d["smoothness_loss"]) < TOL
+    out["loss"].sum().backward()
+    assert O.rel_err(torch.stack([i.grad for i in invs]), d["g_inv_depths"]) < 1e-4
+    assert O.rel_err(vecs.grad, d["g_poses"]) < 1e-4
+
+
+def test_supervised_loss():
+    d = fx("sup_loss")
+    invs = [i.clone().requires_grad_(True) for i in d["inv_depths"]]
+    vecs = d["poses"].clone().requires_grad_(True)
+    N, n = vecs.shape[1], vecs.shape[2]
+    poses = [[vecs[:, j, i] for i in range(n)] for j in range(N)]
+    gt = d["gt_depth"]
+    gt_inv = torch.where(gt <= 0, torch.zeros_like(gt), 1.0 / gt.clamp(min=1e-6))
+    out = O.supervised_depth_pose_loss(invs, gt_inv, [d["gt_poses"][:, j] for j in range(N)], poses,
+                                       d["K"], d["K"], float(d["min_depth"]), float(d["max_depth"]))
+    assert O.rel_err(out["loss"], d["loss"]) < TOL
+    assert O.rel_err(out["depth_loss"], d["depth_loss"]) < TOL
+    assert O.rel_err(out["pose_loss"], d["pose_loss"]) < TOL
+    out["loss"].sum().backward()
+    assert O.rel_err(torch.stack([i.grad for i in invs]), d["g_inv_depths"]) < 1e-4
+    assert O.rel_err(vecs.grad, d["g_poses"]) < 1e-4
+
+
+def test_upsample():
+    d = fx("upsample")
+    inv, mask = d["inv"].clone().requires_grad_(True), d["mask"].clone().requires_grad_(True)
+    up = O.convex_upsample(inv, mask, 8)
+    assert O.rel_err(up, d["up"]) < TOL
+    (up * d["G"]).sum().backward()
+    assert O.rel_err(inv.grad, d["g_inv"]) < TOL
+    assert O.rel_err(mask.grad, d["g_mask"]) < TOL
+
+
+def spec_params(name, grad=False):
+    p = params_from_spec(load_spec(os.path.join(G, name + "_keys.json")))
+    if grad:
+        p = {k: (v.requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
+             for k, v in p.items()}
+    return p
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_sepconvgru(hd):
+    d = fx(f"sepconvgru_h{hd}")
+    p = spec_params(f"sepconvgru_h{hd}", grad=True)
+    h, x = d["h"].clone().requires_grad_(True), d["x"].clone().requires_grad_(True)
+    out = O.sep_conv_gru(p, "", h, x)
+    assert O.rel_err(out, d["out"]) < TOL
+    (out * d["G"]).sum().backward()
+    assert O.rel_err(h.grad, d["g_h"]) < 1e-4
+    assert O.rel_err(x.grad, d["g_x"]) < 1e-4
+    for k, v in p.items():
+        ref = d["gsum." + k]
+        got = v.grad.double()
+        assert abs(float(got.sum()) - float(ref[0])) <= 1e-4 * float(ref[1]) + 1e-6, k
+
+
+def test_update_block_depth():
+    d = fx("update_depth")
+    p = spec_params("update_depth", grad=True)
+    net = d["net"].clone().requires_grad_(True)
+    fmap = d["fmap"].clone().requires_grad_(True)
+    frefs = [f.clone().requires_grad_(True) for f in d["fmap_ref"]]
+    poses = list(d["poses"])
+    cost_fn = lambda x: O.depth_cost_calc(x, fmap, frefs, poses, d["K"], d["K"], 1.0 / 8)
+    scale = lambda x: O.disp_to_depth(x, 0.5, 80.0)
+    out, masks, invs = O.update_block_depth(p, "", net, cost_fn, d["disp"], d["ctx"], 2, scale)
+    assert O.rel_err(out, d["net_out"]) < 1e-4
+    assert O.rel_err(torch.stack(invs), d["invs"]) < 1e-4
+    assert O.rel_err(torch.stack(masks)[:, :, :24], d["masks"]) < 1e-4
+    ((out * d["Gn"]).sum() + (invs[-1] * d["Gi"]).sum() + (masks[-1] * d["Gm"]).sum()).backward()
+    assert O.rel_err(net.grad, d["g_net"]) < 1e-4
+    assert O.rel_err(fmap.grad, d["g_fmap"]) < 1e-4
+    assert O.rel_err(torch.stack([f.grad for f in frefs]), d["g_fmap_ref"]) < 1e-4
+    for k, v in p.items():
+        if v.requires_grad:
+            ref = d["gsum." + k]
+            assert abs(float(v.grad.double().sum()) - float(ref[0])) <= 1e-4 * float(ref[1]) + 1e-6, k
+
+
+def test_update_block_pose():
+    d = fx("update_pose")
+    p = spec_params("update_pose", grad=True)
+    fmap = d["fmap"].clone().requires_grad_(True)
+    fref = d["fmap_ref"].clone().requires_grad_(True)
+    pose = d["pose"].clone().requires_grad_(True)
+    cost_fn = lambda q: O.get_cost_each(q, fmap, fref, d["depth"], d["K"], d["K"], 1.0 / 8)
+    out, seqs = O.update_block_pose(p, "", d["net"], cost_fn, pose, d["ctx"], 2)
+    assert O.rel_err(out, d["net_out"]) < 1e-4
+    assert O.rel_err(torch.stack(seqs), d["poses"]) < 1e-4
+    ((out * d["Gn"]).sum() + (seqs[-1] * d["Gp"]).sum()).backward()
+    assert O.rel_err(pose.grad, d["g_pose"]) < 1e-4
+    assert O.rel_err(fmap.grad, d["g_fmap"]) < 1e-4
+    assert O.rel_err(fref.grad, d["g_fmap_ref"]) < 1e-4
+
+
+@pytest.mark.parametrize("tag,version", [("it8", "it8-seq4-inter-out"), ("it12h", "it12-h-out")])
+def test_depth_pose_net(tag, version):
+    d = fx(f"depthposenet_{tag}")
+    p = spec_params(f"depthposenet_{tag}")
+    mind, maxd = float(d["min_depth"]), float(d["max_depth"])
+    with torch.no_grad():
+        invs, poses = O.depth_pose_net(dict(p), version, mind, maxd, d["image"], list(d["refs"]),
+                                       d["K"], training=True)
+        assert O.rel_err(torch.stack(invs), d["inv_depths"]) < 1e-4
+        assert O.rel_err(poses, d["poses"]) < 1e-4
+        # the reference eval pass runs after the train pass updated BN running stats
+        inv_e, pose_e = O.depth_pose_net(p, version, mind, maxd, d["image"], list(d["refs"]),
+                                         d["K"], training=False)
+        assert O.rel_err(inv_e, d["inv_eval"]) < 1e-4
+        assert O.rel_err(pose_e, d["poses_eval"]) < 1e-4
+
+
+@pytest.mark.parametrize("tag,version,kind", [("it8", "it8-seq4-inter-out", "selfsup"),
+                                              ("it12h", "it12-h-out", "sup")])
+def test_train_step(tag, version, kind):
+    d = fx(f"train_step_{tag}")
+    dn = fx(f"depthposenet_{tag}")
+    p = spec_params(f"depthposenet_{tag}", grad=True)
+    mind, maxd = float(dn["min_depth"]), float(dn["max_depth"])
+    N = d["refs"].shape[0]
+    batch = {"rgb": d["image"], "rgb_context": list(d["refs"]), "rgb_original": d["image"],
+             "rgb_context_original": list(d["refs"]), "intrinsics": d["K"], "depth": d["gt_depth"],
+             "pose_context": [d["gt_poses"][:, j] for j in range(N)]}
+    out = O.train_step_loss(p, version, mind, maxd, batch, kind=kind)
+    assert O.rel_err(out["loss"], d["loss"]) < 1e-4
+    out["loss"].sum().backward()
+    worst = 0.0
+    for k, v in p.items():
+        key = "gsum." + k
+        if key in d and v.grad is not None:
+            ref = d[key]
+            worst = max(worst, abs(float(v.grad.double().sum()) - float(ref[0])) / (float(ref[1]) + 1e-12))
+    assert worst < 1e-3

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU session on the MI355X box: each GPU step under its own time limit;
+# stop at the first crash-class exit (fault/abort/segv/timeout), continue past
+# ordinary test failures (exit 1) so later measurements still run.
+# usage: tools/gpu_session.sh <tag> <steps...>   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+crash() { case $1 in 0|1|2|5) return 1;; *) return 0;; esac; }
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local st=$?
+  echo "   exit $st"; tail -n 5 "$OUT/$name.log"
+  if crash $st; then echo "!! crash-class exit $st in $name: stopping"; exit $st; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
+    testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
+    bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
+    benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
+echo "== done"
