@@ -20,6 +20,38 @@ int launch_status(const char* what) {
   return DRO_OK;
 }
 
+// Zero a float buffer with a kernel launch.  Deliberately NOT hipMemsetAsync:
+// a memset issued from this library onto a capturing stream is not recorded in
+// the hipGraph on ROCm 7 (observed: it runs once at capture time and is absent
+// from replays), whereas kernel launches are captured.
+__global__ __launch_bounds__(256) void zero_fill_kernel(float4* __restrict__ p4, float* __restrict__ tail,
+                                                        size_t n4, size_t ntail) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntail; i += stride)
+    tail[i] = 0.f;
+}
+
+int launch_zero(float* p, size_t n, hipStream_t s) {
+  if (n == 0) return DRO_OK;
+  // float4 body needs 16-B alignment; handle a misaligned head by treating it as tail
+  const uintptr_t addr = (uintptr_t)p;
+  if (addr % 16 != 0) {
+    const size_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks < 4096 ? blocks : 4096), dim3(256), 0, s,
+                       (float4*)nullptr, p, (size_t)0, n);
+    return launch_status("zero_fill_kernel launch failed");
+  }
+  const size_t n4 = n / 4, ntail = n % 4;
+  size_t blocks = (n4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, s, (float4*)p, p + 4 * n4, n4,
+                     ntail);
+  return launch_status("zero_fill_kernel launch failed");
+}
+
 }  // namespace dro
 
 extern "C" const char* dro_last_error(void) { return dro::g_last_error; }

@@ -15,6 +15,8 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------- error state
 void set_error(const char* msg);
 int launch_status(const char* what);
+// zero n floats on stream s with a (graph-capturable) kernel launch
+int launch_zero(float* p, size_t n, hipStream_t s);
 // Sums per-workgroup pose partials [npose, nblk, 12] (dL/dR row-major, dL/dt)
 // in a fixed order and writes the pose gradient in its own encoding.
 int launch_pose_finalize(const float* partial, int nblk, int npose, const float* pose,

@@ -147,10 +147,7 @@ extern "C" int dro_convex_upsample_backward(const float* inv, const float* mask,
     return DRO_E_NULL;
   }
   hipStream_t s = (hipStream_t)stream;
-  if (grad_inv) {
-    hipError_t e = hipMemsetAsync(grad_inv, 0, sizeof(float) * (size_t)B * h * w, s);
-    if (e != hipSuccess) return (int)e;
-  }
+  if (grad_inv && (st = launch_zero(grad_inv, (size_t)B * h * w, s))) return st;
   const int total = B * ratio * h * w;
   hipLaunchKernelGGL(convex_up_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, inv, mask,
                      grad_out, B, h, w, ratio, grad_inv, grad_mask);

@@ -396,14 +396,8 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
   float* gxy = geo ? (float*)workspace : nullptr;
   const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
   float* partial = (geo && grad_pose) ? gxy + (size_t)N * B * P * 2 : nullptr;
-  if (grad_fmap_ref) {
-    hipError_t e = hipMemsetAsync(grad_fmap_ref, 0, sizeof(float) * (size_t)N * B * C * P, s);
-    if (e != hipSuccess) return (int)e;
-  }
-  if (gxy) {
-    hipError_t e = hipMemsetAsync(gxy, 0, sizeof(float) * (size_t)N * B * P * 2, s);
-    if (e != hipSuccess) return (int)e;
-  }
+  if (grad_fmap_ref && (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s))) return st;
+  if (gxy && (st = launch_zero(gxy, (size_t)N * B * P * 2, s))) return st;
   if (grad_fmap || grad_fmap_ref || gxy) {
     dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
     hipLaunchKernelGGL(warp_cost_bwd_feat_kernel, grid, dim3(256), 0, s, a, grad_cost, grad_fmap,

@@ -156,11 +156,14 @@ class _Photometric(torch.autograd.Function):
         ctx.cfg = (pose_mode, opts)
         ctx.restore = restore
         metrics = out[1:].detach()
-        ctx.mark_non_differentiable(metrics)
-        return out[0:1], metrics
+        # per-pixel argmin over the candidate maps (uint8 [n,B,H,W], the first
+        # region of the workspace); exposed for parity tests
+        sel = ws[:n * B * H * W].view(n, B, H, W)
+        ctx.mark_non_differentiable(metrics, sel)
+        return out[0:1], metrics, sel
 
     @staticmethod
-    def backward(ctx, gloss, _gmetrics):
+    def backward(ctx, gloss, _gmetrics, _gsel):
         lib = _lib.load()
         image, context, inv_depths, pose_flat, K, ref_K, ws = ctx.saved_tensors
         pose_mode, (ssim_w, C1, C2, smooth_w, automask, reduce_min) = ctx.cfg
@@ -180,17 +183,21 @@ class _Photometric(torch.autograd.Function):
 
 
 def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=0.85, C1=1e-4,
-                     C2=9e-4, smooth_w=0.001, automask=True, reduce_min=True):
+                     C2=9e-4, smooth_w=0.001, automask=True, reduce_min=True,
+                     return_selection=False):
     """Fused MultiViewPhotometricDecayLoss (multiview_photometric_loss_mf.py:303-361).
 
     image [B,3,H,W]; context [N,B,3,H,W]; inv_depths [n,B,1,H,W];
     pose [N,n,B,6] euler vectors or [N,n,B,3|4,4] matrices.
-    Returns (loss [1], detached metrics [2] = (photometric_loss, smoothness_loss)).
+    Returns (loss [1], detached metrics [2] = (photometric_loss, smoothness_loss))
+    and, with return_selection, the per-pixel min-candidate index uint8 [n,B,H,W]
+    (candidate order of the reference's torch.cat: warped_0, unwarped_0, ...).
     """
     opts = (float(ssim_w), float(C1), float(C2), float(smooth_w), int(bool(automask)),
             int(bool(reduce_min)))
-    return _Photometric.apply(image, context, inv_depths, pose, K, K if ref_K is None else ref_K,
-                              opts)
+    loss, metrics, sel = _Photometric.apply(image, context, inv_depths, pose, K,
+                                            K if ref_K is None else ref_K, opts)
+    return (loss, metrics, sel) if return_selection else (loss, metrics)
 
 
 # ------------------------------------------------------------------------- convex upsample

@@ -32,6 +32,8 @@ class MultiViewPhotometricDecayLoss(LossBase):
         self.padding_mode = padding_mode
         self.automask_loss = automask_loss
         self.progressive_scaling = ProgressiveScaling(progressive_scaling, self.n)
+        self.keep_selection = False       # tests: keep the per-pixel min-candidate map
+        self.last_selection = None
         if self.automask_loss:
             assert self.photometric_reduce_op == "min", \
                 "For automasking only the min photometric_reduce_op is supported."
@@ -60,10 +62,11 @@ class MultiViewPhotometricDecayLoss(LossBase):
         invs = torch.stack(list(inv_depths), 0)                               # [n,B,1,H,W]
         kp = [[poses[j][i].kernel_pose() for i in range(n)] for j in range(N)]
         pose_t = torch.stack([torch.stack(row, 0) for row in kp], 0)          # [N,n,B,6|3x4]
-        loss, metrics = photometric_loss(
+        loss, metrics, sel = photometric_loss(
             image, ctx, invs, pose_t, K.float(), ref_K.float(), ssim_w=self.ssim_loss_weight,
             C1=self.C1, C2=self.C2, smooth_w=self.smooth_loss_weight, automask=self.automask_loss,
-            reduce_min=self.photometric_reduce_op == "min")
+            reduce_min=self.photometric_reduce_op == "min", return_selection=True)
+        self.last_selection = sel.clone() if self.keep_selection else None
         # The reference stores a detached alias of the photometric loss and then adds
         # the smoothness in place (:268, :356), so its 'photometric_loss' metric
         # reports the total; mirror that.

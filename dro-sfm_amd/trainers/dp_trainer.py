@@ -193,7 +193,7 @@ class GraphedTrainStep:
     before capture on a side stream and are real training steps.
     """
 
-    def __init__(self, trainer, example_batch, warmup=3, flips=(False, True)):
+    def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True):
         self.tr = trainer
         self.model = trainer.model
         self.static = _clone_batch(example_batch)
@@ -207,7 +207,7 @@ class GraphedTrainStep:
                 self._body(flips[i % len(flips)])
         cur.wait_stream(side)
         torch.cuda.synchronize()
-        self.pool = torch.cuda.graph_pool_handle()
+        self.pool = torch.cuda.graph_pool_handle() if share_pool else None
         self.graphs = {}
         for f in flips:
             g = torch.cuda.CUDAGraph()

@@ -174,7 +174,8 @@ def smoothness(inv_depths, image, smooth_w):
 
 
 def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_w=0.85, C1=1e-4,
-                           C2=9e-4, smooth_w=0.001, automask=True, reduce="min"):
+                           C2=9e-4, smooth_w=0.001, automask=True, reduce="min",
+                           forced_selection=None):
     """MultiViewPhotometricDecayLoss.forward (multiview_photometric_loss_mf.py:303-361).
 
     context: list of N [B,3,H,W]; inv_depths: list of n [B,1,H,W] (full res);
@@ -193,7 +194,12 @@ def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_
     photo = 0.0
     for i in range(n):
         maps = per_pred[i]
-        if reduce == "min":
+        if reduce == "min" and forced_selection is not None:
+            # test hook: take the candidate another implementation selected (its
+            # value is that implementation's min) so near-ties cannot flip
+            idx = forced_selection[i].long().unsqueeze(1)
+            li = torch.gather(torch.cat(maps, 1), 1, idx).mean()
+        elif reduce == "min":
             li = torch.cat(maps, 1).min(1, True)[0].mean()
         else:
             li = sum(m.mean() for m in maps) / len(maps)
@@ -406,7 +412,8 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
     return inv_preds, torch.stack([torch.stack(pr, 1) for pr in pose_preds], 2)
 
 
-def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", loss_kw=None):
+def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", loss_kw=None,
+                    forced_selection=None):
     """SelfSupModelMF / SupModelMF .forward in training mode with flip disabled
     (models/SfmModelMF.py:140-189, SelfSupModelMF.py:63-99, SupModelMF.py:78-119)."""
     loss_kw = loss_kw or {}
@@ -417,7 +424,7 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
     K = batch["intrinsics"]
     if kind == "selfsup":
         return photometric_decay_loss(batch["rgb_original"], batch["rgb_context_original"], invs, K,
-                                      K, poses, **loss_kw)
+                                      K, poses, forced_selection=forced_selection, **loss_kw)
     gt_inv = torch.where(batch["depth"] <= 0, torch.zeros_like(batch["depth"]),
                          1.0 / batch["depth"].clamp(min=1e-6))
     return supervised_depth_pose_loss(invs, gt_inv, batch["pose_context"], poses, K, K, min_depth,

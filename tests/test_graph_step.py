@@ -40,6 +40,7 @@ def test_graph_replay_matches_eager():
         losses_a.append(ta.step(batch, flip=f)[0].clone())
     b = _setup()
     tb = DataParallelTrainer(b, capturable=True)
+    batch["intrinsics"].copy_(K0)                       # the last eager step flipped K in place
     gs = GraphedTrainStep(tb, batch, warmup=3)          # eager warmup: flips F, T, F
     batch["intrinsics"].copy_(K0)
     l3 = gs.step(batch, flip=False)[0].clone()
