@@ -6,10 +6,23 @@ BasicBlocks (conv1/bn1/conv2/bn2[/downsample.0,1]), upconv1.0,
 upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  The convolutions run on
 MIOpen (SURVEY.md §8(f) ranks a fused encoder as the next step); pretrained
 ImageNet weights are never downloaded -- load a checkpoint instead.
+
+Batch normalisation runs on PyTorch's native kernels, not MIOpen: measured on
+MI355X (tools/diag_miopen2.py), MIOpen's training-mode BN (one-pass variance)
+put 1e-2 relative error on encoder gradients against the fp64 oracle, while
+the native kernels stay at the fp32 floor (~1e-3 through the recurrent net).
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d (same state_dict) computed by the native kernels."""
+
+    def forward(self, x):
+        with torch.backends.cudnn.flags(enabled=False):
+            return super().forward(x)
 
 
 class BasicBlock(nn.Module):
@@ -18,13 +31,13 @@ class BasicBlock(nn.Module):
     def __init__(self, cin, cout, stride=1):
         super().__init__()
         self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(cout)
+        self.bn1 = BatchNorm2d(cout)
         self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
-        self.bn2 = nn.BatchNorm2d(cout)
+        self.bn2 = BatchNorm2d(cout)
         self.downsample = None
         if stride != 1 or cin != cout:
             self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
-                                            nn.BatchNorm2d(cout))
+                                            BatchNorm2d(cout))
 
     def forward(self, x):
         y = F.relu(self.bn1(self.conv1(x)), inplace=True)
@@ -49,7 +62,7 @@ class ResNetEncoder(nn.Module):
             raise NotImplementedError("stride must be 4 or 8 (extractor.py:28-41)")
         self.stride = stride
         self.conv1 = nn.Conv2d(3 * num_input_images, 64, 7, 2, 3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = BatchNorm2d(64)
         self.layer1 = _stage(64, 64, 1)
         self.layer2 = _stage(64, 128, 2)
         self.layer3 = _stage(128, 256, 2)

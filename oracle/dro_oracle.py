@@ -197,7 +197,8 @@ def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_
         if reduce == "min" and forced_selection is not None:
             # test hook: take the candidate another implementation selected (its
             # value is that implementation's min) so near-ties cannot flip
-            idx = forced_selection[i].long().unsqueeze(1)
+            idx = forced_selection[i].long()
+            idx = idx.unsqueeze(1) if idx.dim() == 3 else idx           # [B,1,H,W]
             li = torch.gather(torch.cat(maps, 1), 1, idx).mean()
         elif reduce == "min":
             li = torch.cat(maps, 1).min(1, True)[0].mean()
