@@ -153,10 +153,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
-    ap.add_argument("--miopen", action="store_true",
-                    help="route convolutions/batch-norm through MIOpen (default: native kernels)")
+    ap.add_argument("--no-miopen", action="store_true",
+                    help="run the remaining library convolutions on PyTorch's native kernels")
     args = ap.parse_args()
-    torch.backends.cudnn.enabled = args.miopen
+    torch.backends.cudnn.enabled = not args.no_miopen
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)

@@ -29,7 +29,7 @@ def _batch():
 
 def test_graph_replay_matches_eager():
     """From one saved state, a graph replay and an eager step give the same loss
-    and the same updated parameters (atomics make the last bits vary)."""
+    and the same gradients (fp32 atomics make the last bits vary)."""
     import copy
     from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep
     batch = _batch()
@@ -46,14 +46,15 @@ def test_graph_replay_matches_eager():
         # at capture, so replay first, then re-seat the state for the eager step)
         batch["intrinsics"].copy_(K0)
         lg = gs.step(batch, flip=flip)[0].clone()
-        pg = [p.detach().clone() for p in m.parameters()]
+        gg = tr.grads.flat.clone()
         m.load_state_dict(snap_m)
         for st, sv in zip(tr.optimizer.state.values(), snap_o["state"].values()):
             for k in st:
                 st[k].copy_(sv[k])
         batch["intrinsics"].copy_(K0)
         le = tr.step(batch, flip=flip)[0].clone()
+        ge = tr.grads.flat.clone()
         torch.cuda.synchronize()
         assert O.rel_err(lg.cpu(), le.cpu()) < 1e-5, flip
-        for (k, p), q in zip(m.named_parameters(), pg):
-            assert O.rel_err(q.cpu(), p.detach().cpu()) < 1e-4, (flip, k)
+        # gradients of the whole step (fp32 atomics order differs run to run)
+        assert float((gg - ge).norm() / ge.norm()) < 1e-4, flip

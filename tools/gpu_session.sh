@@ -26,7 +26,7 @@ for step in "$@"; do
     testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
     bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    benchm) run bench_miopen 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --miopen ;;
+    benchn) run bench_native 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-miopen ;;
     prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
     *) echo "unknown step $step" ;;
   esac
