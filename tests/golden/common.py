@@ -80,13 +80,13 @@ def load_spec(path):
         return json.load(f)
 
 
-def smooth_images(n, H, W, seed):
-    """Bilinear-upsampled U[0,1) noise at 1/8 res + 0.1 U[0,1) detail, clamped."""
+def smooth_images(n, H, W, seed, detail=0.1):
+    """Bilinear-upsampled U[0,1) noise at 1/8 res + `detail` x U[0,1) detail, clamped."""
     g = torch.Generator()
     g.manual_seed(seed)
     lo = torch.rand(n, 3, max(H // 8, 2), max(W // 8, 2), generator=g)
     up = torch.nn.functional.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False)
-    img = up + 0.1 * torch.rand(n, 3, H, W, generator=g)
+    img = up + detail * torch.rand(n, 3, H, W, generator=g)
     return img.clamp(0.0, 1.0).contiguous()
 
 

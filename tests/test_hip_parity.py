@@ -190,8 +190,8 @@ def test_photometric_loss_kitti_size_vs_oracle(hip):
     g = torch.Generator().manual_seed(9)
     B, H, W, n, N = 2, 192, 640, 9, 2
     K = kitti_K(B)
-    image = smooth_images(B, H, W, 41)
-    ctx = torch.stack([smooth_images(B, H, W, 42 + j) for j in range(N)])
+    image = smooth_images(B, H, W, 41, detail=0.3)      # textured: keeps SSIM well conditioned
+    ctx = torch.stack([smooth_images(B, H, W, 42 + j, detail=0.3) for j in range(N)])
     invs = 0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g)
     vec = torch.cat([0.1 * torch.randn(B, N, n, 3, generator=g), 0.02 * torch.randn(B, N, n, 3, generator=g)], 3)
     ig, vg = invs.to(DEV).requires_grad_(True), vec.to(DEV).requires_grad_(True)
@@ -203,7 +203,8 @@ def test_photometric_loss_kitti_size_vs_oracle(hip):
     assert rel(loss, free["loss"]) < TOL                     # un-forced oracle: same scalar
     ref = {}
     for dt in (torch.float32, torch.float64):
-        ic, vc = invs.to(dt).requires_grad_(True), vec.to(dt).requires_grad_(True)
+        ic = invs.to(dt).detach().clone().requires_grad_(True)
+        vc = vec.to(dt).detach().clone().requires_grad_(True)
         out = O.photometric_decay_loss(image.to(dt), list(ctx.to(dt)), list(ic), K.to(dt), K.to(dt),
                                        [[vc[:, j, i] for i in range(n)] for j in range(N)],
                                        forced_selection=sel.cpu().unsqueeze(2))
@@ -280,9 +281,9 @@ def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None):
 
 def _grad_check(model, g64, g32, floor_mult=8.0, abs_floor=2e-3):
     """Every parameter gradient within max(abs_floor, floor_mult x the fp32
-    oracle's own distance to fp64) of the fp64 oracle, plus the global relative
-    L2 error of the whole gradient within abs_floor."""
-    bad, num, den = [], 0.0, 0.0
+    oracle's own distance to fp64) of the fp64 oracle; the global relative L2
+    error of the whole gradient likewise.  Returns (offenders, ok_global, info)."""
+    bad, num, num32, den = [], 0.0, 0.0, 0.0
     for k, v in model.depth_net.named_parameters():
         if k in g64 and v.grad is not None:
             e = rel(v.grad, g64[k])
@@ -290,8 +291,10 @@ def _grad_check(model, g64, g32, floor_mult=8.0, abs_floor=2e-3):
             if e > tol:
                 bad.append((k, e, tol))
             num += float((v.grad.double().cpu() - g64[k].double()).pow(2).sum())
+            num32 += float((g32[k].double() - g64[k].double()).pow(2).sum())
             den += float(g64[k].double().pow(2).sum())
-    return bad, (num / den) ** 0.5
+    l2, l2_32 = (num / den) ** 0.5, (num32 / den) ** 0.5
+    return bad, l2 <= max(abs_floor, floor_mult * l2_32), (l2, l2_32)
 
 
 def _selfsup_model(mind, maxd, tag, version):
@@ -335,8 +338,8 @@ def test_train_step_golden(hip, tag, version, kind):
     cpu_batch = {k: (v.cpu() if torch.is_tensor(v) else [t.cpu() for t in v]) for k, v in batch.items()}
     _, g64 = _oracle_grads(spec, version, mind, maxd, cpu_batch, kind, torch.float64, forced)
     _, g32 = _oracle_grads(spec, version, mind, maxd, cpu_batch, kind, torch.float32, forced)
-    bad, l2 = _grad_check(model, g64, g32)
-    assert not bad and l2 < 2e-3, (bad[:5], l2)
+    bad, ok, info = _grad_check(model, g64, g32)
+    assert not bad and ok, (bad[:5], info)
 
 
 def test_train_step_kitti_metric_config(hip):
@@ -345,8 +348,9 @@ def test_train_step_kitti_metric_config(hip):
     loss 1e-4; gradients as in test_train_step_golden."""
     B, N, H, W = 2, 2, 192, 640
     spec = load_spec(os.path.join(G, "depthposenet_it8_keys.json"))
-    img = smooth_images(B, H, W, 51)
-    refs = [torch.roll(img, 3 * (j + 1), 3) * 0.97 + 0.03 * smooth_images(B, H, W, 52 + j) for j in range(N)]
+    img = smooth_images(B, H, W, 51, detail=0.3)
+    refs = [torch.roll(img, 3 * (j + 1), 3) * 0.9 + 0.1 * smooth_images(B, H, W, 52 + j, detail=0.3)
+            for j in range(N)]
     K = kitti_K(B)
     batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
              "intrinsics": K}
@@ -358,5 +362,5 @@ def test_train_step_kitti_metric_config(hip):
     loss64, g64 = _oracle_grads(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", torch.float64, forced)
     _, g32 = _oracle_grads(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", torch.float32, forced)
     assert rel(out["loss"], loss64) < TOL
-    bad, l2 = _grad_check(model, g64, g32)
-    assert not bad and l2 < 2e-3, (bad[:5], l2)
+    bad, ok, info = _grad_check(model, g64, g32)
+    assert not bad and ok, (bad[:5], info)
