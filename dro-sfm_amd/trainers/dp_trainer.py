@@ -191,6 +191,10 @@ class GraphedTrainStep:
     flip branch mutates them in place (as the reference does).
     The first eager steps (bucket discovery, MIOpen algorithm selection) run
     before capture on a side stream and are real training steps.
+
+    The graphs hold the ADDRESSES of the parameters, gradients and Adam state:
+    restore checkpoints in place (tensor.copy_), or build a new GraphedTrainStep
+    after optimizer.load_state_dict (which replaces the state tensors).
     """
 
     def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True):

@@ -10,7 +10,8 @@
  *     the library never allocates or frees; outputs are fully overwritten;
  *   * `stream` is a hipStream_t passed as void* (NULL = default stream); all
  *     work is enqueued asynchronously on it and is hipGraph-capturable (no
- *     host synchronisation, no allocation, memsets are async on `stream`);
+ *     host synchronisation, no allocation; buffers are zeroed by kernels, not
+ *     hipMemsetAsync, which is not recorded when issued into a capture);
  *   * return value: 0 on success, a negative DRO_E_* code for an invalid
  *     argument (nothing is launched), or a positive hipError_t from the launch.
  *     dro_last_error() returns a static message for the last failure on the
@@ -132,6 +133,70 @@ int dro_convex_upsample_forward(const float* inv, const float* mask, int B, int 
 int dro_convex_upsample_backward(const float* inv, const float* mask, const float* grad_out,
                                  int B, int h, int w, int ratio,
                                  float* grad_inv, float* grad_mask, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Stride-1 'same' convolutions on f32 MFMA for the recurrent update blocks.
+ * Replace the nn.Conv2d + activation + torch.cat chains of
+ * networks/optim/update.py:5-199 (SepConvGRU :47-74, ProjectionInput* :77-124,
+ * heads :5-28, mask :150-153).  The input is the VIRTUAL channel concatenation
+ * of 1..3 slices (no copy); source 0 may be multiplied elementwise by `scale0`
+ * (same channel count, e.g. the GRU's r*h).  weight [Cout][Cin][KH][KW] with
+ * Cin = sum of slice channels; odd KH, KW; padding KH/2, KW/2.
+ * act: 0 none, 1 relu, 2 sigmoid, 3 tanh, applied in the epilogue after bias,
+ * then the result is multiplied by alpha (alpha != 1 only with act none: the
+ * 0.25-scaled mask heads, update.py:153).  Up to 4 input slices.
+ * The output goes to channels [out_coff, out_coff+Cout) of a [B,out_ctot,H,W]
+ * tensor.
+ * ---------------------------------------------------------------------- */
+typedef struct dro_slice {
+  const float* data;      /* base of a dense [B, total_channels, H, W] tensor */
+  int channels;           /* channels taken */
+  int total_channels;     /* channel count of the underlying tensor */
+  int channel_offset;     /* first channel taken */
+  int broadcast;          /* 1: data is [B, total_channels, 1, 1], constant over H x W
+                             (e.g. the pose map of ProjectionInputPose, update.py:119) */
+} dro_slice;
+
+#define DRO_ACT_NONE 0
+#define DRO_ACT_RELU 1
+#define DRO_ACT_SIGMOID 2
+#define DRO_ACT_TANH 3
+
+int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
+                       const float* weight, const float* bias, int B, int H, int W, int Cout,
+                       int KH, int KW, int act, float alpha, float* out, int out_ctot,
+                       int out_coff, void* stream);
+
+/* SepConvGRU gate q with the blend fused (update.py:69-70 / :76-77):
+ * q = tanh(conv(srcs) + bias); out = (1 - z) * h + z * q; q also stored to
+ * q_out (channels [q_coff, q_coff+Cout) of [B,q_ctot,H,W]) for the backward. */
+int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
+                              const float* weight, const float* bias, int B, int H, int W,
+                              int Cout, int KH, int KW, const dro_slice* z, const dro_slice* h,
+                              float* q_out, int q_ctot, int q_coff, float* out, int out_ctot,
+                              int out_coff, void* stream);
+
+/* Gradients of dro_conv2d_forward given dout [B,Cout,H,W] (dense) and, for
+ * act != 0, the saved activation output y.  grad_srcs[i] (nullable) receives
+ * d/d(source i) -- for a scaled source 0, the gradient w.r.t. the SCALED values
+ * -- into channels [grad_coff[i], +C_i) of a [B, grad_ctot[i], H, W] tensor,
+ * overwritten or added (grad_accumulate[i]); a broadcast source receives its
+ * per-pixel gradient (the caller sums over H x W).  grad_weight / grad_bias
+ * (nullable) are overwritten. */
+int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
+                        const float* weight, int B, int H, int W, int Cout, int KH, int KW,
+                        int act, float alpha, const dro_slice* y, const float* dout,
+                        float* const* grad_srcs, const int* grad_ctot, const int* grad_coff,
+                        const int* grad_accumulate, float* grad_weight, float* grad_bias,
+                        void* stream);
+
+/* SepConvGRU backward, elementwise parts (update.py:67-70): with zr the saved
+ * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W]:
+ *   stage 1: dq = dh'*z; dzr[:, :hd] = dh'*(q-h); dh = dh'*(1-z)
+ *   stage 2: dzr[:, hd:] = drh*h; dh += drh*r        (drh = dL/d(r*h)) */
+int dro_gru_backward_elem(int stage, int B, int hd, int H, int W, const float* dhn,
+                          const float* zr, const float* q, const float* h, const float* drh,
+                          float* dq, float* dzr, float* dh, void* stream);
 
 #ifdef __cplusplus
 }

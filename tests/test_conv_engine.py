@@ -1,0 +1,144 @@
+"""GPU parity of the f32-MFMA convolution engine (csrc/conv.hip) against
+torch.nn.functional.conv2d evaluated in fp64 on the CPU.
+
+Shapes are the update-block convolutions of networks/optim/update.py
+(reference dro_sfm/networks/optim/update.py:5-199) at a reduced pixel count:
+SepConvGRU 1x5 / 5x1 gates over [h, context, projection, depth|pose-map]
+virtual concatenations, projection-encoder 7x7/3x3/1x1 convs, heads, the
+0.25-scaled mask conv.  Tolerance 1e-4 relative (max|a-b| / max|b|), the
+north_star bound; f32 MFMA accumulates in exact fp32.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import dro_sfm_amd.hip as H
+    from dro_sfm_amd.hip import _lib
+    _lib.load()
+    return H
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+ACTS = {None: lambda x: x, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}
+
+
+def make_src(kind, B, C, H, W, g):
+    """kind: 'dense' | 'slice' (channel slice of a wider tensor) | 'bcast' ([B,C,1,1] expanded)."""
+    if kind == "bcast":
+        base = torch.randn(B, C, 1, 1, generator=g)
+        return base, lambda t: t.expand(B, C, H, W)
+    if kind == "slice":
+        base = torch.randn(B, C + 5, H, W, generator=g)
+        return base, lambda t: t[:, 3:3 + C]
+    base = torch.randn(B, C, H, W, generator=g)
+    return base, lambda t: t
+
+
+CASES = [
+    # (sources [(kind, C)], Cout, (KH, KW), act, alpha, B, H, W)
+    ([("dense", 128), ("dense", 128), ("dense", 63), ("dense", 1)], 256, (1, 5), "sigmoid", 1.0, 2, 24, 80),
+    ([("dense", 128), ("slice", 128), ("dense", 58), ("bcast", 6)], 128, (5, 1), "tanh", 1.0, 2, 24, 80),
+    ([("slice", 64)], 64, (3, 3), "relu", 1.0, 2, 24, 80),
+    ([("dense", 1)], 128, (7, 7), "relu", 1.0, 2, 24, 80),
+    ([("bcast", 6)], 128, (7, 7), "relu", 1.0, 2, 24, 80),
+    ([("dense", 64), ("dense", 64)], 63, (3, 3), "relu", 1.0, 2, 24, 80),
+    ([("slice", 128)], 576, (1, 1), None, 0.25, 2, 24, 80),
+    ([("dense", 128)], 1, (3, 3), "tanh", 1.0, 2, 24, 80),
+    ([("dense", 128)], 6, (3, 3), None, 1.0, 4, 24, 80),
+    ([("dense", 37), ("slice", 11)], 45, (5, 3), "sigmoid", 1.0, 3, 7, 13),
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_conv2d_fwd_bwd(hip, case):
+    srcs_spec, Cout, (KH, KW), act, alpha, B, H, W = CASES[case]
+    g = torch.Generator().manual_seed(100 + case)
+    bases, views = zip(*[make_src(k, B, C, H, W, g) for k, C in srcs_spec])
+    Cin = sum(C for _, C in srcs_spec)
+    w = torch.randn(Cout, Cin, KH, KW, generator=g) / (Cin * KH * KW) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    gout = torch.randn(B, Cout, H, W, generator=g)
+
+    # fp64 reference on the CPU
+    rb = [x.double().requires_grad_() for x in bases]
+    rw, rbias = w.double().requires_grad_(), b.double().requires_grad_()
+    x = torch.cat([v(t) for v, t in zip(views, rb)], 1)
+    ref = ACTS[act](F.conv2d(x, rw, rbias, padding=(KH // 2, KW // 2))) * alpha
+    ref.backward(gout.double())
+
+    db = [x.to(DEV).requires_grad_() for x in bases]
+    dw, dbias = w.to(DEV).requires_grad_(), b.to(DEV).requires_grad_()
+    out = hip.conv2d([v(t) for v, t in zip(views, db)], dw, dbias, act=act, alpha=alpha)
+    out.backward(gout.to(DEV))
+    torch.cuda.synchronize()
+    assert rel(out, ref) < TOL
+    assert rel(dw.grad, rw.grad) < TOL
+    assert rel(dbias.grad, rbias.grad) < TOL
+    for i, (a, r) in enumerate(zip(db, rb)):
+        assert rel(a.grad, r.grad) < TOL, f"source {i}"
+
+
+def _gru_ref(h, xs, wz, bz, wr, br, wq, bq, pad):
+    hx = torch.cat([h, *xs], 1)
+    z = torch.sigmoid(F.conv2d(hx, wz, bz, padding=pad))
+    r = torch.sigmoid(F.conv2d(hx, wr, br, padding=pad))
+    q = torch.tanh(F.conv2d(torch.cat([r * h, *xs], 1), wq, bq, padding=pad))
+    return (1 - z) * h + z * q
+
+
+@pytest.mark.parametrize("kernel", [(1, 5), (5, 1)])
+@pytest.mark.parametrize("pose", [False, True])
+def test_sepconvgru_half(hip, kernel, pose):
+    """One SepConvGRU direction (update.py:59-70) fused: 2 launches forward."""
+    B, hd, H, W = 2, 64, 24, 40
+    g = torch.Generator().manual_seed(7 + pose)
+    KH, KW = kernel
+    pad = (KH // 2, KW // 2)
+    spec = [("slice", 64), ("dense", 58), ("bcast", 6)] if pose else [("dense", 64), ("dense", 63), ("dense", 1)]
+    bases, views = zip(*[make_src(k, B, C, H, W, g) for k, C in spec])
+    h = torch.randn(B, hd, H, W, generator=g).tanh()
+    cin = hd + sum(C for _, C in spec)
+    ws = [torch.randn(hd, cin, KH, KW, generator=g) / (cin * KH * KW) ** 0.5 for _ in range(3)]
+    bs = [torch.randn(hd, generator=g) * 0.1 for _ in range(3)]
+    gout = torch.randn(B, hd, H, W, generator=g)
+
+    rp = [t.double().requires_grad_() for t in (h, *bases, *ws, *bs)]
+    rh, rbases, rws, rbs = rp[0], rp[1:1 + len(bases)], rp[1 + len(bases):4 + len(bases)], rp[4 + len(bases):]
+    ref = _gru_ref(rh, [v(t) for v, t in zip(views, rbases)], rws[0], rbs[0], rws[1], rbs[1], rws[2], rbs[2], pad)
+    ref.backward(gout.double())
+
+    dp = [t.to(DEV).requires_grad_() for t in (h, *bases, *ws, *bs)]
+    dh, dbases, dws, dbs = dp[0], dp[1:1 + len(bases)], dp[1 + len(bases):4 + len(bases)], dp[4 + len(bases):]
+    convs = [torch.nn.Conv2d(cin, hd, kernel, padding=pad).to(DEV) for _ in range(3)]
+    for c, w_, b_ in zip(convs, dws, dbs):     # route the leaves through conv-shaped holders
+        c.weight, c.bias = torch.nn.Parameter(w_), torch.nn.Parameter(b_)
+    out = hip.sepconvgru_half(dh, convs[0], convs[1], convs[2], [v(t) for v, t in zip(views, dbases)])
+    out.backward(gout.to(DEV))
+    torch.cuda.synchronize()
+    assert rel(out, ref) < TOL
+    assert rel(dh.grad, rh.grad) < TOL
+    for i, (a, r) in enumerate(zip(dbases, rbases)):
+        assert rel(a.grad, r.grad) < TOL, f"x{i}"
+    for i, (c, rw, rb) in enumerate(zip(convs, rws, rbs)):
+        assert rel(c.weight.grad, rw.grad) < TOL, f"W{i}"
+        assert rel(c.bias.grad, rb.grad) < TOL, f"b{i}"
+
+
+def test_conv2d_rejects_bad_layout(hip):
+    x = torch.randn(2, 8, 6, 10, device=DEV).permute(0, 1, 3, 2)
+    w = torch.randn(4, 8, 3, 3, device=DEV)
+    with pytest.raises(RuntimeError):
+        hip.conv2d([x], w)
+    with pytest.raises(RuntimeError):
+        hip.conv2d([torch.randn(2, 7, 6, 6, device=DEV)], w)
