@@ -155,8 +155,12 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--no-miopen", action="store_true",
                     help="run the remaining library convolutions on PyTorch's native kernels")
+    ap.add_argument("--conv-backend", choices=("hip", "miopen"), default="hip",
+                    help="update-block convolutions: native f32-MFMA engine or MIOpen (A/B only)")
     args = ap.parse_args()
     torch.backends.cudnn.enabled = not args.no_miopen
+    from dro_sfm_amd.networks.optim import update as _update
+    _update.set_conv_backend(args.conv_backend)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -211,7 +215,8 @@ def main():
         "config": {"workload": "KITTI 192x640 mf self-sup (configs[1])", "model": f"DepthPoseNet {VERSION}",
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch, "ref_frames": NREF,
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
-                   "optimizer": "Adam lr 2e-4", "execution": mode},
+                   "optimizer": "Adam lr 2e-4", "execution": mode,
+                   "update_convs": args.conv_backend},
         "final_loss": round(float(loss), 6),
     }
     if rank == 0 and not args.no_roofline:

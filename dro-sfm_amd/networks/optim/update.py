@@ -3,16 +3,40 @@
 Parameter names and shapes follow dro_sfm/networks/optim/update.py so that
 reference checkpoints load unchanged; layers are declared from small spec
 tables.  Differences are execution-only:
-  * convolutions that read the same input are issued as ONE convolution over
-    concatenated weights (SepConvGRU z|r gates, DepthHead.conv1 | mask.0),
-    halving the launches of the recurrent loop;
+  * every convolution runs on the f32-MFMA conv engine (csrc/conv.hip): bias,
+    activation and the 0.25 mask scale in its epilogue, inputs read as a
+    VIRTUAL channel concatenation (no torch.cat of [h, context, projection,
+    depth | pose map]), the pose map broadcast instead of expanded;
+  * SepConvGRU is one fused op per direction (z|r gates in one launch, the q
+    gate with r*h staged on the fly and the (1-z)h + zq blend in its epilogue);
+  * convolutions that read the same input are ONE convolution over
+    concatenated weights (z|r, DepthHead.conv1 | mask.0);
   * the pose block runs once over all reference views stacked along the batch
     axis (the reference loops over refs in Python, DepthPoseNet.py:186); every
     op in it is per-sample, so the result is identical.
+set_conv_backend("miopen") switches the convolutions to MIOpen for A/B
+measurements only; the default is the native engine.
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ... import hip
+
+_BACKEND = "hip"
+_ACT_FN = {None: lambda x: x, "relu": F.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}
+
+
+def set_conv_backend(name):
+    """'hip' (default: csrc/conv.hip) or 'miopen' (torch F.conv2d), for A/B runs."""
+    global _BACKEND
+    if name not in ("hip", "miopen"):
+        raise ValueError(name)
+    _BACKEND = name
+
+
+def conv_backend():
+    return _BACKEND
 
 
 def declare(module, table):
@@ -21,11 +45,26 @@ def declare(module, table):
         setattr(module, name, nn.Conv2d(cin, cout, k, padding=pad))
 
 
-def conv_cat(x, convs, padding):
+def _as_list(x):
+    return list(x) if isinstance(x, (list, tuple)) else [x]
+
+
+def conv(srcs, weight, bias, act=None, alpha=1.0):
+    """act(conv2d(cat(srcs), weight, bias, 'same')) * alpha."""
+    srcs = _as_list(srcs)
+    if _BACKEND == "hip":
+        return hip.conv2d(srcs, weight, bias, act=act, alpha=alpha)
+    kh, kw = weight.shape[2:]
+    x = srcs[0] if len(srcs) == 1 else torch.cat(srcs, 1)
+    y = _ACT_FN[act](F.conv2d(x, weight, bias, padding=(kh // 2, kw // 2)))
+    return y * alpha if alpha != 1.0 else y
+
+
+def conv_cat(x, convs, act=None):
     """One convolution computing several nn.Conv2d that share the input x."""
     w = torch.cat([c.weight for c in convs], 0)
     b = torch.cat([c.bias for c in convs], 0)
-    return torch.split(F.conv2d(x, w, b, padding=padding), [c.out_channels for c in convs], 1)
+    return torch.split(conv(x, w, b, act), [c.out_channels for c in convs], 1)
 
 
 def mask_seq(hidden_dim, ratio):
@@ -43,7 +82,10 @@ class DepthHead(nn.Module):
         declare(self, {"conv1": (input_dim, hidden_dim, 3, 1), "conv2": (hidden_dim, 1, 3, 1)})
 
     def forward(self, x_d, act_fn=torch.tanh):
-        return act_fn(self.conv2(F.relu(self.conv1(x_d))))
+        act = {torch.tanh: "tanh", torch.sigmoid: "sigmoid"}.get(act_fn)
+        y = conv(conv(x_d, self.conv1.weight, self.conv1.bias, "relu"),
+                 self.conv2.weight, self.conv2.bias, act)
+        return y if act is not None else act_fn(y)
 
 
 class PoseHead(nn.Module):
@@ -55,7 +97,9 @@ class PoseHead(nn.Module):
                        "conv2_pose": (hidden_dim, 6, 3, 1)})
 
     def forward(self, x_p):
-        vec = self.conv2_pose(F.relu(self.conv1_pose(x_p))).mean(3).mean(2)
+        y = conv(conv(x_p, self.conv1_pose.weight, self.conv1_pose.bias, "relu"),
+                 self.conv2_pose.weight, self.conv2_pose.bias)
+        vec = y.mean(3).mean(2)
         return torch.cat([vec[:, :3], 0.01 * vec[:, 3:]], dim=1)
 
 
@@ -69,15 +113,18 @@ class SepConvGRU(nn.Module):
         for axis, k, pad in (("1", (1, 5), (0, 2)), ("2", (5, 1), (2, 0))):
             declare(self, {g + axis: (cin, hidden_dim, k, pad) for g in ("convz", "convr", "convq")})
 
-    def _gate(self, h, x, axis, pad):
+    def _gate(self, h, xs, axis):
         cz, cr, cq = (getattr(self, g + axis) for g in ("convz", "convr", "convq"))
-        zr = conv_cat(torch.cat([h, x], 1), (cz, cr), pad)
-        z, r = torch.sigmoid(zr[0]), torch.sigmoid(zr[1])
-        q = torch.tanh(cq(torch.cat([r * h, x], 1)))
+        if _BACKEND == "hip":
+            return hip.sepconvgru_half(h, cz, cr, cq, xs)
+        z, r = conv_cat([h, *xs], (cz, cr), "sigmoid")
+        q = conv([r * h, *xs], cq.weight, cq.bias, "tanh")
         return (1 - z) * h + z * q
 
     def forward(self, h, x):
-        return self._gate(self._gate(h, x, "1", (0, 2)), x, "2", (2, 0))
+        """x: the input tensor, or a list of tensors read as their channel concat."""
+        xs = _as_list(x)
+        return self._gate(self._gate(h, xs, "1"), xs, "2")
 
 
 class _Projection(nn.Module):
@@ -94,12 +141,14 @@ class _Projection(nn.Module):
                        f"conv{tag}2": (hidden_dim, 64, 3, 1),
                        f"conv{tag}": (64 + hidden_dim, out_chs - state_ch, 3, 1)})
 
-    def _mix(self, state_map, cost):
+    def sources(self, state_map, cost):
+        """The projection output as [fused features, state map] (concat implied)."""
         t = self._tag
-        cor = F.relu(self.convc2(F.relu(self.convc1(cost))))
-        sfm = F.relu(getattr(self, f"conv{t}2")(F.relu(getattr(self, f"conv{t}1")(state_map))))
-        fused = F.relu(getattr(self, f"conv{t}")(torch.cat([cor, sfm], 1)))
-        return torch.cat([fused, state_map], 1)
+        c1, c2 = self.convc1, self.convc2
+        s1, s2, f = (getattr(self, f"conv{t}{i}") for i in ("1", "2", ""))
+        cor = conv(conv(cost, c1.weight, c1.bias, "relu"), c2.weight, c2.bias, "relu")
+        sfm = conv(conv(state_map, s1.weight, s1.bias, "relu"), s2.weight, s2.bias, "relu")
+        return [conv([cor, sfm], f.weight, f.bias, "relu"), state_map]
 
 
 class ProjectionInputDepth(_Projection):
@@ -107,16 +156,22 @@ class ProjectionInputDepth(_Projection):
         super().__init__("d", 1, cost_dim, hidden_dim, out_chs)
 
     def forward(self, depth, cost):
-        return self._mix(depth, cost)
+        return torch.cat(self.sources(depth, cost), 1)
 
 
 class ProjectionInputPose(_Projection):
     def __init__(self, cost_dim, hidden_dim, out_chs):
         super().__init__("p", 6, cost_dim, hidden_dim, out_chs)
 
-    def forward(self, pose, cost):
+    def pose_map(self, pose, cost):
         bs, _, h, w = cost.shape
-        return self._mix(pose.reshape(bs, 6, 1, 1).expand(bs, 6, h, w), cost)
+        return pose.reshape(bs, 6, 1, 1).expand(bs, 6, h, w)
+
+    def sources(self, pose, cost):
+        return super().sources(self.pose_map(pose, cost), cost)
+
+    def forward(self, pose, cost):
+        return torch.cat(self.sources(pose, cost), 1)
 
 
 class UpMaskNet(nn.Module):
@@ -127,7 +182,8 @@ class UpMaskNet(nn.Module):
         self.mask = mask_seq(hidden_dim, ratio)
 
     def forward(self, feat):
-        return 0.25 * self.mask(feat)
+        m0, m2 = self.mask[0], self.mask[2]
+        return conv(conv(feat, m0.weight, m0.bias, "relu"), m2.weight, m2.bias, None, 0.25)
 
 
 class BasicUpdateBlockDepth(nn.Module):
@@ -142,15 +198,16 @@ class BasicUpdateBlockDepth(nn.Module):
 
     def heads(self, net):
         """DepthHead.conv1 and mask.0 read the same state: one launch."""
-        a, b = conv_cat(net, (self.depth_head.conv1, self.mask[0]), 1)
-        return torch.tanh(self.depth_head.conv2(F.relu(a))), 0.25 * self.mask[2](F.relu(b))
+        a, b = conv_cat(net, (self.depth_head.conv1, self.mask[0]), "relu")
+        c2, m2 = self.depth_head.conv2, self.mask[2]
+        return conv(a, c2.weight, c2.bias, "tanh"), conv(b, m2.weight, m2.bias, None, 0.25)
 
     def forward(self, net, cost_func, inv_depth, context, seq_len=4, scale_func=None):
         scale_func = scale_func or (lambda x: (x, None))
         invs, masks = [], []
         for _ in range(seq_len):
-            feat = self.encoder(inv_depth, cost_func(scale_func(inv_depth)[0]))
-            net = self.depth_gru(net, torch.cat([context, feat], 1))
+            feat = self.encoder.sources(inv_depth, cost_func(scale_func(inv_depth)[0]))
+            net = self.depth_gru(net, [context, *feat])
             delta, mask = self.heads(net)
             inv_depth = inv_depth + delta
             invs.append(inv_depth)
@@ -170,7 +227,7 @@ class BasicUpdateBlockPose(nn.Module):
     def forward(self, net, cost_func, pose, inp, seq_len=4):
         seq = []
         for _ in range(seq_len):
-            net = self.pose_gru(net, torch.cat([inp, self.encoder(pose, cost_func(pose))], 1))
+            net = self.pose_gru(net, [inp, *self.encoder.sources(pose, cost_func(pose))])
             pose = pose + self.pose_head(net)
             seq.append(pose)
         return net, seq

@@ -26,6 +26,7 @@ for step in "$@"; do
     testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
     bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchmi) run bench_miopen 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --conv-backend miopen ;;
     benchn) run bench_native 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-miopen ;;
     prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
