@@ -31,11 +31,17 @@ def test_graph_replay_matches_eager():
     """From one saved state, a graph replay and an eager step give the same loss
     and the same gradients.  State is restored IN PLACE: the captured graph holds
     the addresses of the parameters and of Adam's state tensors.  The gradient
-    tolerance covers fp32 reassociation amplified through the recurrent net:
-    eager-vs-eager spread (fp32 atomics order in the cancelling pose-gradient
-    sums) measured <=3.3e-4 L2; graph-vs-eager measured 2.6e-3 L2 with the
-    update-block convolutions on MIOpen (which may select other algorithms
-    while a stream is being captured)."""
+    encoders run on PyTorch's native convolutions here: MIOpen's forward
+    convolutions are not run-to-run deterministic (measured 1.4e-6 max diff on
+    the step outputs, tools/diag_determinism2.py), which the min-reprojection
+    selection and the recurrence amplify to ~1e-3 in the gradients.  With a
+    deterministic forward the only spread left is the fp32 atomics order of the
+    backward kernels (measured 3.5e-7 L2 eager-vs-eager)."""
+    with torch.backends.cudnn.flags(enabled=False):
+        _graph_vs_eager()
+
+
+def _graph_vs_eager():
     from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep
     batch = _batch()
     K0 = batch["intrinsics"].clone()
@@ -64,7 +70,7 @@ def test_graph_replay_matches_eager():
         ge = tr.grads.flat.clone()
         torch.cuda.synchronize()
         assert O.rel_err(lg.cpu(), le.cpu()) < 1e-5, flip
-        assert float((gg - ge).norm() / ge.norm()) < 5e-3, flip
+        assert float((gg - ge).norm() / ge.norm()) < 1e-4, flip
         # the same Adam update was applied (tolerance: lr-scaled grad noise)
         for p, q in zip(m.parameters(), pg):
             assert float((p.detach() - q).abs().max()) < 1e-5, flip
