@@ -2,22 +2,31 @@
 // recurrent update blocks of the DRO optimizer (dro_sfm/networks/optim/
 // update.py): SepConvGRU 1x5 / 5x1 gates, projection encoders, heads.
 //
-// Why not MIOpen: at these shapes (M = B*h*w = 3840..7680 output pixels,
-// 64..576 channels) every MIOpen call is a separate launch of 8-30 us plus
-// NCHW<->NHWC transposes, bias/activation/concat are separate ATen kernels,
-// and its training-mode batch-norm/gradient paths lose precision.
-// Here:
-//   * inputs are a VIRTUAL channel concatenation of up to 3 tensor slices (no
+// Why not MIOpen: at these shapes (3840..7680 output pixels, 1..576 channels)
+// every MIOpen call is a separate launch plus NCHW<->NHWC transposes, bias /
+// activation / concat are separate ATen kernels, and its forward is not
+// run-to-run deterministic.  Here:
+//   * inputs are a VIRTUAL channel concatenation of up to 4 tensor slices (no
 //     torch.cat), optionally with source 0 multiplied elementwise by another
-//     slice (the GRU's r*h) while it is staged;
+//     slice (the GRU's r*h) while it is staged; a source may be a [B,C,1,1]
+//     map broadcast over the image (the pose map);
 //   * bias + activation (+ the GRU blend h' = (1-z)h + zq) run in the epilogue,
 //     and the result lands in a channel slice of a bigger tensor;
-//   * f32 MFMA is exact-f32 (a k-ordered fmaf chain): no TF32-style loss.
-// GEMM orientation: rows = output channels, cols = pixels, so the epilogue
-// stores are coalesced along pixels (the MFMA C column is the lane).
+//   * f32 MFMA is exact f32 (a k-ordered fmaf chain): no TF32-style loss.
 //
-// Roofline: MFMA(f32) bound at 157 TF/s peak for the big gates; the small
-// heads are latency bound.  FLOPs per launch = 2 * Cout * P * Cin * KH * KW.
+// GEMM view (forward): rows = output channels, cols = pixels (B*H*W flattened),
+// K = (tap, input channel) in TAP-MAJOR order: a 32-deep K chunk is 32 channels
+// at one kernel tap, so a thread's shifted pixel and its zero-padding test are
+// computed once per chunk and the channel -> source lookup is wave-uniform.
+// Data gradient: the same kernel with rows = input channels, K = (tap, output
+// channel), the tap offset negated and the weight read transposed.  Weight
+// gradient: rows = output channels, cols = input channels at one tap,
+// K = pixels, split over gridDim.y with f32 atomics.
+// Pipeline: global -> registers for chunk c+1 is issued before the MFMAs of
+// chunk c (two LDS buffers, one barrier per chunk).  Tiles are remapped so
+// that blocks sharing a pixel tile run on the same XCD (same L2).
+//
+// Roofline: MFMA(f32) at 157 TF/s; FLOPs per launch = 2 * Cout * P * Cin * KH * KW.
 #include <hip/hip_runtime.h>
 
 #include "dro_common.hpp"
@@ -26,9 +35,8 @@ namespace dro {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kBO = 32;   // output channels per workgroup
-constexpr int kBP = 64;   // pixels per workgroup
-constexpr int kBK = 16;   // reduction chunk
+constexpr int kBN = 64;   // pixels per tile (forward / data gradient)
+constexpr int kBK = 32;   // reduction chunk
 constexpr int kMaxSrc = 4;
 
 struct Slice {            // channels [coff, coff+C) of a [B, ctot, H, W] tensor
@@ -41,20 +49,29 @@ struct ConvGeom {
   int B, H, W, Cin, Cout, KH, KW, PH, PW;
 };
 
-struct ConvFwdArgs {
+struct IgArgs {
   ConvGeom g;
-  Slice src[kMaxSrc];
+  Slice src[kMaxSrc];     // forward inputs (virtual concat)
   int nsrc;
   Slice scale0;           // optional multiplier of source 0 (p == nullptr: none)
   const float* weight;    // [Cout][Cin][KH][KW]
   const float* bias;      // [Cout] or nullptr
-  float alpha;            // output scale (act == none only)
-  float* out;             // output slice base
+  float alpha;            // output scale (act none only)
+  float* out;             // forward output slice base
   int out_ctot, out_coff;
-  // GRU blend epilogue (epi == 1): out = (1-z) h + z q with q = tanh(acc+b)
-  Slice z, h;
-  float* q_out;           // optional: raw q saved for the backward
+  Slice z, h;             // GRU blend epilogue: out = (1-z) h + z q, q = tanh(acc+b)
+  float* q_out;           // optional: q saved for the backward
   int q_ctot, q_coff;
+  const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation
+  float* gsrc[kMaxSrc];   // data-gradient targets per source (nullable)
+  int gsrc_ctot[kMaxSrc], gsrc_coff[kMaxSrc], gsrc_acc[kMaxSrc];
+  float* gweight;         // [Cout][Cin][KH][KW], zeroed, accumulated atomically
+  float* gbias;           // [Cout], zeroed, accumulated atomically
+  int rows;               // GEMM rows: Cout (forward) / Cin (data gradient)
+  int kch;                // channels reduced per tap: Cin (forward) / Cout (data gradient)
+  int row_tiles;          // row tiles (tile = pixel_tile * row_tiles + row_tile)
+  int ctiles, otiles;     // weight gradient: input-channel / output-channel tiles
+  long long pchunk;       // weight gradient: pixels per split
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -76,322 +93,282 @@ __device__ __forceinline__ float act_bwd(float y, int act) {
   }
 }
 
-// value of the virtual input at channel c, pixel offset `off` of image b
-// (caller checks the zero-padding bounds)
-__device__ __forceinline__ float src_val(const Slice* s, int nsrc, const Slice& scale0, int c, int b,
-                                         size_t HW, size_t off) {
-  int base = 0;
-#pragma unroll
-  for (int i = 0; i < kMaxSrc; ++i) {
-    if (i < nsrc && c < base + s[i].C) {
-      const int cl = c - base;
-      float v = s[i].bcast ? s[i].p[(size_t)b * s[i].ctot + s[i].coff + cl]
-                           : s[i].p[((size_t)b * s[i].ctot + s[i].coff + cl) * HW + off];
-      if (i == 0 && scale0.p) v *= scale0.p[((size_t)b * scale0.ctot + scale0.coff + cl) * HW + off];
-      return v;
-    }
-    base += (i < nsrc) ? s[i].C : 0;
-  }
-  return 0.f;
-}
-
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// ------------------------------------------------------------------ forward
-// Workgroup: 4 waves; tile 32 out-channels x 64 pixels.  Wave w computes
-// pixels [32*(w&1), +32) over k-half (w>>1) of every chunk; the two k-halves
-// are summed through LDS before the epilogue.
-template <int ACT, int EPI>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
-  __shared__ float Ws[kBK][kBO + 1];
-  __shared__ float Xs[kBK][kBP];
-  __shared__ float red[2][16][64];
+// Blocks that share a pixel tile get consecutive logical ids on one XCD
+// (hardware dispatch is round-robin over the 8 XCDs by block id).
+__device__ __forceinline__ int xcd_remap(int id, int total) {
+  const int xcd = id & 7, local = id >> 3, per = total >> 3, rem = total & 7;
+  return (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + local;
+}
+
+// virtual input at channel ch (any lane pattern; sources resolved with
+// compile-time indices, no dynamic indexing of the kernel arguments)
+__device__ __forceinline__ float src_val(const IgArgs& a, int ch, int b, size_t HW, size_t off) {
+  int base = 0;
+  float v = 0.f;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < kMaxSrc; ++i) {
+    if (!done && i < a.nsrc && ch < base + a.src[i].C) {
+      const Slice& s = a.src[i];
+      const int cl = ch - base;
+      v = s.bcast ? s.p[(size_t)b * s.ctot + s.coff + cl]
+                  : s.p[((size_t)b * s.ctot + s.coff + cl) * HW + off];
+      if (i == 0 && a.scale0.p)
+        v *= a.scale0.p[((size_t)b * a.scale0.ctot + a.scale0.coff + cl) * HW + off];
+      done = true;
+    }
+    if (i < a.nsrc) base += a.src[i].C;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------ forward / data gradient
+// MODE 0: out[o, p]  = sum_{tap, c} W[o, c, tap] * X[c, p + d(tap)]   (+ epilogue)
+// MODE 1: din[c, p]  = sum_{tap, o} W[o, c, tap] * G[o, p - d(tap)]
+// Tile BM rows x 64 pixels, 4 waves: BM = 64 -> 2x2 waves of 32x32;
+// BM = 32 -> 2 pixel halves x 2 K halves (summed through LDS at the end).
+template <int BM, int MODE, int ACT, int EPI>
+__global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
+  constexpr int WM = BM / 32;
+  constexpr int KSTEPS = (WM == 2) ? 16 : 8;          // MFMA k-steps per wave per chunk
+  __shared__ float Ws[2][kBK][BM + 1];
+  __shared__ float Xs[2][kBK][kBN];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int o0 = blockIdx.y * kBO, p0 = blockIdx.x * kBP;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
+  const int row0 = rt * BM;
+  const long long p0 = (long long)pt * kBN;
   const size_t HW = (size_t)g.H * g.W;
   const long long P = (long long)g.B * HW;
-  const int T = g.KH * g.KW, K = g.Cin * T;
+  const int T = g.KH * g.KW;
+  const int nck = (a.kch + kBK - 1) / kBK, nchunks = T * nck;
 
-  // this thread's staging pixel (fixed for the whole K loop)
-  const long long pg = p0 + (tid & 63);
+  // staging roles: X column (pixel) fixed; W k-lane fixed
+  const int col = tid & 63, krow = tid >> 6;
+  const long long pg = p0 + col;
   const bool pv = pg < P;
-  const int pb = pv ? (int)(pg / HW) : 0;
-  const int prem = pv ? (int)(pg % HW) : 0;
-  const int py = prem / g.W, px = prem % g.W;
+  const int pb = pv ? (int)(pg / (long long)HW) : 0;
+  const int prem = pv ? (int)(pg - (long long)pb * HW) : 0;
+  const int py = prem / g.W, px = prem - py * g.W;
+  const int wkl = tid & 31, wrow = tid >> 5;
 
+  float xr[8], wv[BM / 8];
+  auto load = [&](int chunk) {
+    const int tap = chunk / nck, c0 = (chunk - tap * nck) * kBK;
+    const int ty = tap / g.KW, dy = ty - g.PH, dx = tap - ty * g.KW - g.PW;
+    const int yy = MODE == 0 ? py + dy : py - dy, xx = MODE == 0 ? px + dx : px - dx;
+    const bool inb = pv && yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
+    const size_t off = inb ? (size_t)yy * g.W + xx : 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = __builtin_amdgcn_readfirstlane(c0 + krow + 4 * i);
+      float v = 0.f;
+      if (inb && ch < a.kch) {
+        if (MODE == 0) v = src_val(a, ch, pb, HW, off);
+        else v = a.G[((size_t)pb * g.Cout + ch) * HW + off];
+      }
+      xr[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BM / 8; ++i) {
+      const int r = row0 + wrow + 8 * i, k = c0 + wkl;
+      float v = 0.f;
+      if (r < a.rows && k < a.kch)
+        v = MODE == 0 ? a.weight[((size_t)r * g.Cin + k) * T + tap]
+                      : a.weight[((size_t)k * g.Cin + r) * T + tap];
+      wv[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Xs[buf][krow + 4 * i][col] = xr[i];
+#pragma unroll
+    for (int i = 0; i < BM / 8; ++i) Ws[buf][wkl][wrow + 8 * i] = wv[i];
+  };
+
+  const int wr = (WM == 2) ? (wave & 1) : 0;
+  const int wc = (WM == 2) ? (wave >> 1) : (wave & 1);
+  const int wk = (WM == 2) ? 0 : (wave >> 1);
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  const int wp = wave & 1, wk = wave >> 1;
-  for (int k0 = 0; k0 < K; k0 += kBK) {
-    // ---- stage X: k rows (wave-uniform) x 64 pixels
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kl = wave * 4 + i, k = k0 + kl;
-      float v = 0.f;
-      if (pv && k < K) {
-        const int c = k / T, tap = k - c * T;
-        const int yy = py + tap / g.KW - g.PH, xx = px + tap % g.KW - g.PW;
-        if (yy >= 0 && yy < g.H && xx >= 0 && xx < g.W)
-          v = src_val(a.src, a.nsrc, a.scale0, c, pb, HW, (size_t)yy * g.W + xx);
-      }
-      Xs[kl][tid & 63] = v;
-    }
-    // ---- stage W^T: 16 k x 32 o
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int ol = tid >> 3, kl = (tid & 7) * 2 + i, o = o0 + ol, k = k0 + kl;
-      Ws[kl][ol] = (o < g.Cout && k < K) ? a.weight[(size_t)o * K + k] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int kl = wk * 8 + kk * 2 + (lane >> 5);
-      acc = mfma32(Ws[kl][lane & 31], Xs[kl][wp * 32 + (lane & 31)], acc);
-    }
-    __syncthreads();
-  }
-  // ---- sum the two k-halves
-  if (wk == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[wp][r][lane] = acc[r];
-  }
+  load(0);
+  store(0);
   __syncthreads();
-  if (wk == 1) return;
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) load(c + 1);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] += red[wp][r][lane];
+    for (int s = 0; s < KSTEPS; ++s) {
+      const int kk = (wk * KSTEPS + s) * 2 + (lane >> 5);
+      acc = mfma32(Ws[buf][kk][wr * 32 + (lane & 31)], Xs[buf][kk][wc * 32 + (lane & 31)], acc);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  if (WM == 1) {   // sum the two K halves (LDS reused after the final barrier)
+    float* red = &Xs[0][0][0];   // [2 pixel halves][16][64]
+    if (wk == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wc * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wk == 1) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += red[(wc * 16 + r) * 64 + lane];
+  }
 
-  // ---- epilogue: element (o, p) with o = row, p = lane column
-  const long long pe = p0 + wp * 32 + (lane & 31);
+  const long long pe = p0 + wc * 32 + (lane & 31);
   if (pe >= P) return;
-  const int eb = (int)(pe / HW);
-  const size_t epix = (size_t)(pe % HW);
+  const int eb = (int)(pe / (long long)HW);
+  const size_t epix = (size_t)(pe - (long long)eb * HW);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int o = o0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (o >= g.Cout) continue;
-    float v = acc[r] + (a.bias ? a.bias[o] : 0.f);
-    v = a.alpha * act_fwd(v, ACT);
-    if (EPI == 1) {
-      const float z = a.z.p[((size_t)eb * a.z.ctot + a.z.coff + o) * HW + epix];
-      const float hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + o) * HW + epix];
-      if (a.q_out) a.q_out[((size_t)eb * a.q_ctot + a.q_coff + o) * HW + epix] = v;
-      v = (1.f - z) * hv + z * v;
+    const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row >= a.rows) continue;
+    if (MODE == 0) {
+      float v = acc[r] + (a.bias ? a.bias[row] : 0.f);
+      v = a.alpha * act_fwd(v, ACT);
+      if (EPI == 1) {
+        const float z = a.z.p[((size_t)eb * a.z.ctot + a.z.coff + row) * HW + epix];
+        const float hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + row) * HW + epix];
+        if (a.q_out) a.q_out[((size_t)eb * a.q_ctot + a.q_coff + row) * HW + epix] = v;
+        v = (1.f - z) * hv + z * v;
+      }
+      a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
+    } else {
+      int base = 0;
+      bool done = false;
+#pragma unroll
+      for (int i = 0; i < kMaxSrc; ++i) {
+        if (!done && i < a.nsrc && row < base + a.src[i].C) {
+          done = true;
+          float* dst = a.gsrc[i];
+          if (dst) {
+            float* q = dst + ((size_t)eb * a.gsrc_ctot[i] + a.gsrc_coff[i] + (row - base)) * HW + epix;
+            *q = a.gsrc_acc[i] ? (*q + acc[r]) : acc[r];
+          }
+        }
+        if (i < a.nsrc) base += a.src[i].C;
+      }
     }
-    a.out[((size_t)eb * a.out_ctot + a.out_coff + o) * HW + epix] = v;
   }
 }
 
-// ------------------------------------------------------------------ backward: data
-// din[c, p] = sum_{o,ky,kx} W[o,c,ky,kx] * G[o, p - (ky-PH, kx-PW)],
-// G = dout * act'(y).  Rows = input channels, cols = pixels, K = (o, tap).
-struct ConvBwdArgs {
-  ConvGeom g;
-  Slice src[kMaxSrc];           // forward inputs (for wgrad) -- and grad targets below
-  int nsrc;
-  Slice scale0;
-  const float* weight;
-  const float* dout;            // [B, Cout, H, W] upstream gradient (dense)
-  float alpha;                  // forward output scale
-  const float* y;               // saved activation output [B, Cout, H, W] (act != 0)
-  Slice y_slice;                // where y lives (dense if ctot == Cout)
-  // grad targets per source (dense [B, C_i, H, W] or slices), accumulate flags
-  float* gsrc[kMaxSrc];
-  int gsrc_ctot[kMaxSrc], gsrc_coff[kMaxSrc], gsrc_acc[kMaxSrc];
-  float* gweight;               // [Cout][Cin][KH][KW], accumulated (atomic)
-  float* gbias;                 // [Cout], accumulated (atomic)
-  int splits;                   // pixel splits of the weight-gradient reduction
-};
-
-__device__ __forceinline__ float grad_pre(const ConvBwdArgs& a, int act, int o, int b, size_t HW,
-                                          size_t pix) {
-  const float d = a.alpha * a.dout[((size_t)b * a.g.Cout + o) * HW + pix];
-  if (act == 0) return d;
-  const float yv = a.y_slice.p[((size_t)b * a.y_slice.ctot + a.y_slice.coff + o) * HW + pix];
-  return d * act_bwd(yv, act);
-}
-
-template <int ACT>
-__global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvBwdArgs a) {
-  __shared__ float Ws[kBK][kBO + 1];   // [k=(o,tap)][c]
-  __shared__ float Gs[kBK][kBP];   // [k][p]
-  __shared__ float red[2][16][64];
+// ------------------------------------------------------------------ weight (+ bias) gradient
+// dW[o, c, tap] = sum_p G[o, p] * X[c, p + d(tap)]: rows = o (64), cols = c (64)
+// at one tap, K = pixels of this split (chunks of 32).  Blocks whose column
+// tile is (tap 0, c-tile 0) also reduce db[o] = sum_p G[o, p].
+__global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
+  __shared__ float Gs[2][kBK][64 + 1];
+  __shared__ float Xs[2][kBK][64 + 1];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c0 = blockIdx.y * kBO, p0 = blockIdx.x * kBP;
+  const int t = blockIdx.x;
+  const int ot = t % a.otiles, rest = t / a.otiles;
+  const int ct = rest % a.ctiles, tap = rest / a.ctiles;
+  const int o0 = ot * 64, c0 = ct * 64;
+  const int ty = tap / g.KW, dy = ty - g.PH, dx = tap - ty * g.KW - g.PW;
   const size_t HW = (size_t)g.H * g.W;
   const long long P = (long long)g.B * HW;
-  const int T = g.KH * g.KW, K = g.Cout * T;
-  const long long pg = p0 + (tid & 63);
-  const bool pv = pg < P;
-  const int pb = pv ? (int)(pg / HW) : 0;
-  const int prem = pv ? (int)(pg % HW) : 0;
-  const int py = prem / g.W, px = prem % g.W;
+  const long long pbeg = (long long)blockIdx.y * a.pchunk;
+  const long long pend = pbeg + a.pchunk < P ? pbeg + a.pchunk : P;
+  const bool do_bias = a.gbias && tap == 0 && ct == 0;
+  // staging: 32 lanes along pixels (coalesced), 8 row groups
+  const int kp = tid & 31, hi = tid >> 5;
+  float gr[8], xr[8], bsum[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bsum[i] = 0.f;
+
+  auto load = [&](long long q0) {
+    const long long p = q0 + kp;
+    const bool v = p < pend;
+    const int b = v ? (int)(p / (long long)HW) : 0;
+    const int pix = v ? (int)(p - (long long)b * HW) : 0;
+    const int py = pix / g.W, px = pix - py * g.W;
+    const int yy = py + dy, xx = px + dx;
+    const bool inb = v && yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
+    const size_t off = inb ? (size_t)yy * g.W + xx : 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int o = o0 + hi + 8 * i;
+      gr[i] = (v && o < g.Cout) ? a.G[((size_t)b * g.Cout + o) * HW + pix] : 0.f;
+      const int c = c0 + hi + 8 * i;
+      xr[i] = (inb && c < g.Cin) ? src_val(a, c, b, HW, off) : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      Gs[buf][kp][hi + 8 * i] = gr[i];
+      Xs[buf][kp][hi + 8 * i] = xr[i];
+      if (do_bias) bsum[i] += gr[i];
+    }
+  };
+
+  const int wo = wave & 1, wc = wave >> 1;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int wp = wave & 1, wk = wave >> 1;
-  for (int k0 = 0; k0 < K; k0 += kBK) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kl = wave * 4 + i, k = k0 + kl;
-      float v = 0.f;
-      if (pv && k < K) {
-        const int o = k / T, tap = k - o * T;
-        const int yy = py - (tap / g.KW - g.PH), xx = px - (tap % g.KW - g.PW);
-        if (yy >= 0 && yy < g.H && xx >= 0 && xx < g.W)
-          v = grad_pre(a, ACT, o, pb, HW, (size_t)yy * g.W + xx);
-      }
-      Gs[kl][tid & 63] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cl = tid >> 3, kl = (tid & 7) * 2 + i, c = c0 + cl, k = k0 + kl;
-      float w = 0.f;
-      if (c < g.Cin && k < K) {
-        const int o = k / T, tap = k - o * T;
-        w = a.weight[((size_t)o * g.Cin + c) * T + tap];
-      }
-      Ws[kl][cl] = w;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int kl = wk * 8 + kk * 2 + (lane >> 5);
-      acc = mfma32(Ws[kl][lane & 31], Gs[kl][wp * 32 + (lane & 31)], acc);
-    }
-    __syncthreads();
-  }
-  if (wk == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[wp][r][lane] = acc[r];
+  if (pbeg < pend) {
+    load(pbeg);
+    store(0);
   }
   __syncthreads();
-  if (wk == 1) return;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] += red[wp][r][lane];
-  const long long pe = p0 + wp * 32 + (lane & 31);
-  if (pe >= P) return;
-  const int eb = (int)(pe / HW);
-  const size_t epix = (size_t)(pe % HW);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int c = c0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (c >= g.Cin) continue;
-    int base = 0, which = 0;
-    for (int i = 0; i < a.nsrc; ++i) {
-      if (c < base + a.src[i].C) {
-        which = i;
-        break;
-      }
-      base += a.src[i].C;
-    }
-    float* dst = a.gsrc[which];
-    if (!dst) continue;
-    float* q = dst + ((size_t)eb * a.gsrc_ctot[which] + a.gsrc_coff[which] + (c - base)) * HW + epix;
-    *q = a.gsrc_acc[which] ? (*q + acc[r]) : acc[r];
-  }
-}
-
-// ------------------------------------------------------------------ backward: weights
-// dW[o, k=(c,tap)] = sum_p G[o,p] * X[k,p]; rows = o, cols = k, reduction over
-// pixels split across gridDim.z (fp32 atomics into the zeroed dW).  Wave w:
-// k columns [32*(w&1), +32), pixel half (w>>1) of every chunk.
-template <int ACT>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvBwdArgs a) {
-  __shared__ float Gs[kBK][kBO + 1];   // [p][o]
-  __shared__ float Xs[kBK][kBP + 1];   // [p][k]
-  __shared__ float red[2][16][64];
-  const ConvGeom& g = a.g;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kt0 = blockIdx.x * kBP, o0 = blockIdx.y * kBO;
-  const size_t HW = (size_t)g.H * g.W;
-  const long long P = (long long)g.B * HW;
-  const int T = g.KH * g.KW, K = g.Cin * T;
-  const long long chunk = ((P + a.splits - 1) / a.splits + kBK - 1) / kBK * kBK;
-  const long long pbeg = (long long)blockIdx.z * chunk;
-  const long long pend = pbeg + chunk < P ? pbeg + chunk : P;
-  // staging role: pixel-in-chunk pl (16 consecutive lanes = 16 consecutive
-  // pixels, coalesced) and 4 fixed k columns, decoded once
-  const int pl = tid & 15;
-  int kc[4], kdy[4], kdx[4];
-  bool kv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int kg = kt0 + (tid >> 4) * 4 + i;
-    kv[i] = kg < K;
-    kc[i] = kv[i] ? kg / T : 0;
-    const int tap = kv[i] ? kg - kc[i] * T : 0;
-    kdy[i] = tap / g.KW - g.PH;
-    kdx[i] = tap % g.KW - g.PW;
-  }
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int wk = wave & 1, wp = wave >> 1;
+  int buf = 0;
   for (long long q0 = pbeg; q0 < pend; q0 += kBK) {
-    const long long p = q0 + pl;
-    const bool pvld = p < pend;
-    const int b = pvld ? (int)(p / HW) : 0, rem = pvld ? (int)(p % HW) : 0;
-    const int py = rem / g.W, px = rem % g.W;
+    const bool more = q0 + kBK < pend;
+    if (more) load(q0 + kBK);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float v = 0.f;
-      const int yy = py + kdy[i], xx = px + kdx[i];
-      if (pvld && kv[i] && yy >= 0 && yy < g.H && xx >= 0 && xx < g.W)
-        v = src_val(a.src, a.nsrc, a.scale0, kc[i], b, HW, (size_t)yy * g.W + xx);
-      Xs[pl][(tid >> 4) * 4 + i] = v;
+    for (int s = 0; s < 16; ++s) {
+      const int kk = s * 2 + (lane >> 5);
+      acc = mfma32(Gs[buf][kk][wo * 32 + (lane & 31)], Xs[buf][kk][wc * 32 + (lane & 31)], acc);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int ol = (tid >> 4) * 2 + i, o = o0 + ol;
-      float v = 0.f;
-      if (o < g.Cout && pvld) v = grad_pre(a, ACT, o, b, HW, (size_t)rem);
-      Gs[pl][ol] = v;
-    }
+    if (more) store(buf ^ 1);
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int pr = wp * 8 + kk * 2 + (lane >> 5);
-      acc = mfma32(Gs[pr][lane & 31], Xs[pr][wk * 32 + (lane & 31)], acc);
-    }
-    __syncthreads();
+    buf ^= 1;
   }
-  if (wp == 1) {
+  const int T = g.KH * g.KW;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[wk][r][lane] = acc[r];
+  for (int r = 0; r < 16; ++r) {
+    const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int c = c0 + wc * 32 + (lane & 31);
+    if (o < g.Cout && c < g.Cin) atomicAdd(a.gweight + ((size_t)o * g.Cin + c) * T + tap, acc[r]);
   }
-  __syncthreads();
-  if (wp == 0) {
+  if (do_bias) {
+    // lanes kp = 0..31 of each half-wave hold the same 8 output channels
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = acc[r] + red[wk][r][lane];
-      const int o = o0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int k = kt0 + wk * 32 + (lane & 31);
-      if (o < g.Cout && k < K) atomicAdd(a.gweight + (size_t)o * K + k, v);
+    for (int i = 0; i < 8; ++i) {
+      float v = bsum[i];
+#pragma unroll
+      for (int m = 16; m > 0; m >>= 1) v += __shfl_xor(v, m, 32);
+      const int o = o0 + hi + 8 * i;
+      if (kp == 0 && o < g.Cout) atomicAdd(a.gbias + o, v);
     }
   }
 }
 
-// bias gradient: db[o] = sum_p G[o,p] (one workgroup per output channel chunk)
-template <int ACT>
-__global__ __launch_bounds__(256) void conv_bgrad_kernel(ConvBwdArgs a) {
-  __shared__ float scratch[4];
-  const ConvGeom& g = a.g;
-  const int o = blockIdx.x;
-  const size_t HW = (size_t)g.H * g.W;
-  const long long P = (long long)g.B * HW;
-  float s = 0.f;
-  for (long long p = (long long)blockIdx.y * blockDim.x + threadIdx.x; p < P;
-       p += (long long)gridDim.y * blockDim.x)
-    s += grad_pre(a, ACT, o, (int)(p / HW), HW, (size_t)(p % HW));
-  float v[1] = {s};
-  block_sum<1>(v, scratch);
-  if (threadIdx.x == 0) atomicAdd(a.gbias + o, v[0]);
+// G = alpha * dout * act'(y) (only when act != none or alpha != 1)
+__global__ __launch_bounds__(256) void grad_pre_kernel(int act, float alpha, int Cout, size_t HW,
+                                                       size_t total, const float* __restrict__ dout,
+                                                       Slice y, float* __restrict__ G) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    float d = alpha * dout[i];
+    if (act) {
+      const size_t b = i / ((size_t)Cout * HW), rem = i - b * Cout * HW;
+      const size_t o = rem / HW, pix = rem - o * HW;
+      d *= act_bwd(y.p[(b * y.ctot + y.coff + o) * HW + pix], act);
+    }
+    G[i] = d;
+  }
 }
 
 }  // namespace dro
@@ -403,7 +380,7 @@ namespace {
 int conv_setup_geom(ConvGeom& g, const dro_slice* srcs, int nsrc, int B, int H, int W, int Cout,
                     int KH, int KW) {
   if (!srcs || nsrc < 1 || nsrc > kMaxSrc) {
-    set_error("conv2d: need 1..3 input slices");
+    set_error("conv2d: need 1..4 input slices");
     return DRO_E_SHAPE;
   }
   int cin = 0;
@@ -419,7 +396,8 @@ int conv_setup_geom(ConvGeom& g, const dro_slice* srcs, int nsrc, int B, int H, 
     }
     cin += srcs[i].channels;
   }
-  if (B < 1 || H < 1 || W < 1 || Cout < 1 || KH < 1 || KW < 1 || (KH % 2) == 0 || (KW % 2) == 0) {
+  if (B < 1 || H < 1 || W < 1 || Cout < 1 || KH < 1 || KW < 1 || (KH % 2) == 0 || (KW % 2) == 0 ||
+      (long long)B * H * W > (1LL << 30)) {
     set_error("conv2d: sizes out of range (odd kernels, 'same' padding, stride 1)");
     return DRO_E_SHAPE;
   }
@@ -445,6 +423,25 @@ Slice to_slice(const dro_slice* s) {
   return r;
 }
 
+// 64-row tiles when they alone give ~2 blocks per CU, else 32-row tiles
+bool use_bm64(int rows, long long P) {
+  const long long ptiles = (P + kBN - 1) / kBN;
+  return ((rows + 63) / 64) * ptiles >= 448;
+}
+
+template <int MODE, int ACT, int EPI>
+int launch_igemm(IgArgs& a, long long P, hipStream_t s) {
+  const int ptiles = (int)((P + kBN - 1) / kBN);
+  if (use_bm64(a.rows, P)) {
+    a.row_tiles = (a.rows + 63) / 64;
+    hipLaunchKernelGGL((igemm_kernel<64, MODE, ACT, EPI>), dim3(a.row_tiles * ptiles), dim3(256), 0, s, a);
+  } else {
+    a.row_tiles = (a.rows + 31) / 32;
+    hipLaunchKernelGGL((igemm_kernel<32, MODE, ACT, EPI>), dim3(a.row_tiles * ptiles), dim3(256), 0, s, a);
+  }
+  return launch_status("igemm_kernel launch failed");
+}
+
 }  // namespace
 
 #define DRO_ACT_SWITCH(act, ...)                  \
@@ -460,12 +457,16 @@ extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_sli
                                   const float* weight, const float* bias, int B, int H, int W,
                                   int Cout, int KH, int KW, int act, float alpha, float* out,
                                   int out_ctot, int out_coff, void* stream) {
-  ConvFwdArgs a = {};
+  IgArgs a = {};
   int st = conv_setup_geom(a.g, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
   if (!weight || !out || out_coff < 0 || out_coff + Cout > out_ctot) {
     set_error("conv2d_forward: NULL weight/out or bad output slice");
     return DRO_E_NULL;
+  }
+  if (alpha != 1.f && act != 0) {
+    set_error("conv2d_forward: alpha != 1 requires act none");
+    return DRO_E_MODE;
   }
   for (int i = 0; i < nsrc; ++i) a.src[i] = to_slice(srcs + i);
   a.nsrc = nsrc;
@@ -473,18 +474,15 @@ extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_sli
   a.weight = weight;
   a.bias = bias;
   a.alpha = alpha;
-  if (alpha != 1.f && act != 0) {
-    set_error("conv2d_forward: alpha != 1 requires act none");
-    return DRO_E_MODE;
-  }
   a.out = out;
   a.out_ctot = out_ctot;
   a.out_coff = out_coff;
+  a.rows = Cout;
+  a.kch = a.g.Cin;
   const long long P = (long long)B * H * W;
-  dim3 grid((unsigned)((P + kBP - 1) / kBP), (Cout + kBO - 1) / kBO);
   hipStream_t s = (hipStream_t)stream;
-  DRO_ACT_SWITCH(act, hipLaunchKernelGGL((conv_fwd_kernel<A_, 0>), grid, dim3(256), 0, s, a));
-  return launch_status("conv_fwd_kernel launch failed");
+  DRO_ACT_SWITCH(act, st = (launch_igemm<0, A_, 0>(a, P, s)));
+  return st;
 }
 
 extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
@@ -492,7 +490,7 @@ extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const 
                                          int W, int Cout, int KH, int KW, const dro_slice* z,
                                          const dro_slice* h, float* q_out, int q_ctot, int q_coff,
                                          float* out, int out_ctot, int out_coff, void* stream) {
-  ConvFwdArgs a = {};
+  IgArgs a = {};
   int st = conv_setup_geom(a.g, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
   if (!weight || !out || !z || !h || !z->data || !h->data) {
@@ -513,25 +511,29 @@ extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const 
   a.q_out = q_out;
   a.q_ctot = q_ctot;
   a.q_coff = q_coff;
-  const long long P = (long long)B * H * W;
-  dim3 grid((unsigned)((P + kBP - 1) / kBP), (Cout + kBO - 1) / kBO);
-  hipLaunchKernelGGL((conv_fwd_kernel<3, 1>), grid, dim3(256), 0, (hipStream_t)stream, a);
-  return launch_status("conv_fwd_kernel<blend> launch failed");
+  a.rows = Cout;
+  a.kch = a.g.Cin;
+  return launch_igemm<0, 3, 1>(a, (long long)B * H * W, (hipStream_t)stream);
 }
 
 extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
                                    const float* weight, int B, int H, int W, int Cout, int KH,
                                    int KW, int act, float alpha, const dro_slice* y,
-                                   const float* dout,
+                                   const float* dout, float* workspace,
                                    float* const* grad_srcs, const int* grad_ctot,
                                    const int* grad_coff, const int* grad_accumulate,
                                    float* grad_weight, float* grad_bias, void* stream) {
-  ConvBwdArgs a = {};
+  IgArgs a = {};
   int st = conv_setup_geom(a.g, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
-  if (!weight || !dout || (act != 0 && (!y || !y->data))) {
-    set_error("conv2d_backward: NULL weight/dout/y");
+  const bool pre = act != 0 || alpha != 1.f;
+  if (!weight || !dout || (act != 0 && (!y || !y->data)) || (pre && !workspace)) {
+    set_error("conv2d_backward: NULL weight/dout/y/workspace");
     return DRO_E_NULL;
+  }
+  if (act < 0 || act > 3) {
+    set_error("conv2d_backward: unknown activation");
+    return DRO_E_MODE;
   }
   for (int i = 0; i < nsrc; ++i) {
     a.src[i] = to_slice(srcs + i);
@@ -543,47 +545,58 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_sl
   a.nsrc = nsrc;
   a.scale0 = to_slice(scale0);
   a.weight = weight;
-  a.dout = dout;
-  a.alpha = alpha;
-  a.y_slice = to_slice(y);
   a.gweight = grad_weight;
   a.gbias = grad_bias;
   hipStream_t s = (hipStream_t)stream;
-  const long long P = (long long)B * H * W;
-  const int K = a.g.Cin * KH * KW;
+  const size_t HW = (size_t)H * W;
+  const long long P = (long long)B * HW;
+  if (pre) {
+    const size_t total = (size_t)Cout * P;
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(grad_pre_kernel, dim3((unsigned)blocks), dim3(256), 0, s, act, alpha, Cout, HW,
+                       total, dout, to_slice(y), workspace);
+    if ((st = launch_status("grad_pre_kernel launch failed"))) return st;
+    a.G = workspace;
+  } else {
+    a.G = dout;
+  }
   bool any_dgrad = false;
   for (int i = 0; i < nsrc; ++i) any_dgrad |= a.gsrc[i] != nullptr;
   if (any_dgrad) {
-    dim3 grid((unsigned)((P + kBP - 1) / kBP), (a.g.Cin + kBO - 1) / kBO);
-    DRO_ACT_SWITCH(act, hipLaunchKernelGGL((conv_dgrad_kernel<A_>), grid, dim3(256), 0, s, a));
-    if ((st = launch_status("conv_dgrad_kernel launch failed"))) return st;
+    a.rows = a.g.Cin;
+    a.kch = Cout;
+    if ((st = launch_igemm<1, 0, 0>(a, P, s))) return st;
   }
-  if (grad_weight) {
-    if ((st = launch_zero(grad_weight, (size_t)Cout * K, s))) return st;
-    const int ktiles = (K + kBP - 1) / kBP, otiles = (Cout + kBO - 1) / kBO;
-    int splits = (int)((512 + ktiles * otiles - 1) / (ktiles * otiles));
-    const long long maxs = (P + 63) / 64;
-    if (splits > maxs) splits = (int)maxs;
+  if (grad_weight || grad_bias) {
+    if (!grad_weight) {
+      set_error("conv2d_backward: grad_bias requires grad_weight");
+      return DRO_E_NULL;
+    }
+    const int T = KH * KW;
+    if ((st = launch_zero(grad_weight, (size_t)Cout * a.g.Cin * T, s))) return st;
+    if (grad_bias && (st = launch_zero(grad_bias, (size_t)Cout, s))) return st;
+    a.otiles = (Cout + 63) / 64;
+    a.ctiles = (a.g.Cin + 63) / 64;
+    const long long tiles = (long long)a.otiles * a.ctiles * T;
+    long long splits = (768 + tiles - 1) / tiles;
+    const long long maxs = (P + 4 * kBK - 1) / (4 * kBK);   // >= 4 chunks per split
+    if (splits > maxs) splits = maxs;
     if (splits < 1) splits = 1;
-    a.splits = splits;
-    dim3 grid(ktiles, otiles, splits);
-    DRO_ACT_SWITCH(act, hipLaunchKernelGGL((conv_wgrad_kernel<A_>), grid, dim3(256), 0, s, a));
-    if ((st = launch_status("conv_wgrad_kernel launch failed"))) return st;
-  }
-  if (grad_bias) {
-    if ((st = launch_zero(grad_bias, (size_t)Cout, s))) return st;
-    dim3 grid(Cout, 8);
-    DRO_ACT_SWITCH(act, hipLaunchKernelGGL((conv_bgrad_kernel<A_>), grid, dim3(256), 0, s, a));
-    if ((st = launch_status("conv_bgrad_kernel launch failed"))) return st;
+    a.pchunk = ((P + splits - 1) / splits + kBK - 1) / kBK * kBK;
+    splits = (P + a.pchunk - 1) / a.pchunk;
+    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, s, a);
+    if ((st = launch_status("wgrad_kernel launch failed"))) return st;
   }
   return DRO_OK;
 }
 
 // ------------------------------------------------------------------ SepConvGRU elementwise backward
-// update.py:67-70 (and :74-77): h' = (1-z) h + z q, q = tanh(.), rh = r * h.
-// stage 1 (before the q-gate backward):  dq = dh' * z;  dz = dh' * (q - h);  dh = dh' * (1 - z)
-// stage 2 (after it, drh = dL/d(r*h)):   dr = drh * h;  dh += drh * r
-// z = zr[:, :hd], r = zr[:, hd:], dz / dr written into dzr likewise.
+// update.py:67-70 (and :74-77): h' = (1-z) h + z q, q = tanh(.), z, r = sigmoid(.).
+// Outputs are gradients w.r.t. the PRE-activations, ready for the conv backward:
+// stage 1: dq~ = dh' z (1-q^2);  dz~ = dh' (q-h) z (1-z);  dh = dh' (1-z)
+// stage 2 (after the q-gate backward, drh = dL/d(r*h)):  dr~ = drh h r (1-r);  dh += drh r
+// z = zr[:, :hd], r = zr[:, hd:], dz~ / dr~ written into dzr likewise.
 namespace dro {
 __global__ __launch_bounds__(256) void gru_elem_kernel(int stage, int hd, size_t HW, size_t total,
                                                        const float* __restrict__ dhn,
@@ -596,17 +609,17 @@ __global__ __launch_bounds__(256) void gru_elem_kernel(int stage, int hd, size_t
                                                        float* __restrict__ dh) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const size_t b = i / ((size_t)hd * HW), rem = i % ((size_t)hd * HW);
+    const size_t b = i / ((size_t)hd * HW), rem = i - b * hd * HW;
     const size_t zi = b * 2 * hd * HW + rem, ri = zi + (size_t)hd * HW;
     if (stage == 1) {
-      const float g = dhn[i], z = zr[zi];
-      dq[i] = g * z;
-      dzr[zi] = g * (q[i] - h[i]);
-      dh[i] = g * (1.f - z);
+      const float gn = dhn[i], z = zr[zi], qv = q[i], hv = h[i];
+      dq[i] = gn * z * (1.f - qv * qv);
+      dzr[zi] = gn * (qv - hv) * z * (1.f - z);
+      dh[i] = gn * (1.f - z);
     } else {
-      const float d = drh[i];
-      dzr[ri] = d * h[i];
-      dh[i] += d * zr[ri];
+      const float d = drh[i], r = zr[ri];
+      dzr[ri] = d * h[i] * r * (1.f - r);
+      dh[i] += d * r;
     }
   }
 }

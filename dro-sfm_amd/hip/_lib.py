@@ -49,7 +49,7 @@ def load():
     _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, P, P, S)
     _sig(lib.dro_conv2d_forward, P, I, P, P, P, I, I, I, I, I, I, I, F, P, I, I, S)
     _sig(lib.dro_convgru_blend_forward, P, I, P, P, P, I, I, I, I, I, I, P, P, P, I, I, P, I, I, S)
-    _sig(lib.dro_conv2d_backward, P, I, P, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, S)
+    _sig(lib.dro_conv2d_backward, P, I, P, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, P, S)
     _sig(lib.dro_gru_backward_elem, I, I, I, I, I, P, P, P, P, P, P, P, P, S)
     _lib = lib
     return lib

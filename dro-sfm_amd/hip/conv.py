@@ -89,9 +89,10 @@ class _Conv2d(torch.autograd.Function):
         ptrs, ctot, coff = _grad_targets(gsrc)
         acc = (ctypes.c_int * len(srcs))()
         ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
+        ws = torch.empty_like(gout) if (act or alpha != 1.0) else None
         check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), None, ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb),
+                                      ptr(gout), ptr(ws), ptrs, ctot, coff, acc, ptr(gw), ptr(gb),
                                       stream_of(gout)), "dro_conv2d_backward")
         return (gw, gb, None, None, *gsrc)
 
@@ -142,7 +143,7 @@ class _SepGRUHalf(torch.autograd.Function):
         KH, KW = wq.shape[2:]
         st = stream_of(h)
         dhn = dhn.contiguous()
-        dq, dh = torch.empty_like(h), torch.empty_like(h)
+        dq, dh = torch.empty_like(h), torch.empty_like(h)     # dq, dzr: pre-activation grads
         dzr = torch.empty_like(zr)
         check(lib.dro_gru_backward_elem(1, B, hd, H, W, ptr(dhn), ptr(zr), ptr(q), ptr(h), None, ptr(dq),
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(1)")
@@ -156,18 +157,16 @@ class _SepGRUHalf(torch.autograd.Function):
         gwq, gbq = torch.empty_like(wq), torch.empty(hd, device=h.device)
         ptrs, ctot, coff = _grad_targets([drh, *dxs])
         acc = (ctypes.c_int * len(srcs))()
-        q_sl = DroSlice(q.data_ptr(), hd, hd, 0, 0)
         check(lib.dro_conv2d_backward(arr, len(srcs), ctypes.byref(r_sl), ptr(wq), B, H, W, hd, KH, KW,
-                                      ACT["tanh"], ctypes.c_float(1.0), ctypes.byref(q_sl), ptr(dq), ptrs,
+                                      0, ctypes.c_float(1.0), None, ptr(dq), None, ptrs,
                                       ctot, coff, acc, ptr(gwq), ptr(gbq), st), "dro_conv2d_backward(q)")
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
         gwzr, gbzr = torch.empty_like(wzr), torch.empty(2 * hd, device=h.device)
         ptrs, ctot, coff = _grad_targets([dh, *dxs])
         acc = (ctypes.c_int * len(srcs))(*([1] * len(srcs)))
-        zr_sl = DroSlice(zr.data_ptr(), 2 * hd, 2 * hd, 0, 0)
         check(lib.dro_conv2d_backward(arr, len(srcs), None, ptr(wzr), B, H, W, 2 * hd, KH, KW,
-                                      ACT["sigmoid"], ctypes.c_float(1.0), ctypes.byref(zr_sl), ptr(dzr),
+                                      0, ctypes.c_float(1.0), None, ptr(dzr), None,
                                       ptrs, ctot, coff, acc, ptr(gwzr), ptr(gbzr), st),
               "dro_conv2d_backward(zr)")
         return (dh if need[0] else None, gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:], gwq, gbq, *dxs)

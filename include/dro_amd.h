@@ -144,7 +144,7 @@ int dro_convex_upsample_backward(const float* inv, const float* mask, const floa
  * Cin = sum of slice channels; odd KH, KW; padding KH/2, KW/2.
  * act: 0 none, 1 relu, 2 sigmoid, 3 tanh, applied in the epilogue after bias,
  * then the result is multiplied by alpha (alpha != 1 only with act none: the
- * 0.25-scaled mask heads, update.py:153).  Up to 4 input slices.
+ * 0.25-scaled mask heads, update.py:153).  1..4 input slices.
  * The output goes to channels [out_coff, out_coff+Cout) of a [B,out_ctot,H,W]
  * tensor.
  * ---------------------------------------------------------------------- */
@@ -177,23 +177,29 @@ int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const dro_slice* 
                               int out_coff, void* stream);
 
 /* Gradients of dro_conv2d_forward given dout [B,Cout,H,W] (dense) and, for
- * act != 0, the saved activation output y.  grad_srcs[i] (nullable) receives
- * d/d(source i) -- for a scaled source 0, the gradient w.r.t. the SCALED values
- * -- into channels [grad_coff[i], +C_i) of a [B, grad_ctot[i], H, W] tensor,
- * overwritten or added (grad_accumulate[i]); a broadcast source receives its
- * per-pixel gradient (the caller sums over H x W).  grad_weight / grad_bias
- * (nullable) are overwritten. */
+ * act != 0, the saved activation output y.  When act != 0 or alpha != 1 the
+ * pre-activation gradient alpha*dout*act'(y) is formed first in `workspace`
+ * (B*Cout*H*W floats; may be NULL otherwise).  grad_srcs[i] (nullable)
+ * receives d/d(source i) -- for a scaled source 0, the gradient w.r.t. the
+ * SCALED values -- into channels [grad_coff[i], +C_i) of a
+ * [B, grad_ctot[i], H, W] tensor, overwritten or added (grad_accumulate[i]);
+ * a broadcast source receives its per-pixel gradient (the caller sums over
+ * H x W).  grad_weight / grad_bias (nullable; grad_bias needs grad_weight)
+ * are overwritten.  Weight gradients are split over pixels and summed with
+ * f32 atomics (order-dependent in the last bits). */
 int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
                         const float* weight, int B, int H, int W, int Cout, int KH, int KW,
                         int act, float alpha, const dro_slice* y, const float* dout,
-                        float* const* grad_srcs, const int* grad_ctot, const int* grad_coff,
-                        const int* grad_accumulate, float* grad_weight, float* grad_bias,
-                        void* stream);
+                        float* workspace, float* const* grad_srcs, const int* grad_ctot,
+                        const int* grad_coff, const int* grad_accumulate, float* grad_weight,
+                        float* grad_bias, void* stream);
 
 /* SepConvGRU backward, elementwise parts (update.py:67-70): with zr the saved
- * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W]:
- *   stage 1: dq = dh'*z; dzr[:, :hd] = dh'*(q-h); dh = dh'*(1-z)
- *   stage 2: dzr[:, hd:] = drh*h; dh += drh*r        (drh = dL/d(r*h)) */
+ * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W].
+ * Outputs are gradients w.r.t. the gates' PRE-activations (feed them to
+ * dro_conv2d_backward with act = DRO_ACT_NONE):
+ *   stage 1: dq = dh' z (1-q^2); dzr[:, :hd] = dh' (q-h) z (1-z); dh = dh' (1-z)
+ *   stage 2: dzr[:, hd:] = drh h r (1-r); dh += drh r     (drh = dL/d(r*h)) */
 int dro_gru_backward_elem(int stage, int B, int hd, int H, int W, const float* dhn,
                           const float* zr, const float* q, const float* h, const float* drh,
                           float* dq, float* dzr, float* dh, void* stream);
