@@ -49,6 +49,18 @@ def _grad_targets(bufs):
     return ptrs, ctot, coff
 
 
+_WS = {}
+
+
+def _workspace(B, H, W, Cin, Cout, KH, KW, device):
+    """Scratch for one conv call (torch caching allocator: graph-capture safe)."""
+    key = (B, H, W, Cin, Cout, KH, KW)
+    n = _WS.get(key)
+    if n is None:
+        n = _WS[key] = int(_lib.load().dro_conv2d_workspace_bytes(B, H, W, Cin, Cout, KH, KW))
+    return torch.empty(max(n, 1), dtype=torch.uint8, device=device), n
+
+
 def _dense_out(srcs, C):
     B, _, H, W = srcs[0].shape
     return torch.empty(B, C, H, W, device=srcs[0].device, dtype=torch.float32)
@@ -66,9 +78,10 @@ class _Conv2d(torch.autograd.Function):
         weight = weight.contiguous()
         out = _dense_out(srcs, Cout)
         arr = _slices(srcs)
+        ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, out.device)
         check(lib.dro_conv2d_forward(arr, len(srcs), None, ptr(weight), ptr(bias), B, H, W, Cout, KH, KW,
-                                     act, ctypes.c_float(alpha), ptr(out), Cout, 0, stream_of(out)),
-              "dro_conv2d_forward")
+                                     act, ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(ws), nws,
+                                     stream_of(out)), "dro_conv2d_forward")
         ctx.save_for_backward(weight, out if act else None, *srcs)
         ctx.meta = (act, alpha, bias is not None)
         return out
@@ -89,10 +102,10 @@ class _Conv2d(torch.autograd.Function):
         ptrs, ctot, coff = _grad_targets(gsrc)
         acc = (ctypes.c_int * len(srcs))()
         ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
-        ws = torch.empty_like(gout) if (act or alpha != 1.0) else None
+        ws, nws = _workspace(B, H, W, weight.shape[1], Cout, KH, KW, gout.device)
         check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), None, ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                      ptr(gout), ptr(ws), ptrs, ctot, coff, acc, ptr(gw), ptr(gb),
+                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), ptr(ws), nws,
                                       stream_of(gout)), "dro_conv2d_backward")
         return (gw, gb, None, None, *gsrc)
 
@@ -120,18 +133,22 @@ class _SepGRUHalf(torch.autograd.Function):
         srcs = [h, *xs]
         arr = _slices(srcs)
         st = stream_of(h)
+        cin = wz.shape[1]
         zr = torch.empty(B, 2 * hd, H, W, device=h.device)
+        ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_forward(arr, len(srcs), None, ptr(wzr), ptr(bzr), B, H, W, 2 * hd, KH, KW,
-                                     ACT["sigmoid"], ctypes.c_float(1.0), ptr(zr), 2 * hd, 0, st),
-              "dro_conv2d_forward(zr)")
+                                     ACT["sigmoid"], ctypes.c_float(1.0), ptr(zr), 2 * hd, 0, ptr(ws), nws,
+                                     st), "dro_conv2d_forward(zr)")
         q = torch.empty_like(h)
         hn = torch.empty_like(h)
         r_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, hd, 0)
         z_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, 0, 0)
         h_sl = DroSlice(h.data_ptr(), hd, hd, 0, 0)
+        wsq, nwsq = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_convgru_blend_forward(arr, len(srcs), ctypes.byref(r_sl), ptr(wq), ptr(bq), B, H, W,
                                             hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl), ptr(q),
-                                            hd, 0, ptr(hn), hd, 0, st), "dro_convgru_blend_forward")
+                                            hd, 0, ptr(hn), hd, 0, ptr(wsq), nwsq, st),
+              "dro_convgru_blend_forward")
         ctx.save_for_backward(h, wzr, wq, zr, q, *xs)
         return hn
 
@@ -157,17 +174,20 @@ class _SepGRUHalf(torch.autograd.Function):
         gwq, gbq = torch.empty_like(wq), torch.empty(hd, device=h.device)
         ptrs, ctot, coff = _grad_targets([drh, *dxs])
         acc = (ctypes.c_int * len(srcs))()
+        cin = wq.shape[1]
+        ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(arr, len(srcs), ctypes.byref(r_sl), ptr(wq), B, H, W, hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dq), None, ptrs,
-                                      ctot, coff, acc, ptr(gwq), ptr(gbq), st), "dro_conv2d_backward(q)")
+                                      0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
+                                      ptr(gwq), ptr(gbq), ptr(ws), nws, st), "dro_conv2d_backward(q)")
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
         gwzr, gbzr = torch.empty_like(wzr), torch.empty(2 * hd, device=h.device)
         ptrs, ctot, coff = _grad_targets([dh, *dxs])
         acc = (ctypes.c_int * len(srcs))(*([1] * len(srcs)))
+        ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(arr, len(srcs), None, ptr(wzr), B, H, W, 2 * hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dzr), None,
-                                      ptrs, ctot, coff, acc, ptr(gwzr), ptr(gbzr), st),
+                                      0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
+                                      ptr(gwzr), ptr(gbzr), ptr(ws), nws, st),
               "dro_conv2d_backward(zr)")
         return (dh if need[0] else None, gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:], gwq, gbq, *dxs)
 

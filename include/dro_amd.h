@@ -162,10 +162,16 @@ typedef struct dro_slice {
 #define DRO_ACT_SIGMOID 2
 #define DRO_ACT_TANH 3
 
+/* Scratch needed by any of the three calls below for this shape (split-K
+ * partials, weight-gradient partials, the pre-activation gradient); pass a
+ * device buffer of at least this size as `workspace`.  No call keeps state in
+ * it, and every result is bitwise run-to-run deterministic (no atomics). */
+size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int Cout, int KH, int KW);
+
 int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
                        const float* weight, const float* bias, int B, int H, int W, int Cout,
                        int KH, int KW, int act, float alpha, float* out, int out_ctot,
-                       int out_coff, void* stream);
+                       int out_coff, void* workspace, size_t workspace_bytes, void* stream);
 
 /* SepConvGRU gate q with the blend fused (update.py:69-70 / :76-77):
  * q = tanh(conv(srcs) + bias); out = (1 - z) * h + z * q; q also stored to
@@ -174,25 +180,23 @@ int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const dro_slice* 
                               const float* weight, const float* bias, int B, int H, int W,
                               int Cout, int KH, int KW, const dro_slice* z, const dro_slice* h,
                               float* q_out, int q_ctot, int q_coff, float* out, int out_ctot,
-                              int out_coff, void* stream);
+                              int out_coff, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Gradients of dro_conv2d_forward given dout [B,Cout,H,W] (dense) and, for
- * act != 0, the saved activation output y.  When act != 0 or alpha != 1 the
- * pre-activation gradient alpha*dout*act'(y) is formed first in `workspace`
- * (B*Cout*H*W floats; may be NULL otherwise).  grad_srcs[i] (nullable)
+ * act != 0, the saved activation output y (the pre-activation gradient
+ * alpha*dout*act'(y) is formed in the workspace).  grad_srcs[i] (nullable)
  * receives d/d(source i) -- for a scaled source 0, the gradient w.r.t. the
  * SCALED values -- into channels [grad_coff[i], +C_i) of a
  * [B, grad_ctot[i], H, W] tensor, overwritten or added (grad_accumulate[i]);
  * a broadcast source receives its per-pixel gradient (the caller sums over
  * H x W).  grad_weight / grad_bias (nullable; grad_bias needs grad_weight)
- * are overwritten.  Weight gradients are split over pixels and summed with
- * f32 atomics (order-dependent in the last bits). */
+ * are overwritten. */
 int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
                         const float* weight, int B, int H, int W, int Cout, int KH, int KW,
                         int act, float alpha, const dro_slice* y, const float* dout,
-                        float* workspace, float* const* grad_srcs, const int* grad_ctot,
-                        const int* grad_coff, const int* grad_accumulate, float* grad_weight,
-                        float* grad_bias, void* stream);
+                        float* const* grad_srcs, const int* grad_ctot, const int* grad_coff,
+                        const int* grad_accumulate, float* grad_weight, float* grad_bias,
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* SepConvGRU backward, elementwise parts (update.py:67-70): with zr the saved
  * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W].

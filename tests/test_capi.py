@@ -68,6 +68,10 @@ def test_bad_sizes_and_modes_rejected(lib):
 def test_workspace_sizes(lib):
     assert lib.dro_warp_cost_workspace_bytes(2, 2, 24, 80) >= 2 * 2 * 24 * 80 * 2 * 4
     assert lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640) >= 9 * 2 * 192 * 640
+    # conv: at least the pre-activation gradient and the weight-gradient partials
+    P = 2 * 24 * 80
+    assert lib.dro_conv2d_workspace_bytes(2, 24, 80, 320, 256, 1, 5) >= 256 * P * 4 + 256 * 320 * 5 * 4
+    assert lib.dro_conv2d_workspace_bytes(0, 24, 80, 320, 256, 1, 5) == 0
 
 
 def test_no_cpu_fallback():
