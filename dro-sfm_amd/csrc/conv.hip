@@ -7,11 +7,11 @@
 // activation / concat are separate ATen kernels, and its forward is not
 // run-to-run deterministic.  Here:
 //   * inputs are a VIRTUAL channel concatenation of up to 4 tensor slices (no
-//     torch.cat), optionally with source 0 multiplied elementwise by another
-//     slice (the GRU's r*h) while it is staged; a source may be a [B,C,1,1]
-//     map broadcast over the image (the pose map);
-//   * bias + activation (+ the GRU blend h' = (1-z)h + zq) run in the epilogue,
-//     and the result lands in a channel slice of a bigger tensor;
+//     torch.cat); a source may be a [B,C,1,1] map broadcast over the image
+//     (the pose map of ProjectionInputPose);
+//   * bias + activation run in the epilogue, plus two SepConvGRU epilogues:
+//     the z|r gate conv also writes r*h, and the q conv writes the blended
+//     state h' = (1-z)h + zq; results land in a channel slice of a tensor;
 //   * f32 MFMA is exact f32 (a k-ordered fmaf chain): no TF32-style loss;
 //   * no atomics: split reductions go through a workspace and are summed in a
 //     fixed order, so every result is bitwise run-to-run deterministic.
@@ -19,18 +19,24 @@
 // GEMM view (forward): rows = output channels, cols = pixels (B*H*W flattened),
 // K = (tap, input channel) flattened TAP-MAJOR (k = tap*Cin + c), 32-deep
 // chunks.  Each K row of a chunk is staged by one wave, so its (tap, channel,
-// source) decode is wave-uniform; lanes run along pixels (coalesced).
+// source) decode is wave-uniform scalar work; lanes run along pixels.
 // Data gradient: the same kernel with rows = input channels, K = (tap, output
 // channel), the tap offset negated and the weight read transposed.
-// Weight gradient: rows = output channels, cols = (tap, input channel),
-// K = pixels split over gridDim.y into per-split partials.
-// Pipeline: global -> registers for chunk c+1 is issued before the MFMAs of
-// chunk c (two LDS buffers, one barrier per chunk).  Tiles are remapped so
-// that blocks sharing a pixel tile run on the same XCD (same L2).  Shapes with
-// few output tiles and a long K split K over gridDim.y (partials + finish).
+// Weight gradient: rows = output channels, cols = (tap, input channel) plus a
+// ones column that yields the bias gradient, K = pixels split over gridDim.y
+// into per-split partials.
+// Staging: every load of a chunk is issued unconditionally from a clamped
+// address (a load under a branch, or one whose value is consumed at once,
+// serialises the chunk), global -> registers for chunk c+1 before the MFMAs of
+// chunk c, two LDS buffers, one barrier per chunk.  Tiles are remapped so that
+// blocks sharing a pixel tile run on the same XCD (same L2).  Shapes with few
+// output tiles and a long K split K over gridDim.y (partials + finish).
 //
 // Roofline: MFMA(f32) at 157 TF/s; FLOPs per launch = 2 * Cout * P * Cin * KH * KW.
 #include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdio>
 
 #include "dro_common.hpp"
 
@@ -39,7 +45,8 @@ namespace dro {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBN = 64;   // pixels per tile (forward / data gradient)
-constexpr int kBK = 32;   // reduction chunk
+constexpr int kBK = 32;   // reduction chunk (forward / data gradient)
+constexpr int kWP = 64;   // pixels per weight-gradient chunk
 constexpr int kMaxSrc = 4;
 
 struct Slice {            // channels [coff, coff+C) of a [B, ctot, H, W] tensor
@@ -48,12 +55,13 @@ struct Slice {            // channels [coff, coff+C) of a [B, ctot, H, W] tensor
   int bcast;              // 1: a [B, ctot, 1, 1] tensor broadcast over H x W
 };
 
-// exact n / d for 0 <= n < 2^16, 1 <= d < 2^12: (n * ceil(2^32/d)) >> 32
+// exact n / d for 0 <= n < 2^16, 1 <= d < 2^12: umulhi(n, ceil(2^32/d)), d = 1 apart
 struct FastDiv {
-  unsigned long long m;
+  unsigned m;
+  int one;
 };
 __device__ __forceinline__ int fdiv(int n, FastDiv f) {
-  return (int)(((unsigned long long)(unsigned)n * f.m) >> 32);
+  return f.one ? n : (int)__umulhi((unsigned)n, f.m);
 }
 
 struct ConvGeom {
@@ -62,17 +70,16 @@ struct ConvGeom {
 
 struct IgArgs {
   ConvGeom g;
-  Slice src[kMaxSrc];     // forward inputs (virtual concat)
+  Slice src[kMaxSrc];     // forward inputs (virtual concat); read by index from the kernarg segment
   int cbase[kMaxSrc];     // first virtual channel of each source (Cin for unused)
-  Slice scale0;           // optional multiplier of source 0 (p == nullptr: none)
   const float* weight;    // [Cout][Cin][KH][KW]
   const float* bias;      // [Cout] or nullptr
   float alpha;            // output scale (act none only)
   float* out;             // forward output slice base
   int out_ctot, out_coff;
-  Slice z, h;             // GRU blend epilogue: out = (1-z) h + z q, q = tanh(acc+b)
-  float* q_out;           // optional: q saved for the backward
-  int q_ctot, q_coff;
+  Slice z, h;             // EPI 1: out = (1-z) h + z q, q = tanh(acc + b); EPI 2: h for r*h
+  float* aux;             // EPI 1: q (saved for the backward); EPI 2: r*h  (dense, [B, hd, H, W])
+  int hd;                 // EPI 2: rows >= hd are the r gate
   const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation
   float* gsrc[kMaxSrc];   // data-gradient targets per source (nullable)
   int gsrc_ctot[kMaxSrc], gsrc_coff[kMaxSrc], gsrc_acc[kMaxSrc];
@@ -84,8 +91,7 @@ struct IgArgs {
   FastDiv kdiv, kwdiv, cindiv;
   int row_tiles;          // tile = pixel_tile * row_tiles + row_tile
   int chunks_per_split;   // split-K (gridDim.y > 1): partials to `part`
-  float* part;            // [ksplit][rows][P] (igemm) / [splits][Cout][Cin*T] (wgrad)
-  float* bpart;           // [splits][Cout] (wgrad bias)
+  float* part;            // [ksplit][rows][P] (igemm) / [splits][Cout][NK+1] (wgrad)
   int otiles;             // weight gradient: output-channel tiles
   long long pchunk;       // weight gradient: pixels per split
 };
@@ -120,25 +126,36 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + local;
 }
 
-// one source's value (channel cl of slice s)
-__device__ __forceinline__ float slice_val(const Slice& s, int cl, int b, size_t HW, size_t off) {
-  const size_t ci = (size_t)b * s.ctot + s.coff + cl;
-  return s.bcast ? s.p[ci] : s.p[ci * HW + off];
+// The source descriptors are read straight from the kernel-argument segment
+// with a computed index (s_load for a wave-uniform channel).  Selecting among
+// struct fields instead gets rewritten by the compiler into a dynamically
+// indexed copy of the arguments in scratch.
+typedef __attribute__((address_space(4))) const Slice* KSlice;
+
+__device__ __forceinline__ KSlice kernarg_srcs() {
+  return (KSlice)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                  offsetof(IgArgs, src));
 }
 
-// virtual input at channel ch, image b, pixel offset off (caller checks
-// padding).  One branch (and load) per source with constant indices: a
-// select-then-load form gets rewritten into a dynamically indexed copy of the
-// kernel arguments in scratch.
-__device__ __forceinline__ float src_val(const IgArgs& a, int ch, int b, size_t HW, size_t off) {
-  if (ch < a.cbase[1]) {
-    float v = slice_val(a.src[0], ch, b, HW, off);
-    if (a.scale0.p) v *= a.scale0.p[((size_t)b * a.scale0.ctot + a.scale0.coff + ch) * HW + off];
-    return v;
-  }
-  if (ch < a.cbase[2]) return slice_val(a.src[1], ch - a.cbase[1], b, HW, off);
-  if (ch < a.cbase[3]) return slice_val(a.src[2], ch - a.cbase[2], b, HW, off);
-  return slice_val(a.src[3], ch - a.cbase[3], b, HW, off);
+// Element offset of virtual channel ch in its source is b * A + Bc + (M ? pixel : 0)
+// (broadcast sources: A = ctot, M = 0).  32-bit element offsets (checked on the host).
+struct RowDesc {
+  const float* p;
+  unsigned A, Bc;
+  bool M;
+};
+
+__device__ __forceinline__ RowDesc row_desc(int cb1, int cb2, int cb3, int ch, unsigned HW) {
+  const int si = (ch >= cb1) + (ch >= cb2) + (ch >= cb3);
+  const KSlice ks = kernarg_srcs() + si;
+  const int cl = ch - (si == 0 ? 0 : si == 1 ? cb1 : si == 2 ? cb2 : cb3);
+  const int ctot = ks->ctot, coff = ks->coff, bc = ks->bcast;
+  RowDesc d;
+  d.p = ks->p;
+  d.A = bc ? (unsigned)ctot : (unsigned)ctot * HW;
+  d.Bc = bc ? (unsigned)(coff + cl) : (unsigned)(coff + cl) * HW;
+  d.M = !bc;
+  return d;
 }
 
 __device__ __forceinline__ void grad_put(float* dst, int ctot, int coff, int accf, int cl, int eb,
@@ -158,12 +175,18 @@ __device__ __forceinline__ void epi_store(const IgArgs& a, int row, int eb, size
     if (EPI == 1) {
       const float z = a.z.p[((size_t)eb * a.z.ctot + a.z.coff + row) * HW + epix];
       const float hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + row) * HW + epix];
-      if (a.q_out) a.q_out[((size_t)eb * a.q_ctot + a.q_coff + row) * HW + epix] = v;
+      a.aux[((size_t)eb * a.rows + row) * HW + epix] = v;
       v = (1.f - z) * hv + z * v;
+    }
+    if (EPI == 2 && row >= a.hd) {
+      const int c = row - a.hd;
+      const float hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + c) * HW + epix];
+      a.aux[((size_t)eb * a.hd + c) * HW + epix] = v * hv;
     }
     a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
   } else {
-    if (row < a.cbase[1]) grad_put(a.gsrc[0], a.gsrc_ctot[0], a.gsrc_coff[0], a.gsrc_acc[0], row, eb, epix, HW, acc);
+    if (row < a.cbase[1])
+      grad_put(a.gsrc[0], a.gsrc_ctot[0], a.gsrc_coff[0], a.gsrc_acc[0], row, eb, epix, HW, acc);
     else if (row < a.cbase[2])
       grad_put(a.gsrc[1], a.gsrc_ctot[1], a.gsrc_coff[1], a.gsrc_acc[1], row - a.cbase[1], eb, epix, HW, acc);
     else if (row < a.cbase[3])
@@ -184,16 +207,22 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   constexpr int KSTEPS = (WM == 2) ? 16 : 8;          // MFMA k-steps per wave per chunk
   __shared__ float Ws[2][kBK][BM + 1];
   __shared__ float Xs[2][kBK][kBN];
-  const ConvGeom& g = a.g;
+  const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
+  const int H = a.g.H, W = a.g.W, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
+  const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch, K = a.K;
+  const FastDiv kdiv = a.kdiv, kwdiv = a.kwdiv;
+  const float* __restrict__ Wt = a.weight;
+  const float* __restrict__ Gp = a.G;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
   const int row0 = rt * BM;
   const long long p0 = (long long)pt * kBN;
-  const size_t HW = (size_t)g.H * g.W;
-  const long long P = (long long)g.B * HW;
-  const int T = g.KH * g.KW;
-  const int nchunks = (a.K + kBK - 1) / kBK;
+  const size_t HW = (size_t)H * W;
+  const unsigned HWu = (unsigned)HW;
+  const long long P = (long long)a.g.B * HW;
+  const int T = a.g.KH * KW;
+  const int nchunks = (K + kBK - 1) / kBK;
   const int cbeg = blockIdx.y * a.chunks_per_split;
   const int cend = min(nchunks, cbeg + a.chunks_per_split);
 
@@ -203,46 +232,54 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   const bool pv = pg < P;
   const int pb = pv ? (int)(pg / (long long)HW) : 0;
   const int prem = pv ? (int)(pg - (long long)pb * HW) : 0;
-  const int py = prem / g.W, px = prem - py * g.W;
+  const int py = prem / W, px = prem - py * W;
   const int wkl = tid & 31, wrow = tid >> 5;
 
   float xr[8], wv[BM / 8];
+  unsigned xmask = 0, wmask = 0;
   auto load = [&](int chunk) {
     const int k0 = chunk * kBK;
+    xmask = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      // row decode: wave-uniform (scalar)
       const int k = __builtin_amdgcn_readfirstlane(k0 + krow + 4 * i);
-      float v = 0.f;
-      if (k < a.K) {
-        const int tap = fdiv(k, a.kdiv), ch = k - tap * a.kch;
-        const int ty = fdiv(tap, a.kwdiv), dy = ty - g.PH, dx = tap - ty * g.KW - g.PW;
-        const int yy = MODE == 0 ? py + dy : py - dy, xx = MODE == 0 ? px + dx : px - dx;
-        if (pv && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W) {
-          const size_t off = (size_t)yy * g.W + xx;
-          if (MODE == 0) v = src_val(a, ch, pb, HW, off);
-          else v = a.G[((size_t)pb * g.Cout + ch) * HW + off];
-        }
+      const bool kv = k < K;
+      const int kk = kv ? k : 0;
+      const int tap = fdiv(kk, kdiv), ch = kk - tap * kch;
+      const int ty = fdiv(tap, kwdiv), dy = ty - PH, dx = tap - ty * KW - PW;
+      // per lane
+      const int yy = MODE == 0 ? py + dy : py - dy, xx = MODE == 0 ? px + dx : px - dx;
+      const bool ok = kv && pv && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const unsigned pix = (unsigned)(yy * W + xx);
+      xmask |= ok ? (1u << i) : 0u;
+      if (MODE == 0) {
+        const RowDesc d = row_desc(cb1, cb2, cb3, ch, HWu);
+        const unsigned e = (unsigned)pb * d.A + d.Bc + (d.M ? pix : 0u);
+        xr[i] = d.p[ok ? e : 0u];
+      } else {
+        const unsigned e = ((unsigned)pb * (unsigned)Cout + (unsigned)ch) * HWu + pix;
+        xr[i] = Gp[ok ? e : 0u];
       }
-      xr[i] = v;
     }
     const int k = k0 + wkl;
-    const bool kv = k < a.K;
-    const int tap = kv ? fdiv(k, a.kdiv) : 0, ch = k - tap * a.kch;
+    const bool kv = k < K;
+    const int tap = kv ? fdiv(k, kdiv) : 0, ch = kv ? k - tap * kch : 0;
+    wmask = 0;
 #pragma unroll
     for (int i = 0; i < BM / 8; ++i) {
       const int r = row0 + wrow + 8 * i;
-      float v = 0.f;
-      if (kv && r < a.rows)
-        v = MODE == 0 ? a.weight[((size_t)r * g.Cin + ch) * T + tap]
-                      : a.weight[((size_t)ch * g.Cin + r) * T + tap];
-      wv[i] = v;
+      const bool ok = kv && r < rows;
+      wmask |= ok ? (1u << i) : 0u;
+      const unsigned idx = MODE == 0 ? ((unsigned)r * Cin + ch) * T + tap : ((unsigned)ch * Cin + r) * T + tap;
+      wv[i] = Wt[ok ? idx : 0u];
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) Xs[buf][krow + 4 * i][col] = xr[i];
+    for (int i = 0; i < 8; ++i) Xs[buf][krow + 4 * i][col] = (xmask >> i) & 1u ? xr[i] : 0.f;
 #pragma unroll
-    for (int i = 0; i < BM / 8; ++i) Ws[buf][wkl][wrow + 8 * i] = wv[i];
+    for (int i = 0; i < BM / 8; ++i) Ws[buf][wkl][wrow + 8 * i] = (wmask >> i) & 1u ? wv[i] : 0.f;
   };
 
   const int wr = (WM == 2) ? (wave & 1) : 0;
@@ -284,11 +321,11 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   const long long pe = p0 + wc * 32 + (lane & 31);
   if (pe >= P) return;
   if (a.part) {   // split-K partial: [split][rows][P]
-    float* dst = a.part + (size_t)blockIdx.y * a.rows * P + pe;
+    float* dst = a.part + (size_t)blockIdx.y * rows * P + pe;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < a.rows) dst[(size_t)row * P] = acc[r];
+      if (row < rows) dst[(size_t)row * P] = acc[r];
     }
     return;
   }
@@ -297,7 +334,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < a.rows) epi_store<MODE, ACT, EPI>(a, row, eb, epix, HW, acc[r]);
+    if (row < rows) epi_store<MODE, ACT, EPI>(a, row, eb, epix, HW, acc[r]);
   }
 }
 
@@ -319,61 +356,68 @@ __global__ __launch_bounds__(256) void igemm_finish_kernel(IgArgs a, int ksplit)
 }
 
 // ------------------------------------------------------------------ weight (+ bias) gradient
-// dW[o, n] = sum_p G[o, p] * X[c(n), p + d(tap(n))] with n = tap*Cin + c:
-// rows = o (64), cols = n (64), K = the pixels of split blockIdx.y (chunks of
-// 32).  Writes per-split partials [split][Cout][Cin*T]; blocks of column tile
-// 0 also write the bias partials sum_p G[o, p].
+// dW[o, n] = sum_p G[o, p] * X[c(n), p + d(tap(n))] with n = tap*Cin + c, and
+// column n = NK (= Cin*T) of X all ones, giving db[o] = sum_p G[o, p].
+// rows = o (64), cols = n (64), K = the pixels of split blockIdx.y in chunks
+// of 64.  Lane = pixel; wave w stages rows o0+16w.. and columns n0+16w.., so
+// every row / column decode is wave-uniform.  Writes per-split partials
+// [split][Cout][NK+1].
 __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
-  __shared__ float Gs[2][kBK][64 + 1];
-  __shared__ float Xs[2][kBK][64 + 1];
-  const ConvGeom& g = a.g;
+  __shared__ float Gs[2][kWP][64 + 1];
+  __shared__ float Xs[2][kWP][64 + 1];
+  const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
+  const int H = a.g.H, W = a.g.W, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
+  const int Cin = a.g.Cin, Cout = a.g.Cout;
+  const float* __restrict__ Gp = a.G;
+  const FastDiv cindiv = a.cindiv, kwdiv = a.kwdiv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = blockIdx.x;
   const int ot = t % a.otiles, nt = t / a.otiles;
   const int o0 = ot * 64, n0 = nt * 64;
-  const int NK = a.K;     // Cin * T
-  const size_t HW = (size_t)g.H * g.W;
-  const long long P = (long long)g.B * HW;
+  const int NK = a.K;                         // Cin * T; column NK = bias
+  const int NC = a.gbias ? NK + 1 : NK;       // columns computed
+  const size_t HW = (size_t)H * W;
+  const unsigned HWu = (unsigned)HW;
+  const long long P = (long long)a.g.B * HW;
   const long long pbeg = (long long)blockIdx.y * a.pchunk;
   const long long pend = pbeg + a.pchunk < P ? pbeg + a.pchunk : P;
-  const bool do_bias = a.bpart && nt == 0;
-  // staging: 32 lanes along pixels (coalesced), 8 row / column groups
-  const int kp = tid & 31, hi = tid >> 5;
-  int cdy[8], cdx[8], cch[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = n0 + hi + 8 * i;
-    const int tap = n < NK ? fdiv(n, a.cindiv) : 0;
-    const int ty = fdiv(tap, a.kwdiv);
-    cch[i] = n < NK ? n - tap * g.Cin : -1;
-    cdy[i] = ty - g.PH;
-    cdx[i] = tap - ty * g.KW - g.PW;
-  }
-  float gr[8], xr[8], bsum[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) bsum[i] = 0.f;
+  float gr[16], xr[16];
+  unsigned gmask = 0, xmask = 0, omask = 0;
 
   auto load = [&](long long q0) {
-    const long long p = q0 + kp;
+    const long long p = q0 + lane;
     const bool v = p < pend;
     const int b = v ? (int)(p / (long long)HW) : 0;
     const int pix = v ? (int)(p - (long long)b * HW) : 0;
-    const int py = pix / g.W, px = pix - py * g.W;
+    const int py = pix / W, px = pix - py * W;
+    gmask = 0;
+    xmask = 0;
+    omask = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int o = o0 + hi + 8 * i;
-      gr[i] = (v && o < g.Cout) ? a.G[((size_t)b * g.Cout + o) * HW + pix] : 0.f;
-      const int yy = py + cdy[i], xx = px + cdx[i];
-      xr[i] = (v && cch[i] >= 0 && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W)
-                  ? src_val(a, cch[i], b, HW, (size_t)yy * g.W + xx) : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const int o = o0 + wave * 16 + j;        // wave-uniform
+      const bool gok = v && o < Cout;
+      gmask |= gok ? (1u << j) : 0u;
+      gr[j] = Gp[gok ? ((unsigned)b * Cout + o) * HWu + pix : 0u];
+      const int n = __builtin_amdgcn_readfirstlane(n0 + wave * 16 + j);
+      const bool nv = n < NK;
+      const int tap = nv ? fdiv(n, cindiv) : 0, ch = nv ? n - tap * Cin : 0;
+      const int ty = fdiv(tap, kwdiv), dy = ty - PH, dx = tap - ty * KW - PW;
+      const int yy = py + dy, xx = px + dx;
+      const bool ok = v && nv && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const unsigned spix = (unsigned)(yy * W + xx);
+      xmask |= ok ? (1u << j) : 0u;
+      omask |= (v && n == NK) ? (1u << j) : 0u;
+      const RowDesc d = row_desc(cb1, cb2, cb3, ch, HWu);
+      const unsigned e = (unsigned)b * d.A + d.Bc + (d.M ? spix : 0u);
+      xr[j] = d.p[ok ? e : 0u];
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      Gs[buf][kp][hi + 8 * i] = gr[i];
-      Xs[buf][kp][hi + 8 * i] = xr[i];
-      if (do_bias) bsum[i] += gr[i];
+    for (int j = 0; j < 16; ++j) {
+      Gs[buf][lane][wave * 16 + j] = (gmask >> j) & 1u ? gr[j] : 0.f;
+      Xs[buf][lane][wave * 16 + j] = (xmask >> j) & 1u ? xr[j] : ((omask >> j) & 1u ? 1.f : 0.f);
     }
   };
 
@@ -387,11 +431,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
   }
   __syncthreads();
   int buf = 0;
-  for (long long q0 = pbeg; q0 < pend; q0 += kBK) {
-    const bool more = q0 + kBK < pend;
-    if (more) load(q0 + kBK);
+  for (long long q0 = pbeg; q0 < pend; q0 += kWP) {
+    const bool more = q0 + kWP < pend;
+    if (more) load(q0 + kWP);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < kWP / 2; ++s) {
       const int kk = s * 2 + (lane >> 5);
       acc = mfma32(Gs[buf][kk][wo * 32 + (lane & 31)], Xs[buf][kk][wc * 32 + (lane & 31)], acc);
     }
@@ -399,43 +443,33 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
     __syncthreads();
     buf ^= 1;
   }
-  float* wp = a.part + (size_t)blockIdx.y * g.Cout * NK;
+  float* wp = a.part + (size_t)blockIdx.y * Cout * (NK + 1);
   const int n = n0 + wc * 32 + (lane & 31);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (o < g.Cout && n < NK) wp[(size_t)o * NK + n] = acc[r];
-  }
-  if (do_bias) {
-    // lanes kp = 0..31 of each half-wave hold the same 8 output channels
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v = bsum[i];
-#pragma unroll
-      for (int m = 16; m > 0; m >>= 1) v += __shfl_xor(v, m, 32);
-      const int o = o0 + hi + 8 * i;
-      if (kp == 0 && o < g.Cout) a.bpart[(size_t)blockIdx.y * g.Cout + o] = v;
-    }
+    if (o < Cout && n < NC) wp[(size_t)o * (NK + 1) + n] = acc[r];
   }
 }
 
-// dW[o][c][tap] = sum_s part[s][o][tap*Cin + c]; db[o] = sum_s bpart[s][o]
+// dW[o][c][tap] = sum_s part[s][o][tap*Cin + c]; db[o] = sum_s part[s][o][NK].
+// Threads walk the partials in their (coalesced) [o][n] order.
 __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits) {
-  const ConvGeom& g = a.g;
-  const int T = g.KH * g.KW, NK = a.K;
-  const long long total = (long long)g.Cout * NK;
+  const int Cin = a.g.Cin, T = a.g.KH * a.g.KW, NK = a.K, Cout = a.g.Cout;
+  const int NC = a.gbias ? NK + 1 : NK;
+  const long long total = (long long)Cout * NC;
+  const size_t sstride = (size_t)Cout * (NK + 1);
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const int o = (int)(e / NK), rem = (int)(e - (long long)o * NK);
-    const int c = rem / T, tap = rem - c * T;
-    const size_t src = (size_t)o * NK + (size_t)tap * g.Cin + c;
+    const int o = (int)(e / NC), n = (int)(e - (long long)o * NC);
+    const size_t src = (size_t)o * (NK + 1) + n;
     float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * total + src];
-    a.gweight[e] = v;
-    if (a.gbias && e < g.Cout) {
-      float bv = 0.f;
-      for (int s = 0; s < splits; ++s) bv += a.bpart[(size_t)s * g.Cout + e];
-      a.gbias[e] = bv;
+    for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * sstride + src];
+    if (n == NK) {
+      a.gbias[o] = v;
+    } else {
+      const int tap = n / Cin, c = n - tap * Cin;
+      a.gweight[((size_t)o * Cin + c) * T + tap] = v;
     }
   }
 }
@@ -464,7 +498,8 @@ namespace {
 
 FastDiv make_fdiv(int d) {
   FastDiv f;
-  f.m = ((1ULL << 32) + (unsigned long long)d - 1) / (unsigned long long)d;
+  f.one = d == 1;
+  f.m = d == 1 ? 0u : (unsigned)(((1ULL << 32) + (unsigned long long)d - 1) / (unsigned long long)d);
   return f;
 }
 
@@ -500,23 +535,23 @@ IgPlan plan_igemm(int rows, int kch, int T, long long P) {
 struct WgPlan {
   int otiles, ntiles, splits;
   long long pchunk;
-  size_t part_bytes, bpart_bytes;
+  size_t part_bytes;
 };
 
 WgPlan plan_wgrad(int Cin, int Cout, int T, long long P) {
   WgPlan pl;
+  const int NK = Cin * T;
   pl.otiles = (Cout + 63) / 64;
-  pl.ntiles = (Cin * T + 63) / 64;
+  pl.ntiles = (NK + 1 + 63) / 64;
   const long long tiles = (long long)pl.otiles * pl.ntiles;
   long long splits = (640 + tiles - 1) / tiles;
-  const long long maxs = (P + 4 * kBK - 1) / (4 * kBK);   // >= 4 chunks per split
+  const long long maxs = (P + 2 * kWP - 1) / (2 * kWP);   // >= 2 chunks per split
   if (splits > maxs) splits = maxs;
   if (splits > 64) splits = 64;
   if (splits < 1) splits = 1;
-  pl.pchunk = ((P + splits - 1) / splits + kBK - 1) / kBK * kBK;
+  pl.pchunk = ((P + splits - 1) / splits + kWP - 1) / kWP * kWP;
   pl.splits = (int)((P + pl.pchunk - 1) / pl.pchunk);
-  pl.part_bytes = align256((size_t)pl.splits * Cout * Cin * T * sizeof(float));
-  pl.bpart_bytes = align256((size_t)pl.splits * Cout * sizeof(float));
+  pl.part_bytes = align256((size_t)pl.splits * Cout * (NK + 1) * sizeof(float));
   return pl;
 }
 
@@ -527,17 +562,22 @@ size_t fwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
 size_t bwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   const long long P = (long long)B * H * W;
   const int T = KH * KW;
-  const WgPlan wp = plan_wgrad(Cin, Cout, T, P);
   return align256((size_t)Cout * P * sizeof(float)) +              // pre-activation gradient
          plan_igemm(Cin, Cout, T, P).part_bytes +                   // data-gradient split-K
-         wp.part_bytes + wp.bpart_bytes;                            // weight-gradient partials
+         plan_wgrad(Cin, Cout, T, P).part_bytes;                    // weight-gradient partials
 }
+
+bool too_big(long long B, long long C, long long HW) { return B * C * HW >= (1LL << 30); }
 
 int conv_setup_geom(IgArgs& a, const dro_slice* srcs, int nsrc, int B, int H, int W, int Cout, int KH,
                     int KW) {
   ConvGeom& g = a.g;
   if (!srcs || nsrc < 1 || nsrc > kMaxSrc) {
     set_error("conv2d: need 1..4 input slices");
+    return DRO_E_SHAPE;
+  }
+  if (B < 1 || H < 1 || W < 1 || Cout < 1 || KH < 1 || KW < 1 || (KH % 2) == 0 || (KW % 2) == 0) {
+    set_error("conv2d: sizes out of range (odd kernels, 'same' padding, stride 1)");
     return DRO_E_SHAPE;
   }
   int cin = 0;
@@ -551,12 +591,15 @@ int conv_setup_geom(IgArgs& a, const dro_slice* srcs, int nsrc, int B, int H, in
       set_error("conv2d: bad input slice");
       return DRO_E_SHAPE;
     }
+    if (too_big(B, srcs[i].total_channels, srcs[i].broadcast ? 1LL : (long long)H * W)) {
+      set_error("conv2d: a source tensor has >= 2^30 elements (32-bit offsets)");
+      return DRO_E_SHAPE;
+    }
     cin += srcs[i].channels;
   }
-  if (B < 1 || H < 1 || W < 1 || Cout < 1 || KH < 1 || KW < 1 || (KH % 2) == 0 || (KW % 2) == 0 ||
-      (long long)B * H * W > (1LL << 30) || cin >= 4096 || Cout >= 4096 ||
-      (long long)cin * KH * KW >= 65536 || (long long)Cout * KH * KW >= 65536) {
-    set_error("conv2d: sizes out of range (odd kernels, stride 1, C*KH*KW < 65536, C < 4096)");
+  if (cin >= 4096 || Cout >= 4096 || (long long)cin * KH * KW >= 65535 ||
+      (long long)Cout * KH * KW >= 65535 || too_big(B, cin > Cout ? cin : Cout, (long long)H * W)) {
+    set_error("conv2d: sizes out of range (C < 4096, C*KH*KW < 65535, B*C*H*W < 2^30)");
     return DRO_E_SHAPE;
   }
   g.B = B;
@@ -622,11 +665,11 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   return launch_status("igemm_finish_kernel launch failed");
 }
 
-int check_ws(size_t have, size_t need, const char* what) {
-  if (have < need) {
-    static thread_local char msg[160];
+int check_ws(const void* ws, size_t have, size_t need, const char* what) {
+  if (need > 0 && (!ws || have < need)) {
+    static thread_local char msg[192];
     snprintf(msg, sizeof(msg), "%s: workspace of %zu bytes is smaller than the %zu required "
-             "(dro_conv2d_workspace_bytes)", what, have, need);
+             "(dro_conv2d_workspace_bytes)", what, ws ? have : (size_t)0, need);
     set_error(msg);
     return DRO_E_SHAPE;
   }
@@ -651,15 +694,14 @@ extern "C" size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int C
   return f > b ? f : b;
 }
 
-extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
-                                  const float* weight, const float* bias, int B, int H, int W,
-                                  int Cout, int KH, int KW, int act, float alpha, float* out,
-                                  int out_ctot, int out_coff, void* workspace,
+extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
+                                  int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
+                                  float* out, int out_ctot, int out_coff, void* workspace,
                                   size_t workspace_bytes, void* stream) {
   IgArgs a = {};
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
-  if (!weight || !out || out_coff < 0 || out_coff + Cout > out_ctot) {
+  if (!weight || !out || out_coff < 0 || out_coff + Cout > out_ctot || too_big(B, out_ctot, (long long)H * W)) {
     set_error("conv2d_forward: NULL weight/out or bad output slice");
     return DRO_E_NULL;
   }
@@ -667,10 +709,9 @@ extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_sli
     set_error("conv2d_forward: alpha != 1 requires act none");
     return DRO_E_MODE;
   }
-  if ((st = check_ws(workspace ? workspace_bytes : 0, fwd_workspace(B, H, W, a.g.Cin, Cout, KH, KW),
+  if ((st = check_ws(workspace, workspace_bytes, fwd_workspace(B, H, W, a.g.Cin, Cout, KH, KW),
                      "conv2d_forward")))
     return st;
-  a.scale0 = to_slice(scale0);
   a.weight = weight;
   a.bias = bias;
   a.alpha = alpha;
@@ -686,23 +727,53 @@ extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_sli
   return st;
 }
 
-extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
-                                         const float* weight, const float* bias, int B, int H,
-                                         int W, int Cout, int KH, int KW, const dro_slice* z,
-                                         const dro_slice* h, float* q_out, int q_ctot, int q_coff,
-                                         float* out, int out_ctot, int out_coff, void* workspace,
+extern "C" int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const float* weight,
+                                         const float* bias, int B, int H, int W, int hd, int KH, int KW,
+                                         float* zr, float* rh, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+  IgArgs a = {};
+  int st = conv_setup_geom(a, srcs, nsrc, B, H, W, 2 * hd, KH, KW);
+  if (st) return st;
+  if (!weight || !zr || !rh) {
+    set_error("convgru_gates_forward: NULL weight/zr/rh");
+    return DRO_E_NULL;
+  }
+  if (srcs[0].channels != hd || srcs[0].broadcast) {
+    set_error("convgru_gates_forward: source 0 must be the dense hidden state (hd channels)");
+    return DRO_E_SHAPE;
+  }
+  if ((st = check_ws(workspace, workspace_bytes, fwd_workspace(B, H, W, a.g.Cin, 2 * hd, KH, KW),
+                     "convgru_gates_forward")))
+    return st;
+  a.weight = weight;
+  a.bias = bias;
+  a.alpha = 1.f;
+  a.out = zr;
+  a.out_ctot = 2 * hd;
+  a.out_coff = 0;
+  a.h = to_slice(srcs);
+  a.aux = rh;
+  a.hd = hd;
+  a.rows = 2 * hd;
+  a.kch = a.g.Cin;
+  return launch_igemm<0, 2, 2>(a, (long long)B * H * W, static_cast<char*>(workspace), (hipStream_t)stream);
+}
+
+extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const float* weight,
+                                         const float* bias, int B, int H, int W, int Cout, int KH, int KW,
+                                         const dro_slice* z, const dro_slice* h, float* q_out, float* out,
+                                         int out_ctot, int out_coff, void* workspace,
                                          size_t workspace_bytes, void* stream) {
   IgArgs a = {};
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
-  if (!weight || !out || !z || !h || !z->data || !h->data) {
-    set_error("convgru_blend_forward: NULL weight/out/z/h");
+  if (!weight || !out || !q_out || !z || !h || !z->data || !h->data) {
+    set_error("convgru_blend_forward: NULL weight/out/q/z/h");
     return DRO_E_NULL;
   }
-  if ((st = check_ws(workspace ? workspace_bytes : 0, fwd_workspace(B, H, W, a.g.Cin, Cout, KH, KW),
+  if ((st = check_ws(workspace, workspace_bytes, fwd_workspace(B, H, W, a.g.Cin, Cout, KH, KW),
                      "convgru_blend_forward")))
     return st;
-  a.scale0 = to_slice(scale0);
   a.weight = weight;
   a.bias = bias;
   a.alpha = 1.f;
@@ -711,23 +782,19 @@ extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const 
   a.out_coff = out_coff;
   a.z = to_slice(z);
   a.h = to_slice(h);
-  a.q_out = q_out;
-  a.q_ctot = q_ctot;
-  a.q_coff = q_coff;
+  a.aux = q_out;
   a.rows = Cout;
   a.kch = a.g.Cin;
   return launch_igemm<0, 3, 1>(a, (long long)B * H * W, static_cast<char*>(workspace),
                                (hipStream_t)stream);
 }
 
-extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
-                                   const float* weight, int B, int H, int W, int Cout, int KH,
-                                   int KW, int act, float alpha, const dro_slice* y,
-                                   const float* dout, float* const* grad_srcs,
+extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H,
+                                   int W, int Cout, int KH, int KW, int act, float alpha,
+                                   const dro_slice* y, const float* dout, float* const* grad_srcs,
                                    const int* grad_ctot, const int* grad_coff,
-                                   const int* grad_accumulate, float* grad_weight,
-                                   float* grad_bias, void* workspace, size_t workspace_bytes,
-                                   void* stream) {
+                                   const int* grad_accumulate, float* grad_weight, float* grad_bias,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
   IgArgs a = {};
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
@@ -744,7 +811,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_sl
     set_error("conv2d_backward: grad_bias requires grad_weight");
     return DRO_E_NULL;
   }
-  if ((st = check_ws(workspace ? workspace_bytes : 0, bwd_workspace(B, H, W, a.g.Cin, Cout, KH, KW),
+  if ((st = check_ws(workspace, workspace_bytes, bwd_workspace(B, H, W, a.g.Cin, Cout, KH, KW),
                      "conv2d_backward")))
     return st;
   for (int i = 0; i < nsrc; ++i) {
@@ -752,8 +819,11 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_sl
     a.gsrc_ctot[i] = grad_ctot ? grad_ctot[i] : srcs[i].channels;
     a.gsrc_coff[i] = grad_coff ? grad_coff[i] : 0;
     a.gsrc_acc[i] = grad_accumulate ? grad_accumulate[i] : 0;
+    if (a.gsrc[i] && too_big(B, a.gsrc_ctot[i], (long long)H * W)) {
+      set_error("conv2d_backward: gradient target too large (32-bit offsets)");
+      return DRO_E_SHAPE;
+    }
   }
-  a.scale0 = to_slice(scale0);
   a.weight = weight;
   a.gweight = grad_weight;
   a.gbias = grad_bias;
@@ -790,11 +860,10 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_sl
     a.otiles = pl.otiles;
     a.pchunk = pl.pchunk;
     a.part = reinterpret_cast<float*>(ws_wg);
-    a.bpart = grad_bias ? reinterpret_cast<float*>(ws_wg + pl.part_bytes) : nullptr;
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits),
                        dim3(256), 0, s, a);
     if ((st = launch_status("wgrad_kernel launch failed"))) return st;
-    const long long total = (long long)Cout * a.K;
+    const long long total = (long long)Cout * (a.K + 1);
     long long blocks = (total + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pl.splits);

@@ -77,9 +77,8 @@ class _Conv2d(torch.autograd.Function):
         B, _, H, W = srcs[0].shape
         weight = weight.contiguous()
         out = _dense_out(srcs, Cout)
-        arr = _slices(srcs)
         ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, out.device)
-        check(lib.dro_conv2d_forward(arr, len(srcs), None, ptr(weight), ptr(bias), B, H, W, Cout, KH, KW,
+        check(lib.dro_conv2d_forward(_slices(srcs), len(srcs), ptr(weight), ptr(bias), B, H, W, Cout, KH, KW,
                                      act, ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(ws), nws,
                                      stream_of(out)), "dro_conv2d_forward")
         ctx.save_for_backward(weight, out if act else None, *srcs)
@@ -91,23 +90,23 @@ class _Conv2d(torch.autograd.Function):
         lib = _lib.load()
         weight, y, *srcs = ctx.saved_tensors
         act, alpha, has_bias = ctx.meta
-        Cout, _, KH, KW = weight.shape
+        Cout, Cin, KH, KW = weight.shape
         B, _, H, W = srcs[0].shape
         need = ctx.needs_input_grad
         gout = gout.contiguous()
         gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[4 + i] else None
                 for i, s in enumerate(srcs)]
-        gw = torch.empty_like(weight) if need[0] else None
+        gw = torch.empty_like(weight) if (need[0] or (has_bias and need[1])) else None
         gb = torch.empty(Cout, device=gout.device) if (has_bias and need[1]) else None
         ptrs, ctot, coff = _grad_targets(gsrc)
         acc = (ctypes.c_int * len(srcs))()
         ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
-        ws, nws = _workspace(B, H, W, weight.shape[1], Cout, KH, KW, gout.device)
-        check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), None, ptr(weight), B, H, W, Cout, KH, KW,
+        ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
+        check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
                                       ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), ptr(ws), nws,
                                       stream_of(gout)), "dro_conv2d_backward")
-        return (gw, gb, None, None, *gsrc)
+        return (gw if need[0] else None, gb, None, None, *gsrc)
 
 
 def conv2d(srcs, weight, bias=None, act=None, alpha=1.0):
@@ -119,7 +118,8 @@ def conv2d(srcs, weight, bias=None, act=None, alpha=1.0):
 
 class _SepGRUHalf(torch.autograd.Function):
     """One direction of SepConvGRU (update.py:59-70): z, r = sigmoid(conv([h; x]));
-    q = tanh(conv([r*h; x])); h' = (1-z) h + z q.  x given as sources."""
+    q = tanh(conv([r*h; x])); h' = (1-z) h + z q.  x given as sources.
+    Forward: 2 launches (gates + r*h; candidate + blend)."""
 
     @staticmethod
     def forward(ctx, h, wz, bz, wr, br, wq, bq, *xs):
@@ -128,67 +128,66 @@ class _SepGRUHalf(torch.autograd.Function):
         h = h.contiguous()
         B, hd, H, W = h.shape
         KH, KW = wz.shape[2:]
+        cin = wz.shape[1]
         wzr = torch.cat([wz, wr], 0).contiguous()
         bzr = torch.cat([bz, br], 0).contiguous()
-        srcs = [h, *xs]
-        arr = _slices(srcs)
         st = stream_of(h)
-        cin = wz.shape[1]
         zr = torch.empty(B, 2 * hd, H, W, device=h.device)
+        rh = torch.empty_like(h)
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-        check(lib.dro_conv2d_forward(arr, len(srcs), None, ptr(wzr), ptr(bzr), B, H, W, 2 * hd, KH, KW,
-                                     ACT["sigmoid"], ctypes.c_float(1.0), ptr(zr), 2 * hd, 0, ptr(ws), nws,
-                                     st), "dro_conv2d_forward(zr)")
+        check(lib.dro_convgru_gates_forward(_slices([h, *xs]), 1 + len(xs), ptr(wzr), ptr(bzr), B, H, W, hd,
+                                            KH, KW, ptr(zr), ptr(rh), ptr(ws), nws, st),
+              "dro_convgru_gates_forward")
         q = torch.empty_like(h)
         hn = torch.empty_like(h)
-        r_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, hd, 0)
         z_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, 0, 0)
         h_sl = DroSlice(h.data_ptr(), hd, hd, 0, 0)
         wsq, nwsq = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-        check(lib.dro_convgru_blend_forward(arr, len(srcs), ctypes.byref(r_sl), ptr(wq), ptr(bq), B, H, W,
-                                            hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl), ptr(q),
-                                            hd, 0, ptr(hn), hd, 0, ptr(wsq), nwsq, st),
+        check(lib.dro_convgru_blend_forward(_slices([rh, *xs]), 1 + len(xs), ptr(wq.contiguous()), ptr(bq),
+                                            B, H, W, hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl),
+                                            ptr(q), ptr(hn), hd, 0, ptr(wsq), nwsq, st),
               "dro_convgru_blend_forward")
-        ctx.save_for_backward(h, wzr, wq, zr, q, *xs)
+        ctx.save_for_backward(h, rh, wzr, wq, zr, q, *xs)
         return hn
 
     @staticmethod
     def backward(ctx, dhn):
         lib = _lib.load()
-        h, wzr, wq, zr, q, *xs = ctx.saved_tensors
+        h, rh, wzr, wq, zr, q, *xs = ctx.saved_tensors
         B, hd, H, W = h.shape
         KH, KW = wq.shape[2:]
+        cin = wq.shape[1]
         st = stream_of(h)
         dhn = dhn.contiguous()
-        dq, dh = torch.empty_like(h), torch.empty_like(h)     # dq, dzr: pre-activation grads
+        need = ctx.needs_input_grad
+        n = 1 + len(xs)
+        # stage 1: pre-activation grads of q and z, dh = dh' (1-z)
+        dq, dh = torch.empty_like(h), torch.empty_like(h)
         dzr = torch.empty_like(zr)
         check(lib.dro_gru_backward_elem(1, B, hd, H, W, ptr(dhn), ptr(zr), ptr(q), ptr(h), None, ptr(dq),
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(1)")
-        need = ctx.needs_input_grad
-        srcs = [h, *xs]
-        arr = _slices(srcs)
+        # candidate conv over [r*h, x]: d(r*h), dx (overwrite), dWq, dbq
         drh = torch.empty_like(h)
         dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[7 + i] else None
                for i, x in enumerate(xs)]
-        r_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, hd, 0)
         gwq, gbq = torch.empty_like(wq), torch.empty(hd, device=h.device)
         ptrs, ctot, coff = _grad_targets([drh, *dxs])
-        acc = (ctypes.c_int * len(srcs))()
-        cin = wq.shape[1]
+        acc = (ctypes.c_int * n)()
         ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(arr, len(srcs), ctypes.byref(r_sl), ptr(wq), B, H, W, hd, KH, KW,
+        check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq.contiguous()), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
                                       ptr(gwq), ptr(gbq), ptr(ws), nws, st), "dro_conv2d_backward(q)")
+        # stage 2: pre-activation grad of r, dh += d(r*h) r
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
+        # gate conv over [h, x]: dh, dx accumulate; dWz|dWr, dbz|dbr
         gwzr, gbzr = torch.empty_like(wzr), torch.empty(2 * hd, device=h.device)
         ptrs, ctot, coff = _grad_targets([dh, *dxs])
-        acc = (ctypes.c_int * len(srcs))(*([1] * len(srcs)))
+        acc = (ctypes.c_int * n)(*([1] * n))
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(arr, len(srcs), None, ptr(wzr), B, H, W, 2 * hd, KH, KW,
+        check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
-                                      ptr(gwzr), ptr(gbzr), ptr(ws), nws, st),
-              "dro_conv2d_backward(zr)")
+                                      ptr(gwzr), ptr(gbzr), ptr(ws), nws, st), "dro_conv2d_backward(zr)")
         return (dh if need[0] else None, gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:], gwq, gbq, *dxs)
 
 

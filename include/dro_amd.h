@@ -139,14 +139,14 @@ int dro_convex_upsample_backward(const float* inv, const float* mask, const floa
  * Replace the nn.Conv2d + activation + torch.cat chains of
  * networks/optim/update.py:5-199 (SepConvGRU :47-74, ProjectionInput* :77-124,
  * heads :5-28, mask :150-153).  The input is the VIRTUAL channel concatenation
- * of 1..3 slices (no copy); source 0 may be multiplied elementwise by `scale0`
- * (same channel count, e.g. the GRU's r*h).  weight [Cout][Cin][KH][KW] with
- * Cin = sum of slice channels; odd KH, KW; padding KH/2, KW/2.
+ * of 1..4 slices (no copy).  weight [Cout][Cin][KH][KW] with Cin = sum of
+ * slice channels; odd KH, KW; padding KH/2, KW/2.
  * act: 0 none, 1 relu, 2 sigmoid, 3 tanh, applied in the epilogue after bias,
  * then the result is multiplied by alpha (alpha != 1 only with act none: the
- * 0.25-scaled mask heads, update.py:153).  1..4 input slices.
- * The output goes to channels [out_coff, out_coff+Cout) of a [B,out_ctot,H,W]
- * tensor.
+ * 0.25-scaled mask heads, update.py:153).  The output goes to channels
+ * [out_coff, out_coff+Cout) of a [B,out_ctot,H,W] tensor.
+ * Limits: C < 4096, C*KH*KW < 65535, every tensor < 2^30 elements.
+ * Every call is bitwise run-to-run deterministic (no atomics).
  * ---------------------------------------------------------------------- */
 typedef struct dro_slice {
   const float* data;      /* base of a dense [B, total_channels, H, W] tensor */
@@ -162,41 +162,47 @@ typedef struct dro_slice {
 #define DRO_ACT_SIGMOID 2
 #define DRO_ACT_TANH 3
 
-/* Scratch needed by any of the three calls below for this shape (split-K
- * partials, weight-gradient partials, the pre-activation gradient); pass a
- * device buffer of at least this size as `workspace`.  No call keeps state in
- * it, and every result is bitwise run-to-run deterministic (no atomics). */
+/* Scratch needed by any conv call below for this shape (split-K partials,
+ * weight-gradient partials, the pre-activation gradient); pass a device buffer
+ * of at least this size as `workspace`.  No call keeps state in it. */
 size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int Cout, int KH, int KW);
 
-int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
-                       const float* weight, const float* bias, int B, int H, int W, int Cout,
-                       int KH, int KW, int act, float alpha, float* out, int out_ctot,
-                       int out_coff, void* workspace, size_t workspace_bytes, void* stream);
+int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
+                       int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
+                       float* out, int out_ctot, int out_coff, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
-/* SepConvGRU gate q with the blend fused (update.py:69-70 / :76-77):
- * q = tanh(conv(srcs) + bias); out = (1 - z) * h + z * q; q also stored to
- * q_out (channels [q_coff, q_coff+Cout) of [B,q_ctot,H,W]) for the backward. */
-int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
-                              const float* weight, const float* bias, int B, int H, int W,
-                              int Cout, int KH, int KW, const dro_slice* z, const dro_slice* h,
-                              float* q_out, int q_ctot, int q_coff, float* out, int out_ctot,
-                              int out_coff, void* workspace, size_t workspace_bytes, void* stream);
+/* SepConvGRU z|r gates (update.py:64-65 / :71-72) with r*h fused:
+ * zr = sigmoid(conv([h; x]) + b) into a dense [B, 2hd, H, W] (z first) and
+ * rh = r * h into a dense [B, hd, H, W].  srcs[0] must be the dense hidden
+ * state h (hd channels); weight = cat(convz.weight, convr.weight). */
+int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const float* weight,
+                              const float* bias, int B, int H, int W, int hd, int KH, int KW,
+                              float* zr, float* rh, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
+/* SepConvGRU candidate with the blend fused (update.py:66-67 / :73-74):
+ * q = tanh(conv([r*h; x]) + b) saved to q_out (dense [B, Cout, H, W]) and
+ * out = (1 - z) * h + z * q into channels [out_coff, +Cout) of [B,out_ctot,H,W]. */
+int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const float* weight,
+                              const float* bias, int B, int H, int W, int Cout, int KH, int KW,
+                              const dro_slice* z, const dro_slice* h, float* q_out, float* out,
+                              int out_ctot, int out_coff, void* workspace, size_t workspace_bytes,
+                              void* stream);
 
 /* Gradients of dro_conv2d_forward given dout [B,Cout,H,W] (dense) and, for
  * act != 0, the saved activation output y (the pre-activation gradient
  * alpha*dout*act'(y) is formed in the workspace).  grad_srcs[i] (nullable)
- * receives d/d(source i) -- for a scaled source 0, the gradient w.r.t. the
- * SCALED values -- into channels [grad_coff[i], +C_i) of a
+ * receives d/d(source i) into channels [grad_coff[i], +C_i) of a
  * [B, grad_ctot[i], H, W] tensor, overwritten or added (grad_accumulate[i]);
  * a broadcast source receives its per-pixel gradient (the caller sums over
  * H x W).  grad_weight / grad_bias (nullable; grad_bias needs grad_weight)
  * are overwritten. */
-int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const dro_slice* scale0,
-                        const float* weight, int B, int H, int W, int Cout, int KH, int KW,
-                        int act, float alpha, const dro_slice* y, const float* dout,
-                        float* const* grad_srcs, const int* grad_ctot, const int* grad_coff,
-                        const int* grad_accumulate, float* grad_weight, float* grad_bias,
-                        void* workspace, size_t workspace_bytes, void* stream);
+int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H, int W,
+                        int Cout, int KH, int KW, int act, float alpha, const dro_slice* y,
+                        const float* dout, float* const* grad_srcs, const int* grad_ctot,
+                        const int* grad_coff, const int* grad_accumulate, float* grad_weight,
+                        float* grad_bias, void* workspace, size_t workspace_bytes, void* stream);
 
 /* SepConvGRU backward, elementwise parts (update.py:67-70): with zr the saved
  * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W].
