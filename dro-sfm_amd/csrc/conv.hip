@@ -94,6 +94,9 @@ struct IgArgs {
   float* part;            // [ksplit][rows][P] (igemm) / [splits][Cout][NK+1] (wgrad)
   int otiles;             // weight gradient: output-channel tiles
   long long pchunk;       // weight gradient: pixels per split
+  // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
+  // tile + halo staged once per channel chunk of CK channels
+  int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -338,6 +341,195 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ halo-tiled direct conv
+// Same GEMM as igemm_kernel, but a block's 64 pixels are a TH x TW tile of one
+// image and each K chunk is CK channels x ALL taps: the CK x (TH+KH-1) x
+// (TW+KW-1) input patch is staged once (each element loaded once, instead of
+// once per tap) and the B operand of tap (ty, tx) is a shifted LDS read.  The
+// weight chunk W[rows][CK][T] (contiguous per row) is staged as [tap][c][row].
+// MODE 0 forward, MODE 1 data gradient (tap flipped).  BM = 64: 2x2 waves of
+// 32x32; BM = 32: 2 pixel halves x 2 channel halves (LDS reduction).
+// Dynamic LDS: 2 stages of T*CK*(BM+1) + CK*HPAD floats.
+template <int BM, int MODE, int ACT, int EPI>
+__global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
+  extern __shared__ float smem[];
+  constexpr int WM = BM / 32;
+  const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
+  const int H = a.g.H, W = a.g.W, KH = a.g.KH, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
+  const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch;
+  const int TW = a.TW, HWd = a.HWd, HPAD = a.HPAD, CK = a.CK;
+  const int T = KH * KW;
+  const int HALO = (a.TH + KH - 1) * HWd;
+  const int WSZ = T * CK * (BM + 1), STAGE = WSZ + CK * HPAD;
+  const float* __restrict__ Wt = a.weight;
+  const float* __restrict__ Gp = a.G;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
+  const int row0 = rt * BM;
+  const int b = pt / a.tiles_img, trem = pt - b * a.tiles_img;
+  const int ty0 = (trem / a.tiles_x) * a.TH, tx0 = (trem % a.tiles_x) * TW;
+  const size_t HW = (size_t)H * W;
+  const unsigned HWu = (unsigned)HW;
+  const int nck = (kch + CK - 1) / CK;
+  const int cbeg = blockIdx.y * a.chunks_per_split;
+  const int cend = min(nck, cbeg + a.chunks_per_split);
+  const int hy0 = ty0 - PH, hx0 = tx0 - PW;    // halo origin in the image
+
+  // X staging: wave w stages channels w, w+4, ...; lanes run over the halo
+  const int xper = (CK + 3) / 4;              // channels per wave (<= 4)
+  const int nj = (HALO + 63) / 64;            // halo passes per channel (<= 4)
+  // W staging: element e = tid + 256 i of the BM x (CK*T) chunk block
+  const int CKT = CK * T;
+  const int wtotal = BM * CKT;
+  const int wper = (wtotal + 255) / 256;      // <= 16 (checked on the host)
+  const FastDiv ckt_div = a.kdiv;             // divisor CK*T (set by the host)
+  const FastDiv t_div = a.cindiv;             // divisor T
+  const FastDiv hwd_div = a.kwdiv;            // divisor HWd
+
+  float xr[16], wv[16];
+  unsigned xmask = 0, wmask = 0;
+  auto load = [&](int chunk) {
+    const int c0 = chunk * CK;
+    xmask = 0;
+    wmask = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int slot = i * 4 + j;
+        if (i < xper && j < nj) {
+          const int cl = wave + 4 * i;
+          const int ch = __builtin_amdgcn_readfirstlane(c0 + cl);
+          const int e = lane + 64 * j;
+          const int hy = fdiv(e, hwd_div), hx = e - hy * HWd;
+          const int yy = hy0 + hy, xx = hx0 + hx;
+          const bool ok = cl < CK && ch < kch && e < HALO && (unsigned)yy < (unsigned)H &&
+                          (unsigned)xx < (unsigned)W;
+          const unsigned pix = (unsigned)(yy * W + xx);
+          xmask |= ok ? (1u << slot) : 0u;
+          if (MODE == 0) {
+            const RowDesc d = row_desc(cb1, cb2, cb3, ch < kch ? ch : 0, HWu);
+            const unsigned off = (unsigned)b * d.A + d.Bc + (d.M ? pix : 0u);
+            xr[slot] = d.p[ok ? off : 0u];
+          } else {
+            const unsigned off = ((unsigned)b * (unsigned)Cout + (unsigned)ch) * HWu + pix;
+            xr[slot] = Gp[ok ? off : 0u];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i < wper) {
+        const int e = tid + 256 * i;
+        const int r = fdiv(e, ckt_div), rem = e - r * CKT;
+        const int cl = fdiv(rem, t_div), tap = rem - cl * T;
+        const int row = row0 + r, ch = c0 + cl;
+        const bool ok = e < wtotal && row < rows && ch < kch;
+        wmask |= ok ? (1u << i) : 0u;
+        const unsigned idx = MODE == 0 ? ((unsigned)row * Cin + ch) * T + tap
+                                       : ((unsigned)ch * Cin + row) * T + tap;
+        wv[i] = Wt[ok ? idx : 0u];
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    float* Ws = smem + buf * STAGE;
+    float* Xs = Ws + WSZ;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int slot = i * 4 + j;
+        const int cl = wave + 4 * i, e = lane + 64 * j;
+        if (i < xper && j < nj && cl < CK && e < HPAD)
+          Xs[cl * HPAD + e] = (xmask >> slot) & 1u ? xr[slot] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i < wper) {
+        const int e = tid + 256 * i;
+        if (e < wtotal) {
+          const int r = fdiv(e, ckt_div), rem = e - r * CKT;
+          const int cl = fdiv(rem, t_div), tap = rem - cl * T;
+          Ws[(tap * CK + cl) * (BM + 1) + r] = (wmask >> i) & 1u ? wv[i] : 0.f;
+        }
+      }
+    }
+  };
+
+  const int wr = (WM == 2) ? (wave & 1) : 0;
+  const int wc = (WM == 2) ? (wave >> 1) : (wave & 1);
+  const int wk = (WM == 2) ? 0 : (wave >> 1);
+  const int q = wc * 32 + (lane & 31);          // this lane's pixel in the tile (MFMA column)
+  const int qy = q / TW, qx = q - qy * TW;
+  const int qoff = qy * HWd + qx;
+  const int hi = lane >> 5;
+  const int CKh = CK / 2;
+  const int s_lo = (WM == 2) ? 0 : wk * (CKh / 2), s_hi = (WM == 2) ? CKh : s_lo + CKh / 2;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+  if (cbeg < cend) {
+    load(cbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int c = cbeg; c < cend; ++c) {
+    const int buf = (c - cbeg) & 1;
+    const bool more = c + 1 < cend;
+    if (more) load(c + 1);
+    const float* Ws = smem + buf * STAGE;
+    const float* Xs = Ws + WSZ;
+    for (int ty = 0; ty < KH; ++ty) {
+      for (int tx = 0; tx < KW; ++tx) {
+        const int tap = ty * KW + tx;
+        const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
+        const float* wa = Ws + (tap * CK + hi) * (BM + 1) + wr * 32 + (lane & 31);
+        const float* xb = Xs + hi * HPAD + qoff + toff;
+#pragma unroll 4
+        for (int s = s_lo; s < s_hi; ++s)
+          acc = mfma32(wa[2 * s * (BM + 1)], xb[2 * s * HPAD], acc);
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  if (WM == 1) {   // sum the two channel halves (LDS reused after the final barrier)
+    float* red = smem;   // [2 pixel halves][16][64]
+    if (wk == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wc * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wk == 1) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += red[(wc * 16 + r) * 64 + lane];
+  }
+
+  const int oy = ty0 + qy, ox = tx0 + qx;
+  if (qy >= a.TH || oy >= H || ox >= W) return;
+  const size_t epix = (size_t)oy * W + ox;
+  if (a.part) {   // split-K partial: [split][rows][P]
+    const long long P = (long long)a.g.B * HW;
+    float* dst = a.part + (size_t)blockIdx.y * rows * P + (size_t)b * HW + epix;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < rows) dst[(size_t)row * P] = acc[r];
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row < rows) epi_store<MODE, ACT, EPI>(a, row, b, epix, HW, acc[r]);
+  }
+}
+
 // split-K finish: sum the partials in split order, then the epilogue
 template <int MODE, int ACT, int EPI>
 __global__ __launch_bounds__(256) void igemm_finish_kernel(IgArgs a, int ksplit) {
@@ -507,23 +699,73 @@ size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 // ---- launch plans (shared by the workspace query and the launches)
 struct IgPlan {
+  bool halo;
   int bm, row_tiles, ptiles, ksplit, chunks_per_split;
+  int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
+  size_t lds_bytes;
   size_t part_bytes;
 };
 
-IgPlan plan_igemm(int rows, int kch, int T, long long P) {
-  IgPlan pl;
-  pl.ptiles = (int)((P + kBN - 1) / kBN);
-  const int t64 = (rows + 63) / 64;
-  pl.bm = (long long)t64 * pl.ptiles >= 448 ? 64 : 32;
-  pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
-  const int nchunks = (kch * T + kBK - 1) / kBK;
-  const long long blocks = (long long)pl.row_tiles * pl.ptiles;
+constexpr size_t kHaloLds = 64 * 1024;   // per block: two blocks per CU
+
+IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
+  IgPlan pl = {};
+  const int T = KH * KW;
+  const long long P = (long long)B * H * W;
+  pl.halo = T > 1;
+  long long blocks;
+  int nchunks;
+  if (!pl.halo) {
+    pl.ptiles = (int)((P + kBN - 1) / kBN);
+    const int t64 = (rows + 63) / 64;
+    pl.bm = (long long)t64 * pl.ptiles >= 448 ? 64 : 32;
+    pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
+    nchunks = (kch * T + kBK - 1) / kBK;
+  } else {
+    // tile shape: fewest staged elements (halo + MFMA columns) over the image
+    static const int cand[4][2] = {{1, 64}, {2, 32}, {4, 16}, {8, 8}};
+    long long best = -1;
+    for (const auto& c : cand) {
+      const int th = c[0], tw = c[1];
+      const long long tiles = (long long)((H + th - 1) / th) * ((W + tw - 1) / tw);
+      const int halo = (th + KH - 1) * (tw + KW - 1);
+      const long long cost = tiles * (halo + 64);
+      if (halo <= 256 && (best < 0 || cost < best)) {
+        best = cost;
+        pl.TH = th;
+        pl.TW = tw;
+      }
+    }
+    pl.tiles_x = (W + pl.TW - 1) / pl.TW;
+    pl.tiles_img = ((H + pl.TH - 1) / pl.TH) * pl.tiles_x;
+    pl.ptiles = B * pl.tiles_img;
+    pl.HWd = pl.TW + KW - 1;
+    const int halo = (pl.TH + KH - 1) * pl.HWd;
+    pl.HPAD = halo + ((32 - halo % 64) + 64) % 64;   // channel stride = 32 mod 64 banks
+    const int t64 = (rows + 63) / 64;
+    pl.bm = (long long)t64 * pl.ptiles >= 480 ? 64 : 32;
+    pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
+    // channels per chunk: multiple of 4, <= 16, fits the LDS budget and the
+    // per-thread staging registers (<= 16 weights, <= 4 channels per wave)
+    const int kcap = ((kch + 3) / 4) * 4;
+    pl.CK = 4;
+    for (int ck = 16; ck >= 4; ck -= 4) {
+      const size_t stage = (size_t)T * ck * (pl.bm + 1) + (size_t)ck * pl.HPAD;
+      if (ck <= kcap && 2 * stage * sizeof(float) <= kHaloLds && ((size_t)pl.bm * ck * T + 255) / 256 <= 16) {
+        pl.CK = ck;
+        break;
+      }
+    }
+    pl.lds_bytes = 2 * ((size_t)T * pl.CK * (pl.bm + 1) + (size_t)pl.CK * pl.HPAD) * sizeof(float);
+    nchunks = (kch + pl.CK - 1) / pl.CK;
+  }
+  blocks = (long long)pl.row_tiles * pl.ptiles;
   int ks = 1;
-  if (blocks < 240) {   // under one block per CU: split K, >= 4 chunks per split
+  if (blocks < 240 || (pl.halo && blocks < 480)) {   // split K over blocks
     ks = (int)((480 + blocks - 1) / blocks);
     if (ks > 16) ks = 16;
-    if (ks > nchunks / 4) ks = nchunks / 4;
+    const int minc = pl.halo ? 1 : 4;
+    if (ks > nchunks / minc) ks = nchunks / minc;
     if (ks < 1) ks = 1;
   }
   pl.chunks_per_split = (nchunks + ks - 1) / ks;
@@ -556,14 +798,14 @@ WgPlan plan_wgrad(int Cin, int Cout, int T, long long P) {
 }
 
 size_t fwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
-  return plan_igemm(Cout, Cin, KH * KW, (long long)B * H * W).part_bytes;
+  return plan_igemm(Cout, Cin, KH, KW, B, H, W).part_bytes;
 }
 
 size_t bwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   const long long P = (long long)B * H * W;
   const int T = KH * KW;
   return align256((size_t)Cout * P * sizeof(float)) +              // pre-activation gradient
-         plan_igemm(Cin, Cout, T, P).part_bytes +                   // data-gradient split-K
+         plan_igemm(Cin, Cout, KH, KW, B, H, W).part_bytes +        // data-gradient split-K
          plan_wgrad(Cin, Cout, T, P).part_bytes;                    // weight-gradient partials
 }
 
@@ -644,18 +886,36 @@ Slice to_slice(const dro_slice* s) {
 // rows / kch set by the caller; `ws` must hold plan.part_bytes
 template <int MODE, int ACT, int EPI>
 int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
-  const IgPlan pl = plan_igemm(a.rows, a.kch, a.g.KH * a.g.KW, P);
+  const IgPlan pl = plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
   a.K = a.kch * a.g.KH * a.g.KW;
-  a.kdiv = make_fdiv(a.kch);
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
   const dim3 grid(pl.row_tiles * pl.ptiles, pl.ksplit);
-  if (pl.bm == 64)
-    hipLaunchKernelGGL((igemm_kernel<64, MODE, ACT, EPI>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((igemm_kernel<32, MODE, ACT, EPI>), grid, dim3(256), 0, s, a);
-  int st = launch_status("igemm_kernel launch failed");
+  if (pl.halo) {
+    const int T = a.g.KH * a.g.KW;
+    a.TH = pl.TH;
+    a.TW = pl.TW;
+    a.HWd = pl.HWd;
+    a.HPAD = pl.HPAD;
+    a.tiles_x = pl.tiles_x;
+    a.tiles_img = pl.tiles_img;
+    a.CK = pl.CK;
+    a.kdiv = make_fdiv(pl.CK * T);   // e -> weight row
+    a.cindiv = make_fdiv(T);         // -> channel, tap
+    a.kwdiv = make_fdiv(pl.HWd);     // halo element -> (hy, hx)
+    if (pl.bm == 64)
+      hipLaunchKernelGGL((dconv_kernel<64, MODE, ACT, EPI>), grid, dim3(256), pl.lds_bytes, s, a);
+    else
+      hipLaunchKernelGGL((dconv_kernel<32, MODE, ACT, EPI>), grid, dim3(256), pl.lds_bytes, s, a);
+  } else {
+    a.kdiv = make_fdiv(a.kch);
+    if (pl.bm == 64)
+      hipLaunchKernelGGL((igemm_kernel<64, MODE, ACT, EPI>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((igemm_kernel<32, MODE, ACT, EPI>), grid, dim3(256), 0, s, a);
+  }
+  int st = launch_status("conv kernel launch failed");
   if (st || pl.ksplit == 1) return st;
   const long long total = (long long)a.rows * P;
   long long blocks = (total + 255) / 256;
@@ -834,7 +1094,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   char* ws = static_cast<char*>(workspace);
   char* ws_pre = ws;
   char* ws_ig = ws_pre + align256((size_t)Cout * P * sizeof(float));
-  char* ws_wg = ws_ig + plan_igemm(a.g.Cin, Cout, T, P).part_bytes;
+  char* ws_wg = ws_ig + plan_igemm(a.g.Cin, Cout, KH, KW, B, H, W).part_bytes;
   if (pre) {
     const size_t total = (size_t)Cout * P;
     size_t blocks = (total + 255) / 256;
