@@ -97,6 +97,7 @@ struct IgArgs {
   // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
   // tile + halo staged once per channel chunk of CK channels
   int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
+  FastDiv ckt_div, t_div, hwd_div;   // divisors CK*T, T, HWd
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -383,9 +384,7 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int CKT = CK * T;
   const int wtotal = BM * CKT;
   const int wper = (wtotal + 255) / 256;      // <= 16 (checked on the host)
-  const FastDiv ckt_div = a.kdiv;             // divisor CK*T (set by the host)
-  const FastDiv t_div = a.cindiv;             // divisor T
-  const FastDiv hwd_div = a.kwdiv;            // divisor HWd
+  const FastDiv ckt_div = a.ckt_div, t_div = a.t_div, hwd_div = a.hwd_div;
 
   float xr[16], wv[16];
   unsigned xmask = 0, wmask = 0;
@@ -708,11 +707,13 @@ struct IgPlan {
 
 constexpr size_t kHaloLds = 64 * 1024;   // per block: two blocks per CU
 
+IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W);
+
 IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
   IgPlan pl = {};
   const int T = KH * KW;
   const long long P = (long long)B * H * W;
-  pl.halo = T > 1;
+  pl.halo = T > 1 && T <= 9;
   long long blocks;
   int nchunks;
   if (!pl.halo) {
@@ -748,7 +749,7 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
     // channels per chunk: multiple of 4, <= 16, fits the LDS budget and the
     // per-thread staging registers (<= 16 weights, <= 4 channels per wave)
     const int kcap = ((kch + 3) / 4) * 4;
-    pl.CK = 4;
+    pl.CK = 0;
     for (int ck = 16; ck >= 4; ck -= 4) {
       const size_t stage = (size_t)T * ck * (pl.bm + 1) + (size_t)ck * pl.HPAD;
       if (ck <= kcap && 2 * stage * sizeof(float) <= kHaloLds && ((size_t)pl.bm * ck * T + 255) / 256 <= 16) {
@@ -756,7 +757,9 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
         break;
       }
     }
+    if (pl.CK == 0) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
     pl.lds_bytes = 2 * ((size_t)T * pl.CK * (pl.bm + 1) + (size_t)pl.CK * pl.HPAD) * sizeof(float);
+    if (pl.lds_bytes < 2 * 16 * 64 * sizeof(float)) pl.lds_bytes = 2 * 16 * 64 * sizeof(float);  // K-half reduction
     nchunks = (kch + pl.CK - 1) / pl.CK;
   }
   blocks = (long long)pl.row_tiles * pl.ptiles;
@@ -766,6 +769,31 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
     if (ks > 16) ks = 16;
     const int minc = pl.halo ? 1 : 4;
     if (ks > nchunks / minc) ks = nchunks / minc;
+    if (ks < 1) ks = 1;
+  }
+  pl.chunks_per_split = (nchunks + ks - 1) / ks;
+  pl.ksplit = (nchunks + pl.chunks_per_split - 1) / pl.chunks_per_split;
+  pl.part_bytes = pl.ksplit > 1 ? align256((size_t)pl.ksplit * rows * P * sizeof(float)) : 0;
+  return pl;
+}
+
+// the flattened-pixel implicit GEMM (1x1 and large kernels)
+IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W) {
+  IgPlan pl = {};
+  const int T = KH * KW;
+  const long long P = (long long)B * H * W;
+  pl.halo = false;
+  pl.ptiles = (int)((P + kBN - 1) / kBN);
+  const int t64 = (rows + 63) / 64;
+  pl.bm = (long long)t64 * pl.ptiles >= 448 ? 64 : 32;
+  pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
+  const int nchunks = (kch * T + kBK - 1) / kBK;
+  const long long blocks = (long long)pl.row_tiles * pl.ptiles;
+  int ks = 1;
+  if (blocks < 240) {
+    ks = (int)((480 + blocks - 1) / blocks);
+    if (ks > 16) ks = 16;
+    if (ks > nchunks / 4) ks = nchunks / 4;
     if (ks < 1) ks = 1;
   }
   pl.chunks_per_split = (nchunks + ks - 1) / ks;
@@ -901,9 +929,9 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.tiles_x = pl.tiles_x;
     a.tiles_img = pl.tiles_img;
     a.CK = pl.CK;
-    a.kdiv = make_fdiv(pl.CK * T);   // e -> weight row
-    a.cindiv = make_fdiv(T);         // -> channel, tap
-    a.kwdiv = make_fdiv(pl.HWd);     // halo element -> (hy, hx)
+    a.ckt_div = make_fdiv(pl.CK * T);   // weight element -> row
+    a.t_div = make_fdiv(T);             // -> channel, tap
+    a.hwd_div = make_fdiv(pl.HWd);      // halo element -> (hy, hx)
     if (pl.bm == 64)
       hipLaunchKernelGGL((dconv_kernel<64, MODE, ACT, EPI>), grid, dim3(256), pl.lds_bytes, s, a);
     else
@@ -946,6 +974,19 @@ int check_ws(const void* ws, size_t have, size_t need, const char* what) {
     case 3: { constexpr int A_ = 3; __VA_ARGS__; } break; \
     default: set_error("conv2d: unknown activation"); return DRO_E_MODE; \
   }
+
+extern "C" int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, int W, long long* info) {
+  if (!info || rows < 1 || kch < 1 || KH < 1 || KW < 1 || B < 1 || H < 1 || W < 1) {
+    set_error("conv2d_plan: bad arguments");
+    return DRO_E_SHAPE;
+  }
+  const IgPlan pl = plan_igemm(rows, kch, KH, KW, B, H, W);
+  const long long v[16] = {pl.halo, pl.bm, pl.row_tiles, pl.ptiles, pl.ksplit, pl.chunks_per_split,
+                           pl.TH, pl.TW, pl.HWd, pl.HPAD, pl.tiles_x, pl.tiles_img, pl.CK,
+                           (long long)pl.lds_bytes, (long long)pl.part_bytes, 0};
+  for (int i = 0; i < 16; ++i) info[i] = v[i];
+  return DRO_OK;
+}
 
 extern "C" size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   if (B < 1 || H < 1 || W < 1 || Cin < 1 || Cout < 1 || KH < 1 || KW < 1) return 0;

@@ -167,6 +167,13 @@ typedef struct dro_slice {
  * of at least this size as `workspace`.  No call keeps state in it. */
 size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int Cout, int KH, int KW);
 
+/* Diagnostics: the launch plan the forward (rows = Cout, kch = Cin) or data
+ * gradient (rows = Cin, kch = Cout) would use, as 16 integers: halo, BM,
+ * row tiles, pixel tiles, K splits, chunks per split, TH, TW, halo row width,
+ * channel stride, tiles per row, tiles per image, channels per chunk, LDS bytes,
+ * split-K partial bytes, 0. */
+int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, int W, long long* info);
+
 int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
                        int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
                        float* out, int out_ctot, int out_coff, void* workspace,

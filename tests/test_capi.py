@@ -83,3 +83,45 @@ def test_no_cpu_fallback():
         H.warp_cost(x, x.unsqueeze(0), torch.ones(1, 1, 2, 2), torch.zeros(1, 6), torch.eye(3).unsqueeze(0))
     with pytest.raises(RuntimeError):
         H.convex_upsample(torch.zeros(1, 1, 2, 2), torch.zeros(1, 576, 2, 2))
+
+
+# every conv shape of the update blocks / heads / GRU (hd 64 and 128) and the
+# parity tests, forward (rows=Cout, kch=Cin) and data gradient (rows=Cin, kch=Cout)
+CONV_SHAPES = [  # (Cin, Cout, KH, KW)
+    (160, 128, 1, 5), (160, 64, 1, 5), (160, 128, 5, 1), (160, 64, 5, 1),
+    (320, 256, 1, 5), (320, 128, 1, 5), (320, 256, 5, 1), (320, 128, 5, 1),
+    (128, 64, 1, 1), (64, 64, 3, 3), (1, 64, 7, 7), (6, 64, 7, 7), (128, 63, 3, 3), (128, 58, 3, 3),
+    (64, 192, 3, 3), (64, 1, 3, 3), (128, 576, 1, 1), (64, 6, 3, 3), (128, 128, 3, 3), (128, 1, 3, 3),
+    (256, 128, 3, 3), (128, 6, 3, 3), (128, 256, 3, 3), (256, 576, 1, 1), (48, 45, 5, 3), (128, 128, 3, 3),
+    (1, 128, 7, 7), (6, 128, 7, 7),
+]
+IMAGES = [(2, 24, 80), (4, 24, 80), (2, 24, 40), (3, 7, 13), (1, 8, 12), (8, 30, 40), (16, 30, 40)]
+
+
+def test_conv_plans_within_kernel_limits(lib):
+    """Host-side launch plans respect the limits the kernels are written for
+    (per-thread staging registers, LDS budget, K-half reduction buffer)."""
+    import ctypes
+    info = (ctypes.c_longlong * 16)()
+    for Cin, Cout, KH, KW in CONV_SHAPES:
+        for B, H, W in IMAGES:
+            for rows, kch in ((Cout, Cin), (Cin, Cout)):
+                assert lib.dro_conv2d_plan(rows, kch, KH, KW, B, H, W, info) == 0
+                halo, bm, rt, pt, ks, cps, TH, TW, HWd, HPAD, tx, timg, CK, lds, part, _ = list(info)
+                assert bm in (32, 64) and rt * bm >= rows and ks >= 1 and cps >= 1
+                if not halo:
+                    assert KH * KW == 1 or KH * KW > 9 or CK == 0
+                    continue
+                T = KH * KW
+                assert TH * TW == 64 and HWd == TW + KW - 1
+                halo_n = (TH + KH - 1) * HWd
+                assert halo_n <= 256 and HPAD >= halo_n and HPAD % 64 == 32
+                assert CK % 4 == 0 and 4 <= CK <= 16
+                assert (bm * CK * T + 255) // 256 <= 16            # weight slots per thread
+                stage = T * CK * (bm + 1) + CK * HPAD
+                assert lds == max(2 * stage * 4, 2 * 16 * 64 * 4) <= 64 * 1024
+                assert tx == -(-W // TW) and timg == -(-H // TH) * tx and pt == B * timg
+                nck = -(-kch // CK)
+                assert cps * ks >= nck and cps * (ks - 1) < nck
+                if ks > 1:
+                    assert part >= ks * rows * B * H * W * 4

@@ -17,6 +17,9 @@ run() {  # name seconds cmd...
   local st=$?
   echo "   exit $st"; tail -n 5 "$OUT/$name.log"
   if crash $st; then echo "!! crash-class exit $st in $name: stopping"; exit $st; fi
+  if grep -qE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR|AcceleratorError" "$OUT/$name.log"; then
+    echo "!! GPU fault reported in $name: stopping"; exit 99
+  fi
   return 0
 }
 for step in "$@"; do
