@@ -97,7 +97,8 @@ struct IgArgs {
   // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
   // tile + halo staged once per channel chunk of CK channels
   int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
-  FastDiv ckt_div, t_div, hwd_div;   // divisors CK*T, T, HWd
+  int wstride;                       // LDS row stride of the weight tile
+  FastDiv ckt_div, t_div, hwd_div;   // divisors: weight run length, T, HWd
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -346,11 +347,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 // Same GEMM as igemm_kernel, but a block's 64 pixels are a TH x TW tile of one
 // image and each K chunk is CK channels x ALL taps: the CK x (TH+KH-1) x
 // (TW+KW-1) input patch is staged once (each element loaded once, instead of
-// once per tap) and the B operand of tap (ty, tx) is a shifted LDS read.  The
-// weight chunk W[rows][CK][T] (contiguous per row) is staged as [tap][c][row].
+// once per tap) and the B operand of tap (ty, tx) is a shifted LDS read.
+// The weight chunk is copied as the contiguous runs it has in global memory:
+// forward: BM rows x (CK*T) floats (row stride `wstride` in LDS, odd so the
+// A-operand reads, one row per lane, are bank-conflict free); data gradient:
+// CK output channels x (BM*T) floats.  Staging address math is chunk
+// independent except for one scalar per row, and all loads are unconditional
+// (weights from clamped addresses: padded rows/channels only ever meet zero
+// inputs or discarded outputs).
 // MODE 0 forward, MODE 1 data gradient (tap flipped).  BM = 64: 2x2 waves of
 // 32x32; BM = 32: 2 pixel halves x 2 channel halves (LDS reduction).
-// Dynamic LDS: 2 stages of T*CK*(BM+1) + CK*HPAD floats.
+// Dynamic LDS: 2 stages of (weight tile + CK*HPAD) floats.
 template <int BM, int MODE, int ACT, int EPI>
 __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   extern __shared__ float smem[];
@@ -358,10 +365,11 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W, KH = a.g.KH, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
   const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch;
-  const int TW = a.TW, HWd = a.HWd, HPAD = a.HPAD, CK = a.CK;
-  const int T = KH * KW;
+  const int TW = a.TW, HWd = a.HWd, HPAD = a.HPAD, CK = a.CK, WS = a.wstride;
+  const int T = KH * KW, CinT = Cin * T;
   const int HALO = (a.TH + KH - 1) * HWd;
-  const int WSZ = T * CK * (BM + 1), STAGE = WSZ + CK * HPAD;
+  const int WSZ = MODE == 0 ? BM * WS : CK * WS;
+  const int STAGE = WSZ + CK * HPAD;
   const float* __restrict__ Wt = a.weight;
   const float* __restrict__ Gp = a.G;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -375,61 +383,72 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int nck = (kch + CK - 1) / CK;
   const int cbeg = blockIdx.y * a.chunks_per_split;
   const int cend = min(nck, cbeg + a.chunks_per_split);
-  const int hy0 = ty0 - PH, hx0 = tx0 - PW;    // halo origin in the image
 
-  // X staging: wave w stages channels w, w+4, ...; lanes run over the halo
-  const int xper = (CK + 3) / 4;              // channels per wave (<= 4)
-  const int nj = (HALO + 63) / 64;            // halo passes per channel (<= 4)
-  // W staging: element e = tid + 256 i of the BM x (CK*T) chunk block
-  const int CKT = CK * T;
-  const int wtotal = BM * CKT;
+  // X staging: wave w stages channels w, w+4, .. (<= 4 per wave); lanes run
+  // over the halo in up to 4 passes whose pixel offsets are chunk independent
+  const int xper = (CK + 3) / 4;
+  const int nj = (HALO + 63) / 64;
+  int xpix[4];
+  unsigned xok = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = lane + 64 * j;
+    const int hy = fdiv(e, a.hwd_div), hx = e - hy * HWd;
+    const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
+    const bool ok = j < nj && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+    xpix[j] = ok ? yy * W + xx : 0;
+    xok |= ok ? (1u << j) : 0u;
+  }
+  // W staging: NRUN contiguous runs of RUN floats, element e = tid + 256 i
+  const int RUN = MODE == 0 ? CK * T : BM * T;
+  const int wtotal = (MODE == 0 ? BM : CK) * RUN;
   const int wper = (wtotal + 255) / 256;      // <= 16 (checked on the host)
-  const FastDiv ckt_div = a.ckt_div, t_div = a.t_div, hwd_div = a.hwd_div;
+  const FastDiv run_div = a.ckt_div;          // divisor RUN
+  const unsigned wlast = (unsigned)Cout * CinT - 1;
 
   float xr[16], wv[16];
-  unsigned xmask = 0, wmask = 0;
+  unsigned xmask = 0;
   auto load = [&](int chunk) {
     const int c0 = chunk * CK;
     xmask = 0;
-    wmask = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (i < xper) {
+        const int cl = wave + 4 * i;
+        const int ch = __builtin_amdgcn_readfirstlane(c0 + cl);
+        const bool chok = cl < CK && ch < kch;
+        const float* p;
+        unsigned sbase;
+        bool M;
+        if (MODE == 0) {
+          const RowDesc d = row_desc(cb1, cb2, cb3, chok ? ch : 0, HWu);
+          p = d.p;
+          sbase = (unsigned)b * d.A + d.Bc;
+          M = d.M;
+        } else {
+          p = Gp;
+          sbase = ((unsigned)b * (unsigned)Cout + (unsigned)(chok ? ch : 0)) * HWu;
+          M = true;
+        }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int slot = i * 4 + j;
-        if (i < xper && j < nj) {
-          const int cl = wave + 4 * i;
-          const int ch = __builtin_amdgcn_readfirstlane(c0 + cl);
-          const int e = lane + 64 * j;
-          const int hy = fdiv(e, hwd_div), hx = e - hy * HWd;
-          const int yy = hy0 + hy, xx = hx0 + hx;
-          const bool ok = cl < CK && ch < kch && e < HALO && (unsigned)yy < (unsigned)H &&
-                          (unsigned)xx < (unsigned)W;
-          const unsigned pix = (unsigned)(yy * W + xx);
-          xmask |= ok ? (1u << slot) : 0u;
-          if (MODE == 0) {
-            const RowDesc d = row_desc(cb1, cb2, cb3, ch < kch ? ch : 0, HWu);
-            const unsigned off = (unsigned)b * d.A + d.Bc + (d.M ? pix : 0u);
-            xr[slot] = d.p[ok ? off : 0u];
-          } else {
-            const unsigned off = ((unsigned)b * (unsigned)Cout + (unsigned)ch) * HWu + pix;
-            xr[slot] = Gp[ok ? off : 0u];
+        for (int j = 0; j < 4; ++j) {
+          if (j < nj) {
+            const bool ok = chok && ((xok >> j) & 1u);
+            xmask |= ok ? (1u << (i * 4 + j)) : 0u;
+            xr[i * 4 + j] = p[ok ? sbase + (M ? (unsigned)xpix[j] : 0u) : 0u];
           }
         }
       }
     }
+    const unsigned gdelta = MODE == 0 ? (unsigned)c0 * T : (unsigned)c0 * CinT;
+    const unsigned gfix = MODE == 0 ? (unsigned)row0 * CinT : (unsigned)row0 * T;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       if (i < wper) {
         const int e = tid + 256 * i;
-        const int r = fdiv(e, ckt_div), rem = e - r * CKT;
-        const int cl = fdiv(rem, t_div), tap = rem - cl * T;
-        const int row = row0 + r, ch = c0 + cl;
-        const bool ok = e < wtotal && row < rows && ch < kch;
-        wmask |= ok ? (1u << i) : 0u;
-        const unsigned idx = MODE == 0 ? ((unsigned)row * Cin + ch) * T + tap
-                                       : ((unsigned)ch * Cin + row) * T + tap;
-        wv[i] = Wt[ok ? idx : 0u];
+        const int run = fdiv(e, run_div), rem = e - run * RUN;
+        const unsigned g = gfix + gdelta + (unsigned)run * CinT + (unsigned)rem;
+        wv[i] = Wt[g < wlast ? g : wlast];
       }
     }
   };
@@ -440,10 +459,9 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int slot = i * 4 + j;
         const int cl = wave + 4 * i, e = lane + 64 * j;
         if (i < xper && j < nj && cl < CK && e < HPAD)
-          Xs[cl * HPAD + e] = (xmask >> slot) & 1u ? xr[slot] : 0.f;
+          Xs[cl * HPAD + e] = (xmask >> (i * 4 + j)) & 1u ? xr[i * 4 + j] : 0.f;
       }
     }
 #pragma unroll
@@ -451,9 +469,8 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
       if (i < wper) {
         const int e = tid + 256 * i;
         if (e < wtotal) {
-          const int r = fdiv(e, ckt_div), rem = e - r * CKT;
-          const int cl = fdiv(rem, t_div), tap = rem - cl * T;
-          Ws[(tap * CK + cl) * (BM + 1) + r] = (wmask >> i) & 1u ? wv[i] : 0.f;
+          const int run = fdiv(e, run_div), rem = e - run * RUN;
+          Ws[run * WS + rem] = wv[i];
         }
       }
     }
@@ -466,8 +483,11 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int qy = q / TW, qx = q - qy * TW;
   const int qoff = qy * HWd + qx;
   const int hi = lane >> 5;
+  const int arow = wr * 32 + (lane & 31);       // this lane's A row in the tile
   const int CKh = CK / 2;
   const int s_lo = (WM == 2) ? 0 : wk * (CKh / 2), s_hi = (WM == 2) ? CKh : s_lo + CKh / 2;
+  const int astep = MODE == 0 ? 2 * T : 2 * WS;  // A offset per channel pair
+  const int abase = MODE == 0 ? arow * WS + hi * T : hi * WS + arow * T;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -487,11 +507,11 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
       for (int tx = 0; tx < KW; ++tx) {
         const int tap = ty * KW + tx;
         const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
-        const float* wa = Ws + (tap * CK + hi) * (BM + 1) + wr * 32 + (lane & 31);
+        const float* wa = Ws + abase + tap;
         const float* xb = Xs + hi * HPAD + qoff + toff;
 #pragma unroll 4
         for (int s = s_lo; s < s_hi; ++s)
-          acc = mfma32(wa[2 * s * (BM + 1)], xb[2 * s * HPAD], acc);
+          acc = mfma32(wa[s * astep], xb[2 * s * HPAD], acc);
       }
     }
     if (more) store(buf ^ 1);
@@ -707,6 +727,15 @@ struct IgPlan {
 
 constexpr size_t kHaloLds = 64 * 1024;   // per block: two blocks per CU
 
+int odd_up(int n) { return n | 1; }
+
+// weight tile floats, the larger of the two layouts (forward: BM rows of
+// CK*T; data gradient: CK channels of BM*T), rows padded to an odd stride
+size_t halo_wtile(int bm, int ck, int T) {
+  const size_t f = (size_t)bm * odd_up(ck * T), d = (size_t)ck * odd_up(bm * T);
+  return f > d ? f : d;
+}
+
 IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W);
 
 IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
@@ -751,14 +780,14 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
     const int kcap = ((kch + 3) / 4) * 4;
     pl.CK = 0;
     for (int ck = 16; ck >= 4; ck -= 4) {
-      const size_t stage = (size_t)T * ck * (pl.bm + 1) + (size_t)ck * pl.HPAD;
+      const size_t stage = halo_wtile(pl.bm, ck, T) + (size_t)ck * pl.HPAD;
       if (ck <= kcap && 2 * stage * sizeof(float) <= kHaloLds && ((size_t)pl.bm * ck * T + 255) / 256 <= 16) {
         pl.CK = ck;
         break;
       }
     }
     if (pl.CK == 0) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
-    pl.lds_bytes = 2 * ((size_t)T * pl.CK * (pl.bm + 1) + (size_t)pl.CK * pl.HPAD) * sizeof(float);
+    pl.lds_bytes = 2 * (halo_wtile(pl.bm, pl.CK, T) + (size_t)pl.CK * pl.HPAD) * sizeof(float);
     if (pl.lds_bytes < 2 * 16 * 64 * sizeof(float)) pl.lds_bytes = 2 * 16 * 64 * sizeof(float);  // K-half reduction
     nchunks = (kch + pl.CK - 1) / pl.CK;
   }
@@ -929,8 +958,10 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.tiles_x = pl.tiles_x;
     a.tiles_img = pl.tiles_img;
     a.CK = pl.CK;
-    a.ckt_div = make_fdiv(pl.CK * T);   // weight element -> row
-    a.t_div = make_fdiv(T);             // -> channel, tap
+    const int run = MODE == 0 ? pl.CK * T : pl.bm * T;   // contiguous weight run
+    a.wstride = odd_up(run);
+    a.ckt_div = make_fdiv(run);
+    a.t_div = make_fdiv(T);
     a.hwd_div = make_fdiv(pl.HWd);      // halo element -> (hy, hx)
     if (pl.bm == 64)
       hipLaunchKernelGGL((dconv_kernel<64, MODE, ACT, EPI>), grid, dim3(256), pl.lds_bytes, s, a);

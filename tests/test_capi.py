@@ -118,7 +118,8 @@ def test_conv_plans_within_kernel_limits(lib):
                 assert halo_n <= 256 and HPAD >= halo_n and HPAD % 64 == 32
                 assert CK % 4 == 0 and 4 <= CK <= 16
                 assert (bm * CK * T + 255) // 256 <= 16            # weight slots per thread
-                stage = T * CK * (bm + 1) + CK * HPAD
+                odd = lambda n: n | 1
+                stage = max(bm * odd(CK * T), CK * odd(bm * T)) + CK * HPAD
                 assert lds == max(2 * stage * 4, 2 * 16 * 64 * 4) <= 64 * 1024
                 assert tx == -(-W // TW) and timg == -(-H // TH) * tx and pt == B * timg
                 nck = -(-kch // CK)
