@@ -358,21 +358,22 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 // MODE 0 forward, MODE 1 data gradient (tap flipped).  BM = 64: 2x2 waves of
 // 32x32; BM = 32: 2 pixel halves x 2 channel halves (LDS reduction).
 // Dynamic LDS: 2 stages of (weight tile + CK*HPAD) floats.
-template <int BM, int MODE, int ACT, int EPI>
+template <int BM, int CK, int MODE, int ACT, int EPI>
 __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   extern __shared__ float smem[];
   constexpr int WM = BM / 32;
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W, KH = a.g.KH, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
   const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch;
-  const int TW = a.TW, HWd = a.HWd, HPAD = a.HPAD, CK = a.CK, WS = a.wstride;
+  const int TW = a.TW, HWd = a.HWd, HPAD = a.HPAD, WS = a.wstride;
   const int T = KH * KW, CinT = Cin * T;
   const int HALO = (a.TH + KH - 1) * HWd;
   const int WSZ = MODE == 0 ? BM * WS : CK * WS;
   const int STAGE = WSZ + CK * HPAD;
   const float* __restrict__ Wt = a.weight;
   const float* __restrict__ Gp = a.G;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar)
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
   const int row0 = rt * BM;
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
 
   // X staging: wave w stages channels w, w+4, .. (<= 4 per wave); lanes run
   // over the halo in up to 4 passes whose pixel offsets are chunk independent
-  const int xper = (CK + 3) / 4;
+  constexpr int xper = CK / 4;
   const int nj = (HALO + 63) / 64;
   int xpix[4];
   unsigned xok = 0;
@@ -484,8 +485,8 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int qoff = qy * HWd + qx;
   const int hi = lane >> 5;
   const int arow = wr * 32 + (lane & 31);       // this lane's A row in the tile
-  const int CKh = CK / 2;
-  const int s_lo = (WM == 2) ? 0 : wk * (CKh / 2), s_hi = (WM == 2) ? CKh : s_lo + CKh / 2;
+  constexpr int NS = (WM == 2) ? CK / 2 : CK / 4;   // channel pairs per wave per tap
+  const int s_lo = (WM == 2) ? 0 : wk * NS;
   const int astep = MODE == 0 ? 2 * T : 2 * WS;  // A offset per channel pair
   const int abase = MODE == 0 ? arow * WS + hi * T : hi * WS + arow * T;
   f32x16 acc;
@@ -509,9 +510,14 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
         const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
         const float* wa = Ws + abase + tap;
         const float* xb = Xs + hi * HPAD + qoff + toff;
-#pragma unroll 4
-        for (int s = s_lo; s < s_hi; ++s)
-          acc = mfma32(wa[s * astep], xb[2 * s * HPAD], acc);
+        float av[NS], bv[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          av[s] = wa[(s_lo + s) * astep];
+          bv[s] = xb[2 * (s_lo + s) * HPAD];
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc = mfma32(av[s], bv[s], acc);
       }
     }
     if (more) store(buf ^ 1);
@@ -775,18 +781,15 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
     const int t64 = (rows + 63) / 64;
     pl.bm = (long long)t64 * pl.ptiles >= 480 ? 64 : 32;
     pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
-    // channels per chunk: multiple of 4, <= 16, fits the LDS budget and the
-    // per-thread staging registers (<= 16 weights, <= 4 channels per wave)
-    const int kcap = ((kch + 3) / 4) * 4;
-    pl.CK = 0;
-    for (int ck = 16; ck >= 4; ck -= 4) {
-      const size_t stage = halo_wtile(pl.bm, ck, T) + (size_t)ck * pl.HPAD;
-      if (ck <= kcap && 2 * stage * sizeof(float) <= kHaloLds && ((size_t)pl.bm * ck * T + 255) / 256 <= 16) {
-        pl.CK = ck;
-        break;
-      }
-    }
-    if (pl.CK == 0) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
+    // channels per chunk (a template parameter of the kernel): BM=32 -> 16,
+    // BM=64 -> 8, halved for T > 5, so a thread stages <= 16 weights and
+    // <= 4 channels per wave; small-Cin convs keep the smaller chunk
+    pl.CK = (pl.bm == 32 ? 16 : 8) / (T > 5 ? 2 : 1);
+    if (pl.bm == 32 && pl.CK == 16 && kch <= 8) pl.CK = 8;
+    if (pl.bm == 64 && pl.CK == 8 && kch <= 4) pl.CK = 4;
+    const size_t stage = halo_wtile(pl.bm, pl.CK, T) + (size_t)pl.CK * pl.HPAD;
+    if (2 * stage * sizeof(float) > kHaloLds || ((size_t)pl.bm * pl.CK * T + 255) / 256 > 16)
+      return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
     pl.lds_bytes = 2 * (halo_wtile(pl.bm, pl.CK, T) + (size_t)pl.CK * pl.HPAD) * sizeof(float);
     if (pl.lds_bytes < 2 * 16 * 64 * sizeof(float)) pl.lds_bytes = 2 * 16 * 64 * sizeof(float);  // K-half reduction
     nchunks = (kch + pl.CK - 1) / pl.CK;
@@ -963,10 +966,19 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.ckt_div = make_fdiv(run);
     a.t_div = make_fdiv(T);
     a.hwd_div = make_fdiv(pl.HWd);      // halo element -> (hy, hx)
-    if (pl.bm == 64)
-      hipLaunchKernelGGL((dconv_kernel<64, MODE, ACT, EPI>), grid, dim3(256), pl.lds_bytes, s, a);
-    else
-      hipLaunchKernelGGL((dconv_kernel<32, MODE, ACT, EPI>), grid, dim3(256), pl.lds_bytes, s, a);
+    const size_t lds = pl.lds_bytes;
+    if (pl.bm == 64 && pl.CK == 8)
+      hipLaunchKernelGGL((dconv_kernel<64, 8, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
+    else if (pl.bm == 64 && pl.CK == 4)
+      hipLaunchKernelGGL((dconv_kernel<64, 4, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
+    else if (pl.bm == 32 && pl.CK == 16)
+      hipLaunchKernelGGL((dconv_kernel<32, 16, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
+    else if (pl.bm == 32 && pl.CK == 8)
+      hipLaunchKernelGGL((dconv_kernel<32, 8, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
+    else {
+      set_error("conv: no kernel for this halo plan");
+      return DRO_E_SHAPE;
+    }
   } else {
     a.kdiv = make_fdiv(a.kch);
     if (pl.bm == 64)

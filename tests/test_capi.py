@@ -116,7 +116,7 @@ def test_conv_plans_within_kernel_limits(lib):
                 assert TH * TW == 64 and HWd == TW + KW - 1
                 halo_n = (TH + KH - 1) * HWd
                 assert halo_n <= 256 and HPAD >= halo_n and HPAD % 64 == 32
-                assert CK % 4 == 0 and 4 <= CK <= 16
+                assert (bm, CK) in ((32, 16), (32, 8), (64, 8), (64, 4))
                 assert (bm * CK * T + 255) // 256 <= 16            # weight slots per thread
                 odd = lambda n: n | 1
                 stage = max(bm * odd(CK * T), CK * odd(bm * T)) + CK * HPAD
