@@ -37,6 +37,7 @@
 
 #include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 
 #include "dro_common.hpp"
 
@@ -97,8 +98,6 @@ struct IgArgs {
   // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
   // tile + halo staged once per channel chunk of CK channels
   int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
-  int wstride;                       // LDS row stride of the weight tile
-  FastDiv ckt_div, t_div, hwd_div;   // divisors: weight run length, T, HWd
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -349,7 +348,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 // (TW+KW-1) input patch is staged once (each element loaded once, instead of
 // once per tap) and the B operand of tap (ty, tx) is a shifted LDS read.
 // The weight chunk is copied as the contiguous runs it has in global memory:
-// forward: BM rows x (CK*T) floats (row stride `wstride` in LDS, odd so the
+// forward: BM rows x (CK*T) floats (odd LDS row stride, so the
 // A-operand reads, one row per lane, are bank-conflict free); data gradient:
 // CK output channels x (BM*T) floats.  Staging address math is chunk
 // independent except for one scalar per row, and all loads are unconditional
@@ -357,19 +356,45 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 // inputs or discarded outputs).
 // MODE 0 forward, MODE 1 data gradient (tap flipped).  BM = 64: 2x2 waves of
 // 32x32; BM = 32: 2 pixel halves x 2 channel halves (LDS reduction).
-// Dynamic LDS: 2 stages of (weight tile + CK*HPAD) floats.
-template <int BM, int CK, int MODE, int ACT, int EPI>
+// Static LDS: 2 stages of (weight tile + CK*HPAD) floats (HaloShape).
+// Compile-time shape of the halo kernel: kernel (KH, KW) -> pixel tile and
+// channels per chunk.  1x5: 4x16 tiles (halo 4x20); 5x1 and 3x3: 8x8 tiles
+// (halo 12x8 / 10x10).  CK: 16 (BM 32) / 8 (BM 64), halved for 3x3, so a
+// thread stages <= 16 weights and <= 4 channels per wave per chunk.
+template <int BM, int KH, int KW>
+struct HaloShape {
+  static constexpr int T = KH * KW;
+  static constexpr int TH = KW == 1 || (KH == 3 && KW == 3) ? 8 : 4;
+  static constexpr int TW = 64 / TH;
+  static constexpr int HWd = TW + KW - 1;
+  static constexpr int HALO = (TH + KH - 1) * HWd;
+  static constexpr int HPAD = HALO + ((32 - HALO % 64) + 64) % 64;   // channel stride = 32 mod 64 banks
+  static constexpr int NJ = (HALO + 63) / 64;
+  static constexpr int CK = (BM == 32 ? 16 : 8) / (T > 5 ? 2 : 1);
+  static constexpr int RUN0 = CK * T, RUN1 = BM * T;                 // weight runs (fwd / dgrad)
+  static constexpr int WS0 = RUN0 | 1, WS1 = RUN1 | 1;               // odd LDS strides
+  static constexpr int WTOT = BM * CK * T;
+  static constexpr int WPER = (WTOT + 255) / 256;
+  static constexpr int WSZ0 = BM * WS0, WSZ1 = CK * WS1;
+  static constexpr int STAGE = (WSZ0 > WSZ1 ? WSZ0 : WSZ1) + CK * HPAD;
+  static constexpr int LDS = 2 * STAGE > 2 * 16 * 64 ? 2 * STAGE : 2 * 16 * 64;   // floats
+  static_assert(NJ <= 4 && WPER <= 16 && CK % 4 == 0 && TH * TW == 64, "halo shape");
+};
+
+template <int BM, int KH, int KW, int MODE, int ACT, int EPI>
 __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
-  extern __shared__ float smem[];
+  using S = HaloShape<BM, KH, KW>;
+  constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
+  constexpr int CK = S::CK, NJ = S::NJ, XPER = CK / 4;
+  constexpr int RUN = MODE == 0 ? S::RUN0 : S::RUN1, WS = MODE == 0 ? S::WS0 : S::WS1;
+  constexpr int WSZ = MODE == 0 ? S::WSZ0 : S::WSZ1, STAGE = S::STAGE;
   constexpr int WM = BM / 32;
+  constexpr int PH = KH / 2, PW = KW / 2;
+  __shared__ float smem[S::LDS];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
-  const int H = a.g.H, W = a.g.W, KH = a.g.KH, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
+  const int H = a.g.H, W = a.g.W;
   const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch;
-  const int TW = a.TW, HWd = a.HWd, HPAD = a.HPAD, WS = a.wstride;
-  const int T = KH * KW, CinT = Cin * T;
-  const int HALO = (a.TH + KH - 1) * HWd;
-  const int WSZ = MODE == 0 ? BM * WS : CK * WS;
-  const int STAGE = WSZ + CK * HPAD;
+  const int CinT = Cin * T;
   const float* __restrict__ Wt = a.weight;
   const float* __restrict__ Gp = a.G;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -378,101 +403,84 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
   const int row0 = rt * BM;
   const int b = pt / a.tiles_img, trem = pt - b * a.tiles_img;
-  const int ty0 = (trem / a.tiles_x) * a.TH, tx0 = (trem % a.tiles_x) * TW;
+  const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
   const size_t HW = (size_t)H * W;
   const unsigned HWu = (unsigned)HW;
   const int nck = (kch + CK - 1) / CK;
   const int cbeg = blockIdx.y * a.chunks_per_split;
   const int cend = min(nck, cbeg + a.chunks_per_split);
 
-  // X staging: wave w stages channels w, w+4, .. (<= 4 per wave); lanes run
-  // over the halo in up to 4 passes whose pixel offsets are chunk independent
-  constexpr int xper = CK / 4;
-  const int nj = (HALO + 63) / 64;
-  int xpix[4];
+  // X staging: wave w stages channels w, w+4, ..; lanes run over the halo in
+  // NJ passes whose pixel offsets are chunk independent
+  int xpix[NJ];
   unsigned xok = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int e = lane + 64 * j;
-    const int hy = fdiv(e, a.hwd_div), hx = e - hy * HWd;
+    const int hy = e / HWd, hx = e - hy * HWd;
     const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
-    const bool ok = j < nj && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+    const bool ok = e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
     xpix[j] = ok ? yy * W + xx : 0;
     xok |= ok ? (1u << j) : 0u;
   }
-  // W staging: NRUN contiguous runs of RUN floats, element e = tid + 256 i
-  const int RUN = MODE == 0 ? CK * T : BM * T;
-  const int wtotal = (MODE == 0 ? BM : CK) * RUN;
-  const int wper = (wtotal + 255) / 256;      // <= 16 (checked on the host)
-  const FastDiv run_div = a.ckt_div;          // divisor RUN
   const unsigned wlast = (unsigned)Cout * CinT - 1;
 
-  float xr[16], wv[16];
+  float xr[XPER * NJ], wv[S::WPER];
   unsigned xmask = 0;
   auto load = [&](int chunk) {
     const int c0 = chunk * CK;
     xmask = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i < xper) {
-        const int cl = wave + 4 * i;
-        const int ch = __builtin_amdgcn_readfirstlane(c0 + cl);
-        const bool chok = cl < CK && ch < kch;
-        const float* p;
-        unsigned sbase;
-        bool M;
-        if (MODE == 0) {
-          const RowDesc d = row_desc(cb1, cb2, cb3, chok ? ch : 0, HWu);
-          p = d.p;
-          sbase = (unsigned)b * d.A + d.Bc;
-          M = d.M;
-        } else {
-          p = Gp;
-          sbase = ((unsigned)b * (unsigned)Cout + (unsigned)(chok ? ch : 0)) * HWu;
-          M = true;
-        }
+    for (int i = 0; i < XPER; ++i) {
+      const int ch = c0 + wave + 4 * i;          // scalar
+      const bool chok = ch < kch;
+      const float* p;
+      unsigned sbase;
+      bool M;
+      if (MODE == 0) {
+        const RowDesc d = row_desc(cb1, cb2, cb3, chok ? ch : 0, HWu);
+        p = d.p;
+        sbase = (unsigned)b * d.A + d.Bc;
+        M = d.M;
+      } else {
+        p = Gp;
+        sbase = ((unsigned)b * (unsigned)Cout + (unsigned)(chok ? ch : 0)) * HWu;
+        M = true;
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (j < nj) {
-            const bool ok = chok && ((xok >> j) & 1u);
-            xmask |= ok ? (1u << (i * 4 + j)) : 0u;
-            xr[i * 4 + j] = p[ok ? sbase + (M ? (unsigned)xpix[j] : 0u) : 0u];
-          }
-        }
+      for (int j = 0; j < NJ; ++j) {
+        const bool ok = chok && ((xok >> j) & 1u);
+        xmask |= ok ? (1u << (i * NJ + j)) : 0u;
+        xr[i * NJ + j] = p[ok ? sbase + (M ? (unsigned)xpix[j] : 0u) : 0u];
       }
     }
-    const unsigned gdelta = MODE == 0 ? (unsigned)c0 * T : (unsigned)c0 * CinT;
-    const unsigned gfix = MODE == 0 ? (unsigned)row0 * CinT : (unsigned)row0 * T;
+    const unsigned gbase = MODE == 0 ? (unsigned)row0 * CinT + (unsigned)c0 * T
+                                     : (unsigned)c0 * CinT + (unsigned)row0 * T;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i < wper) {
-        const int e = tid + 256 * i;
-        const int run = fdiv(e, run_div), rem = e - run * RUN;
-        const unsigned g = gfix + gdelta + (unsigned)run * CinT + (unsigned)rem;
-        wv[i] = Wt[g < wlast ? g : wlast];
-      }
+    for (int i = 0; i < S::WPER; ++i) {
+      const int e = tid + 256 * i;
+      const int run = e / RUN, rem = e - run * RUN;
+      const unsigned g = gbase + (unsigned)run * CinT + (unsigned)rem;
+      wv[i] = Wt[g < wlast ? g : wlast];
     }
   };
   auto store = [&](int buf) {
     float* Ws = smem + buf * STAGE;
     float* Xs = Ws + WSZ;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XPER; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int cl = wave + 4 * i, e = lane + 64 * j;
-        if (i < xper && j < nj && cl < CK && e < HPAD)
-          Xs[cl * HPAD + e] = (xmask >> (i * 4 + j)) & 1u ? xr[i * 4 + j] : 0.f;
+        if (e < HPAD) Xs[cl * HPAD + e] = (xmask >> (i * NJ + j)) & 1u ? xr[i * NJ + j] : 0.f;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i < wper) {
-        const int e = tid + 256 * i;
-        if (e < wtotal) {
-          const int run = fdiv(e, run_div), rem = e - run * RUN;
-          Ws[run * WS + rem] = wv[i];
-        }
+    for (int i = 0; i < S::WPER; ++i) {
+      const int e = tid + 256 * i;
+      if (S::WTOT % 256 == 0 || e < S::WTOT) {
+        const int run = e / RUN, rem = e - run * RUN;
+        Ws[run * WS + rem] = wv[i];
       }
     }
   };
@@ -487,8 +495,9 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   const int arow = wr * 32 + (lane & 31);       // this lane's A row in the tile
   constexpr int NS = (WM == 2) ? CK / 2 : CK / 4;   // channel pairs per wave per tap
   const int s_lo = (WM == 2) ? 0 : wk * NS;
-  const int astep = MODE == 0 ? 2 * T : 2 * WS;  // A offset per channel pair
-  const int abase = MODE == 0 ? arow * WS + hi * T : hi * WS + arow * T;
+  constexpr int ASTEP = MODE == 0 ? 2 * T : 2 * WS;  // A offset per channel pair
+  const int abase = (MODE == 0 ? arow * WS + hi * T : hi * WS + arow * T) + s_lo * ASTEP;
+  const int bbase = hi * HPAD + qoff + 2 * s_lo * HPAD;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -502,22 +511,19 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
     const int buf = (c - cbeg) & 1;
     const bool more = c + 1 < cend;
     if (more) load(c + 1);
-    const float* Ws = smem + buf * STAGE;
-    const float* Xs = Ws + WSZ;
+    const float* wa = smem + buf * STAGE + abase;
+    const float* xb = smem + buf * STAGE + WSZ + bbase;
+#pragma unroll
     for (int ty = 0; ty < KH; ++ty) {
+#pragma unroll
       for (int tx = 0; tx < KW; ++tx) {
+        constexpr int dummy = 0;
+        (void)dummy;
         const int tap = ty * KW + tx;
         const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
-        const float* wa = Ws + abase + tap;
-        const float* xb = Xs + hi * HPAD + qoff + toff;
-        float av[NS], bv[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          av[s] = wa[(s_lo + s) * astep];
-          bv[s] = xb[2 * (s_lo + s) * HPAD];
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s) acc = mfma32(av[s], bv[s], acc);
+        for (int s = 0; s < NS; ++s)
+          acc = mfma32(wa[tap + s * ASTEP], xb[toff + 2 * s * HPAD], acc);
       }
     }
     if (more) store(buf ^ 1);
@@ -536,7 +542,7 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   }
 
   const int oy = ty0 + qy, ox = tx0 + qx;
-  if (qy >= a.TH || oy >= H || ox >= W) return;
+  if (oy >= H || ox >= W) return;
   const size_t epix = (size_t)oy * W + ox;
   if (a.part) {   // split-K partial: [split][rows][P]
     const long long P = (long long)a.g.B * HW;
@@ -731,77 +737,49 @@ struct IgPlan {
   size_t part_bytes;
 };
 
-constexpr size_t kHaloLds = 64 * 1024;   // per block: two blocks per CU
-
-int odd_up(int n) { return n | 1; }
-
-// weight tile floats, the larger of the two layouts (forward: BM rows of
-// CK*T; data gradient: CK channels of BM*T), rows padded to an odd stride
-size_t halo_wtile(int bm, int ck, int T) {
-  const size_t f = (size_t)bm * odd_up(ck * T), d = (size_t)ck * odd_up(bm * T);
-  return f > d ? f : d;
-}
 
 IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W);
 
+template <int BM, int KH, int KW>
+void halo_fill(IgPlan& pl) {
+  using S = HaloShape<BM, KH, KW>;
+  pl.TH = S::TH;
+  pl.TW = S::TW;
+  pl.HWd = S::HWd;
+  pl.HPAD = S::HPAD;
+  pl.CK = S::CK;
+  pl.lds_bytes = S::LDS * sizeof(float);
+}
+
 IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
+  const bool shape_ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
+  if (!shape_ok) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
   IgPlan pl = {};
-  const int T = KH * KW;
   const long long P = (long long)B * H * W;
-  pl.halo = T > 1 && T <= 9;
-  long long blocks;
-  int nchunks;
-  if (!pl.halo) {
-    pl.ptiles = (int)((P + kBN - 1) / kBN);
-    const int t64 = (rows + 63) / 64;
-    pl.bm = (long long)t64 * pl.ptiles >= 448 ? 64 : 32;
-    pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
-    nchunks = (kch * T + kBK - 1) / kBK;
+  pl.halo = true;
+  const int TH = (KW == 1 || (KH == 3 && KW == 3)) ? 8 : 4, TW = 64 / TH;
+  pl.tiles_x = (W + TW - 1) / TW;
+  pl.tiles_img = ((H + TH - 1) / TH) * pl.tiles_x;
+  pl.ptiles = B * pl.tiles_img;
+  const int t64 = (rows + 63) / 64;
+  pl.bm = (long long)t64 * pl.ptiles >= 480 ? 64 : 32;
+  pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
+  if (pl.bm == 32) {
+    if (KH == 1) halo_fill<32, 1, 5>(pl);
+    else if (KW == 1) halo_fill<32, 5, 1>(pl);
+    else halo_fill<32, 3, 3>(pl);
   } else {
-    // tile shape: fewest staged elements (halo + MFMA columns) over the image
-    static const int cand[4][2] = {{1, 64}, {2, 32}, {4, 16}, {8, 8}};
-    long long best = -1;
-    for (const auto& c : cand) {
-      const int th = c[0], tw = c[1];
-      const long long tiles = (long long)((H + th - 1) / th) * ((W + tw - 1) / tw);
-      const int halo = (th + KH - 1) * (tw + KW - 1);
-      const long long cost = tiles * (halo + 64);
-      if (halo <= 256 && (best < 0 || cost < best)) {
-        best = cost;
-        pl.TH = th;
-        pl.TW = tw;
-      }
-    }
-    pl.tiles_x = (W + pl.TW - 1) / pl.TW;
-    pl.tiles_img = ((H + pl.TH - 1) / pl.TH) * pl.tiles_x;
-    pl.ptiles = B * pl.tiles_img;
-    pl.HWd = pl.TW + KW - 1;
-    const int halo = (pl.TH + KH - 1) * pl.HWd;
-    pl.HPAD = halo + ((32 - halo % 64) + 64) % 64;   // channel stride = 32 mod 64 banks
-    const int t64 = (rows + 63) / 64;
-    pl.bm = (long long)t64 * pl.ptiles >= 480 ? 64 : 32;
-    pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
-    // channels per chunk (a template parameter of the kernel): BM=32 -> 16,
-    // BM=64 -> 8, halved for T > 5, so a thread stages <= 16 weights and
-    // <= 4 channels per wave; small-Cin convs keep the smaller chunk
-    pl.CK = (pl.bm == 32 ? 16 : 8) / (T > 5 ? 2 : 1);
-    if (pl.bm == 32 && pl.CK == 16 && kch <= 8) pl.CK = 8;
-    if (pl.bm == 64 && pl.CK == 8 && kch <= 4) pl.CK = 4;
-    const size_t stage = halo_wtile(pl.bm, pl.CK, T) + (size_t)pl.CK * pl.HPAD;
-    if (2 * stage * sizeof(float) > kHaloLds || ((size_t)pl.bm * pl.CK * T + 255) / 256 > 16)
-      return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
-    pl.lds_bytes = 2 * (halo_wtile(pl.bm, pl.CK, T) + (size_t)pl.CK * pl.HPAD) * sizeof(float);
-    if (pl.lds_bytes < 2 * 16 * 64 * sizeof(float)) pl.lds_bytes = 2 * 16 * 64 * sizeof(float);  // K-half reduction
-    nchunks = (kch + pl.CK - 1) / pl.CK;
+    if (KH == 1) halo_fill<64, 1, 5>(pl);
+    else if (KW == 1) halo_fill<64, 5, 1>(pl);
+    else halo_fill<64, 3, 3>(pl);
   }
-  blocks = (long long)pl.row_tiles * pl.ptiles;
+  const int nchunks = (kch + pl.CK - 1) / pl.CK;
+  const long long blocks = (long long)pl.row_tiles * pl.ptiles;
   int ks = 1;
-  if (blocks < 240 || (pl.halo && blocks < 480)) {   // split K over blocks
+  if (blocks < 480) {   // split K over blocks (one chunk minimum per split)
     ks = (int)((480 + blocks - 1) / blocks);
     if (ks > 16) ks = 16;
-    const int minc = pl.halo ? 1 : 4;
-    if (ks > nchunks / minc) ks = nchunks / minc;
-    if (ks < 1) ks = 1;
+    if (ks > nchunks) ks = nchunks;
   }
   pl.chunks_per_split = (nchunks + ks - 1) / ks;
   pl.ksplit = (nchunks + pl.chunks_per_split - 1) / pl.chunks_per_split;
@@ -953,7 +931,6 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
   const dim3 grid(pl.row_tiles * pl.ptiles, pl.ksplit);
   if (pl.halo) {
-    const int T = a.g.KH * a.g.KW;
     a.TH = pl.TH;
     a.TW = pl.TW;
     a.HWd = pl.HWd;
@@ -961,24 +938,20 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.tiles_x = pl.tiles_x;
     a.tiles_img = pl.tiles_img;
     a.CK = pl.CK;
-    const int run = MODE == 0 ? pl.CK * T : pl.bm * T;   // contiguous weight run
-    a.wstride = odd_up(run);
-    a.ckt_div = make_fdiv(run);
-    a.t_div = make_fdiv(T);
-    a.hwd_div = make_fdiv(pl.HWd);      // halo element -> (hy, hx)
-    const size_t lds = pl.lds_bytes;
-    if (pl.bm == 64 && pl.CK == 8)
-      hipLaunchKernelGGL((dconv_kernel<64, 8, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
-    else if (pl.bm == 64 && pl.CK == 4)
-      hipLaunchKernelGGL((dconv_kernel<64, 4, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
-    else if (pl.bm == 32 && pl.CK == 16)
-      hipLaunchKernelGGL((dconv_kernel<32, 16, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
-    else if (pl.bm == 32 && pl.CK == 8)
-      hipLaunchKernelGGL((dconv_kernel<32, 8, MODE, ACT, EPI>), grid, dim3(256), lds, s, a);
-    else {
-      set_error("conv: no kernel for this halo plan");
-      return DRO_E_SHAPE;
+    const int KH = a.g.KH;
+    const int KW = a.g.KW;
+#define DRO_DCONV(BM_, KH_, KW_) \
+    hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI>), grid, dim3(256), 0, s, a)
+    if (pl.bm == 32) {
+      if (KH == 1) DRO_DCONV(32, 1, 5);
+      else if (KW == 1) DRO_DCONV(32, 5, 1);
+      else DRO_DCONV(32, 3, 3);
+    } else {
+      if (KH == 1) DRO_DCONV(64, 1, 5);
+      else if (KW == 1) DRO_DCONV(64, 5, 1);
+      else DRO_DCONV(64, 3, 3);
     }
+#undef DRO_DCONV
   } else {
     a.kdiv = make_fdiv(a.kch);
     if (pl.bm == 64)

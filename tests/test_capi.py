@@ -109,8 +109,8 @@ def test_conv_plans_within_kernel_limits(lib):
                 assert lib.dro_conv2d_plan(rows, kch, KH, KW, B, H, W, info) == 0
                 halo, bm, rt, pt, ks, cps, TH, TW, HWd, HPAD, tx, timg, CK, lds, part, _ = list(info)
                 assert bm in (32, 64) and rt * bm >= rows and ks >= 1 and cps >= 1
+                assert bool(halo) == ((KH, KW) in ((1, 5), (5, 1), (3, 3)))
                 if not halo:
-                    assert KH * KW == 1 or KH * KW > 9 or CK == 0
                     continue
                 T = KH * KW
                 assert TH * TW == 64 and HWd == TW + KW - 1
