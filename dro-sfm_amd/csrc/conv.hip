@@ -35,6 +35,7 @@
 // Roofline: MFMA(f32) at 157 TF/s; FLOPs per launch = 2 * Cout * P * Cin * KH * KW.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -675,6 +676,182 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ halo-tiled weight gradient
+// dW[o, c, tap] = sum_p G[o, p] X[c, p + d(tap)] for (KH, KW) in {1x5, 5x1, 3x3}:
+// block = 64 output channels x 32 input channels x all taps, K = the pixels of
+// a run of TH x TW pixel tiles.  Per tile the G tile [64 px][64 o] and the X
+// patch [32 c][halo] are staged once; tap (ty, tx) reads the patch shifted.
+// Virtual channel Cin is all ones inside the image, so its centre-tap result
+// is db[o] = sum_p G[o, p].  Waves: 2 (o halves) x 2 (pixel halves, summed
+// through LDS at the end, one tap at a time).  Partials [split][Cout][(Cin+1)*T].
+template <int KH, int KW>
+struct HaloShapeW {
+  static constexpr int T = KH * KW;
+  static constexpr int TH = HaloShape<32, KH, KW>::TH, TW = 64 / TH;
+  static constexpr int HWd = TW + KW - 1;
+  static constexpr int HALO = (TH + KH - 1) * HWd;
+  static constexpr int HPAD = HALO | 1;          // odd: lanes read 32 channels at stride HPAD
+  static constexpr int NJ = (HALO + 63) / 64;
+  static constexpr int BC = 32;                  // input channels per block
+  static constexpr int GPAD = 65;                // [px][o] row stride
+  static constexpr int STAGE = 64 * GPAD + BC * HPAD;
+  static constexpr int LDS = 2 * STAGE > 2 * 16 * 64 * 2 ? 2 * STAGE : 2 * 16 * 64 * 2;
+  static_assert(NJ <= 2 && TW % 2 == 0, "halo shape");
+};
+
+template <int KH, int KW>
+__global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
+  using S = HaloShapeW<KH, KW>;
+  constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
+  constexpr int NJ = S::NJ, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE;
+  constexpr int PH = KH / 2, PW = KW / 2;
+  __shared__ float smem[S::LDS];
+  const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
+  const int H = a.g.H, W = a.g.W, Cin = a.g.Cin, Cout = a.g.Cout;
+  const float* __restrict__ Gp = a.G;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = blockIdx.x;
+  const int ot = t % a.otiles, ct = t / a.otiles;
+  const int o0 = ot * 64, c0 = ct * BC;
+  const size_t HW = (size_t)H * W;
+  const unsigned HWu = (unsigned)HW;
+  const int ntiles = a.g.B * a.tiles_img;
+  const int tbeg = blockIdx.y * a.chunks_per_split;
+  const int tend = min(ntiles, tbeg + a.chunks_per_split);
+
+  float gr[16], xr[8 * NJ];
+  unsigned gmask = 0, xmask = 0;
+  auto load = [&](int tile) {
+    const int b = tile / a.tiles_img, trem = tile - b * a.tiles_img;
+    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+    // G tile: lane = pixel of the tile, wave w -> output channels o0 + 16w + j
+    const int qy = lane / TW, qx = lane - qy * TW;
+    const int oy = ty0 + qy, ox = tx0 + qx;
+    const bool pin = oy < H && ox < W;
+    const unsigned pix = pin ? (unsigned)(oy * W + ox) : 0u;
+    gmask = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int o = o0 + wave * 16 + j;        // scalar
+      const bool ok = pin && o < Cout;
+      gmask |= ok ? (1u << j) : 0u;
+      gr[j] = Gp[ok ? ((unsigned)b * Cout + o) * HWu + pix : 0u];
+    }
+    // X patch: wave w -> channels c0 + w + 4i, lanes over the halo
+    xmask = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = c0 + wave + 4 * i;          // scalar
+      const bool real = ch < Cin, ones = ch == Cin;
+      const RowDesc d = row_desc(cb1, cb2, cb3, real ? ch : 0, HWu);
+      const unsigned sbase = (unsigned)b * d.A + d.Bc;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        const int hy = e / HWd, hx = e - hy * HWd;
+        const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
+        const bool in = e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const bool ok = real && in;
+        xmask |= ok ? (1u << (i * NJ + j)) : 0u;
+        const float v = d.p[ok ? sbase + (d.M ? (unsigned)(yy * W + xx) : 0u) : 0u];
+        xr[i * NJ + j] = ones ? (in ? 1.f : 0.f) : v;
+        if (ones && in) xmask |= 1u << (i * NJ + j);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    float* Gs = smem + buf * STAGE;
+    float* Xs = Gs + 64 * GPAD;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) Gs[lane * GPAD + wave * 16 + j] = (gmask >> j) & 1u ? gr[j] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        if (e < HPAD) Xs[(wave + 4 * i) * HPAD + e] = (xmask >> (i * NJ + j)) & 1u ? xr[i * NJ + j] : 0.f;
+      }
+    }
+  };
+
+  const int wo = wave & 1, wp = wave >> 1;
+  const int hi = lane >> 5;
+  f32x16 acc[T];
+#pragma unroll
+  for (int tp = 0; tp < T; ++tp)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[tp][r] = 0.f;
+
+  if (tbeg < tend) {
+    load(tbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int tl = tbeg; tl < tend; ++tl) {
+    const int buf = (tl - tbeg) & 1;
+    const bool more = tl + 1 < tend;
+    if (more) load(tl + 1);
+    const float* Gs = smem + buf * STAGE;
+    const float* Xs = Gs + 64 * GPAD;
+    const float* ga = Gs + hi * GPAD + wo * 32 + (lane & 31);
+    const float* xb = Xs + (lane & 31) * HPAD + hi;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int pp = 2 * (wp * 16 + s);           // even pixel of this k-step
+      const float av = ga[pp * GPAD];
+      const int poff = (pp / TW) * HWd + (pp % TW);
+#pragma unroll
+      for (int ty = 0; ty < KH; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx)
+          acc[ty * KW + tx] = mfma32(av, xb[poff + ty * HWd + tx], acc[ty * KW + tx]);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  // sum the pixel halves one tap at a time, then write the partials
+  float* red = smem;   // [2 o halves][16][64]
+  float* wpart = a.part + (size_t)blockIdx.y * Cout * (Cin + 1) * T;
+  const int c = c0 + (lane & 31);
+#pragma unroll
+  for (int tp = 0; tp < T; ++tp) {
+    if (wp == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wo * 16 + r) * 64 + lane] = acc[tp][r];
+    }
+    __syncthreads();
+    if (wp == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (o < Cout && c <= Cin)
+          wpart[((size_t)o * (Cin + 1) + c) * T + tp] = acc[tp][r] + red[(wo * 16 + r) * 64 + lane];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dW[o][c][tap] = sum_s part[s][o][c][tap]; db[o] = sum_s part[s][o][Cin][centre]
+__global__ __launch_bounds__(256) void wgrad_halo_finish_kernel(IgArgs a, int splits) {
+  const int Cin = a.g.Cin, Cout = a.g.Cout, T = a.g.KH * a.g.KW;
+  const int centre = (a.g.KH / 2) * a.g.KW + a.g.KW / 2;
+  const long long per_o = (long long)(Cin + 1) * T;
+  const long long total = (long long)Cout * per_o;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int o = (int)(e / per_o);
+    const int rem = (int)(e - (long long)o * per_o);
+    const int c = rem / T, tap = rem - c * T;
+    if (c == Cin && (tap != centre || !a.gbias)) continue;
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * total + e];
+    if (c == Cin) a.gbias[o] = v;
+    else a.gweight[((size_t)o * Cin + c) * T + tap] = v;
+  }
+}
+
 // dW[o][c][tap] = sum_s part[s][o][tap*Cin + c]; db[o] = sum_s part[s][o][NK].
 // Threads walk the partials in their (coalesced) [o][n] order.
 __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits) {
@@ -835,6 +1012,34 @@ WgPlan plan_wgrad(int Cin, int Cout, int T, long long P) {
   return pl;
 }
 
+// halo weight gradient: (KH, KW) in {1x5, 5x1, 3x3}
+struct WhPlan {
+  bool ok;
+  int otiles, ctiles, tiles_x, tiles_img, splits, tiles_per_split;
+  size_t part_bytes;
+};
+
+WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
+  WhPlan pl = {};
+  pl.ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
+  if (!pl.ok) return pl;
+  const int TH = (KW == 1 || (KH == 3 && KW == 3)) ? 8 : 4, TW = 64 / TH;
+  pl.tiles_x = (W + TW - 1) / TW;
+  pl.tiles_img = ((H + TH - 1) / TH) * pl.tiles_x;
+  const int ntiles = B * pl.tiles_img;
+  pl.otiles = (Cout + 63) / 64;
+  pl.ctiles = (Cin + 1 + 31) / 32;
+  const int blocks = pl.otiles * pl.ctiles;
+  int sp = (384 + blocks - 1) / blocks;
+  if (sp > 32) sp = 32;
+  if (sp > ntiles) sp = ntiles;
+  if (sp < 1) sp = 1;
+  pl.tiles_per_split = (ntiles + sp - 1) / sp;
+  pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
+  pl.part_bytes = align256((size_t)pl.splits * Cout * (Cin + 1) * KH * KW * sizeof(float));
+  return pl;
+}
+
 size_t fwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   return plan_igemm(Cout, Cin, KH, KW, B, H, W).part_bytes;
 }
@@ -844,7 +1049,8 @@ size_t bwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   const int T = KH * KW;
   return align256((size_t)Cout * P * sizeof(float)) +              // pre-activation gradient
          plan_igemm(Cin, Cout, KH, KW, B, H, W).part_bytes +        // data-gradient split-K
-         plan_wgrad(Cin, Cout, T, P).part_bytes;                    // weight-gradient partials
+         std::max(plan_wgrad(Cin, Cout, T, P).part_bytes,           // weight-gradient partials
+                  plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).part_bytes);
 }
 
 bool too_big(long long B, long long C, long long HW) { return B * C * HW >= (1LL << 30); }
@@ -1171,7 +1377,24 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.kch = Cout;
     if ((st = launch_igemm<1, 0, 0>(a, P, ws_ig, s))) return st;
   }
-  if (grad_weight) {
+  const WhPlan wh = plan_wgrad_halo(a.g.Cin, Cout, KH, KW, B, H, W);
+  if (grad_weight && wh.ok) {
+    a.otiles = wh.otiles;
+    a.tiles_x = wh.tiles_x;
+    a.tiles_img = wh.tiles_img;
+    a.chunks_per_split = wh.tiles_per_split;
+    a.part = reinterpret_cast<float*>(ws_wg);
+    const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
+    if (KH == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, s, a);
+    else if (KW == 1) hipLaunchKernelGGL((wgrad_halo_kernel<5, 1>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<3, 3>), grid, dim3(256), 0, s, a);
+    if ((st = launch_status("wgrad_halo_kernel launch failed"))) return st;
+    const long long total = (long long)Cout * (a.g.Cin + 1) * T;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
+    if ((st = launch_status("wgrad_halo_finish_kernel launch failed"))) return st;
+  } else if (grad_weight) {
     const WgPlan pl = plan_wgrad(a.g.Cin, Cout, T, P);
     a.K = a.g.Cin * T;
     a.otiles = pl.otiles;
