@@ -87,6 +87,7 @@ struct IgArgs {
   int gsrc_ctot[kMaxSrc], gsrc_coff[kMaxSrc], gsrc_acc[kMaxSrc];
   float* gweight;         // [Cout][Cin][KH][KW]
   float* gbias;           // [Cout]
+  int wacc;               // 1: add into gweight / gbias instead of overwriting
   int rows;               // GEMM rows: Cout (forward) / Cin (data gradient)
   int kch;                // channels reduced per tap: Cin (forward) / Cout (data gradient)
   int K;                  // kch * KH * KW
@@ -847,8 +848,8 @@ __global__ __launch_bounds__(256) void wgrad_halo_finish_kernel(IgArgs a, int sp
     if (c == Cin && (tap != centre || !a.gbias)) continue;
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * total + e];
-    if (c == Cin) a.gbias[o] = v;
-    else a.gweight[((size_t)o * Cin + c) * T + tap] = v;
+    float* d = c == Cin ? a.gbias + o : a.gweight + ((size_t)o * Cin + c) * T + tap;
+    *d = a.wacc ? *d + v : v;
   }
 }
 
@@ -866,10 +867,11 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits)
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * sstride + src];
     if (n == NK) {
-      a.gbias[o] = v;
+      a.gbias[o] = a.wacc ? a.gbias[o] + v : v;
     } else {
       const int tap = n / Cin, c = n - tap * Cin;
-      a.gweight[((size_t)o * Cin + c) * T + tap] = v;
+      float* d = a.gweight + ((size_t)o * Cin + c) * T + tap;
+      *d = a.wacc ? *d + v : v;
     }
   }
 }
@@ -1317,7 +1319,8 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
                                    const dro_slice* y, const float* dout, float* const* grad_srcs,
                                    const int* grad_ctot, const int* grad_coff,
                                    const int* grad_accumulate, float* grad_weight, float* grad_bias,
-                                   void* workspace, size_t workspace_bytes, void* stream) {
+                                   int grad_weight_accumulate, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
   IgArgs a = {};
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
@@ -1350,6 +1353,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   a.weight = weight;
   a.gweight = grad_weight;
   a.gbias = grad_bias;
+  a.wacc = grad_weight_accumulate ? 1 : 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t HW = (size_t)H * W;
   const long long P = (long long)B * HW;

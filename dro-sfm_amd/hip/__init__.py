@@ -6,7 +6,7 @@ be captured into a hipGraph.
 """
 from .ops import (DEPTH_DISP, DEPTH_INV, DEPTH_METRIC, POSE_EULER, POSE_MATRIX,
                   convex_upsample, photometric_loss, plane_sweep_cost, warp_cost)
-from .conv import conv2d, sepconvgru_half
+from .conv import cached_cat, conv2d, sepconvgru_half, weight_grad_scope
 
-__all__ = ["conv2d", "sepconvgru_half", "warp_cost", "plane_sweep_cost", "photometric_loss", "convex_upsample",
+__all__ = ["conv2d", "sepconvgru_half", "weight_grad_scope", "cached_cat", "warp_cost", "plane_sweep_cost", "photometric_loss", "convex_upsample",
            "POSE_EULER", "POSE_MATRIX", "DEPTH_METRIC", "DEPTH_INV", "DEPTH_DISP"]

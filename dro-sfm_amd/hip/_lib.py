@@ -52,7 +52,7 @@ def load():
     _sig(lib.dro_conv2d_forward, P, I, P, P, I, I, I, I, I, I, I, F, P, I, I, P, Z, S)
     _sig(lib.dro_convgru_gates_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, Z, S)
     _sig(lib.dro_convgru_blend_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, Z, S)
-    _sig(lib.dro_conv2d_backward, P, I, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, P, Z, S)
+    _sig(lib.dro_conv2d_backward, P, I, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, I, P, Z, S)
     _sig(lib.dro_gru_backward_elem, I, I, I, I, I, P, P, P, P, P, P, P, P, S)
     _lib = lib
     return lib

@@ -5,7 +5,15 @@ for stride-1 'same' convolutions without materialising the concatenation:
 each source may be a dense NCHW tensor, a channel-slice view of one, or a
 [B,C,1,1] tensor expanded over H x W (a constant map).  `sepconvgru_half`
 is one direction of SepConvGRU (update.py:47-74) in two launches forward.
+
+`weight_grad_scope()`: inside it (one forward of the recurrent net), a weight
+used by several convs gets its gradient summed IN the backward kernels (the
+first backward call of that weight returns the buffer, later ones add into it
+and return None; autograd consumes it only after every producer has run), and
+weight concatenations are built once.  Without the scope every call returns
+its own gradient, as plain autograd would.
 """
+import contextlib
 import ctypes
 
 import torch
@@ -49,6 +57,53 @@ def _grad_targets(bufs):
     return ptrs, ctot, coff
 
 
+class WeightGradScope:
+    def __init__(self):
+        self.grads = {}     # key -> [gw, gb] accumulation buffers
+        self.cats = {}      # key -> concatenated (weight, bias)
+
+
+_SCOPE = [None]
+
+
+@contextlib.contextmanager
+def weight_grad_scope():
+    prev = _SCOPE[0]
+    _SCOPE[0] = WeightGradScope() if torch.is_grad_enabled() else None
+    try:
+        yield _SCOPE[0]
+    finally:
+        _SCOPE[0] = prev
+
+
+def current_scope():
+    return _SCOPE[0]
+
+
+def cached_cat(key, make):
+    """make() once per scope (e.g. torch.cat of conv weights); uncached outside."""
+    sc = _SCOPE[0]
+    if sc is None:
+        return make()
+    v = sc.cats.get(key)
+    if v is None:
+        v = sc.cats[key] = make()
+    return v
+
+
+def _grad_buffers(scope, key, weight, nbias, device):
+    """(gw, gb, accumulate, first) for one backward call."""
+    if scope is None:
+        return (torch.empty_like(weight), torch.empty(nbias, device=device) if nbias else None, 0, True)
+    ent = scope.grads.get(key)
+    if ent is None:
+        gw = torch.empty_like(weight)
+        gb = torch.empty(nbias, device=device) if nbias else None
+        scope.grads[key] = (gw, gb)
+        return gw, gb, 0, True
+    return ent[0], ent[1], 1, False
+
+
 _WS = {}
 
 
@@ -68,7 +123,7 @@ def _dense_out(srcs, C):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, weight, bias, act, alpha, *srcs):
+    def forward(ctx, weight, bias, act, alpha, scope, *srcs):
         lib = _lib.load()
         require_device(weight, bias, *srcs, what="conv2d")
         Cout, Cin, KH, KW = weight.shape
@@ -83,6 +138,7 @@ class _Conv2d(torch.autograd.Function):
                                      stream_of(out)), "dro_conv2d_forward")
         ctx.save_for_backward(weight, out if act else None, *srcs)
         ctx.meta = (act, alpha, bias is not None)
+        ctx.scope = scope
         return out
 
     @staticmethod
@@ -94,26 +150,32 @@ class _Conv2d(torch.autograd.Function):
         B, _, H, W = srcs[0].shape
         need = ctx.needs_input_grad
         gout = gout.contiguous()
-        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[4 + i] else None
+        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[5 + i] else None
                 for i, s in enumerate(srcs)]
-        gw = torch.empty_like(weight) if (need[0] or (has_bias and need[1])) else None
-        gb = torch.empty(Cout, device=gout.device) if (has_bias and need[1]) else None
+        want_w = need[0] or (has_bias and need[1])
+        if want_w:
+            gw, gb, wacc, first = _grad_buffers(ctx.scope, ("conv", weight.data_ptr(), Cout),
+                                                weight, Cout if has_bias else 0, gout.device)
+        else:
+            gw, gb, wacc, first = None, None, 0, False
         ptrs, ctot, coff = _grad_targets(gsrc)
         acc = (ctypes.c_int * len(srcs))()
         ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
         ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
         check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), ptr(ws), nws,
+                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), wacc, ptr(ws), nws,
                                       stream_of(gout)), "dro_conv2d_backward")
-        return (gw if need[0] else None, gb, None, None, *gsrc)
+        rw = gw if (first and need[0]) else None
+        rb = gb if (first and has_bias and need[1]) else None
+        return (rw, rb, None, None, None, *gsrc)
 
 
 def conv2d(srcs, weight, bias=None, act=None, alpha=1.0):
     """act(conv2d(cat(srcs, 1), weight, bias, padding=k//2)) * alpha on f32 MFMA."""
     if torch.is_tensor(srcs):
         srcs = [srcs]
-    return _Conv2d.apply(weight, bias, ACT[act], float(alpha), *srcs)
+    return _Conv2d.apply(weight, bias, ACT[act], float(alpha), current_scope(), *srcs)
 
 
 class _SepGRUHalf(torch.autograd.Function):
@@ -122,15 +184,20 @@ class _SepGRUHalf(torch.autograd.Function):
     Forward: 2 launches (gates + r*h; candidate + blend)."""
 
     @staticmethod
-    def forward(ctx, h, wz, bz, wr, br, wq, bq, *xs):
+    def forward(ctx, h, wz, bz, wr, br, wq, bq, scope, *xs):
         lib = _lib.load()
         require_device(h, wz, wq, *xs, what="sepconvgru")
         h = h.contiguous()
         B, hd, H, W = h.shape
         KH, KW = wz.shape[2:]
         cin = wz.shape[1]
-        wzr = torch.cat([wz, wr], 0).contiguous()
-        bzr = torch.cat([bz, br], 0).contiguous()
+        key = ("zr", wz.data_ptr(), wr.data_ptr())
+        wzr, bzr = scope.cats.get(key, (None, None)) if scope is not None else (None, None)
+        if wzr is None:
+            wzr = torch.cat([wz, wr], 0).contiguous()
+            bzr = torch.cat([bz, br], 0).contiguous()
+            if scope is not None:
+                scope.cats[key] = (wzr, bzr)
         st = stream_of(h)
         zr = torch.empty(B, 2 * hd, H, W, device=h.device)
         rh = torch.empty_like(h)
@@ -148,6 +215,8 @@ class _SepGRUHalf(torch.autograd.Function):
                                             ptr(q), ptr(hn), hd, 0, ptr(wsq), nwsq, st),
               "dro_convgru_blend_forward")
         ctx.save_for_backward(h, rh, wzr, wq, zr, q, *xs)
+        ctx.scope = scope
+        ctx.keys = (key, ("q", wq.data_ptr()))
         return hn
 
     @staticmethod
@@ -168,30 +237,32 @@ class _SepGRUHalf(torch.autograd.Function):
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(1)")
         # candidate conv over [r*h, x]: d(r*h), dx (overwrite), dWq, dbq
         drh = torch.empty_like(h)
-        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[7 + i] else None
+        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[8 + i] else None
                for i, x in enumerate(xs)]
-        gwq, gbq = torch.empty_like(wq), torch.empty(hd, device=h.device)
+        gwq, gbq, qacc, qfirst = _grad_buffers(ctx.scope, ctx.keys[1], wq, hd, h.device)
         ptrs, ctot, coff = _grad_targets([drh, *dxs])
         acc = (ctypes.c_int * n)()
         ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq.contiguous()), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
-                                      ptr(gwq), ptr(gbq), ptr(ws), nws, st), "dro_conv2d_backward(q)")
+                                      ptr(gwq), ptr(gbq), qacc, ptr(ws), nws, st), "dro_conv2d_backward(q)")
         # stage 2: pre-activation grad of r, dh += d(r*h) r
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
         # gate conv over [h, x]: dh, dx accumulate; dWz|dWr, dbz|dbr
-        gwzr, gbzr = torch.empty_like(wzr), torch.empty(2 * hd, device=h.device)
+        gwzr, gbzr, zacc, zfirst = _grad_buffers(ctx.scope, ctx.keys[0], wzr, 2 * hd, h.device)
         ptrs, ctot, coff = _grad_targets([dh, *dxs])
         acc = (ctypes.c_int * n)(*([1] * n))
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
-                                      ptr(gwzr), ptr(gbzr), ptr(ws), nws, st), "dro_conv2d_backward(zr)")
-        return (dh if need[0] else None, gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:], gwq, gbq, *dxs)
+                                      ptr(gwzr), ptr(gbzr), zacc, ptr(ws), nws, st), "dro_conv2d_backward(zr)")
+        gz = (gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:]) if zfirst else (None,) * 4
+        gq = (gwq, gbq) if qfirst else (None, None)
+        return (dh if need[0] else None, *gz, *gq, None, *dxs)
 
 
 def sepconvgru_half(h, convz, convr, convq, xs):
     """h' for one SepConvGRU direction; xs: the input sources (virtual concat)."""
     return _SepGRUHalf.apply(h, convz.weight, convz.bias, convr.weight, convr.bias, convq.weight,
-                             convq.bias, *xs)
+                             convq.bias, current_scope(), *xs)

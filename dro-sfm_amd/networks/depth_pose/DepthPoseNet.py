@@ -86,6 +86,11 @@ class DepthPoseNet(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, target_image, ref_imgs, intrinsics):
+        # one gradient per shared conv weight, summed in-kernel (hip/conv.py)
+        with hip.weight_grad_scope():
+            return self._forward(target_image, ref_imgs, intrinsics)
+
+    def _forward(self, target_image, ref_imgs, intrinsics):
         B, N = target_image.shape[0], len(ref_imgs)
         C, hd, cd = self.foutput_dim, self.hdim, self.cdim
         K = intrinsics.float().contiguous()

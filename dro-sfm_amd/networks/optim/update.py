@@ -61,9 +61,11 @@ def conv(srcs, weight, bias, act=None, alpha=1.0):
 
 
 def conv_cat(x, convs, act=None):
-    """One convolution computing several nn.Conv2d that share the input x."""
-    w = torch.cat([c.weight for c in convs], 0)
-    b = torch.cat([c.bias for c in convs], 0)
+    """One convolution computing several nn.Conv2d that share the input x (the
+    concatenated weights are built once per forward, hip.weight_grad_scope)."""
+    w, b = hip.cached_cat(("cat",) + tuple(id(c) for c in convs),
+                          lambda: (torch.cat([c.weight for c in convs], 0),
+                                   torch.cat([c.bias for c in convs], 0)))
     return torch.split(conv(x, w, b, act), [c.out_channels for c in convs], 1)
 
 

@@ -204,12 +204,14 @@ int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const float* weig
  * [B, grad_ctot[i], H, W] tensor, overwritten or added (grad_accumulate[i]);
  * a broadcast source receives its per-pixel gradient (the caller sums over
  * H x W).  grad_weight / grad_bias (nullable; grad_bias needs grad_weight)
- * are overwritten. */
+ * are overwritten, or added to when grad_weight_accumulate is set (a weight
+ * shared by several convs of one forward collects one summed gradient). */
 int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H, int W,
                         int Cout, int KH, int KW, int act, float alpha, const dro_slice* y,
                         const float* dout, float* const* grad_srcs, const int* grad_ctot,
                         const int* grad_coff, const int* grad_accumulate, float* grad_weight,
-                        float* grad_bias, void* workspace, size_t workspace_bytes, void* stream);
+                        float* grad_bias, int grad_weight_accumulate, void* workspace,
+                        size_t workspace_bytes, void* stream);
 
 /* SepConvGRU backward, elementwise parts (update.py:67-70): with zr the saved
  * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W].

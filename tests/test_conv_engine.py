@@ -146,3 +146,33 @@ def test_conv2d_rejects_bad_layout(hip):
         hip.conv2d([x], w)
     with pytest.raises(RuntimeError):
         hip.conv2d([torch.randn(2, 7, 6, 6, device=DEV)], w)
+
+
+def test_weight_grad_scope_matches_autograd(hip):
+    """A weight shared by several convs / GRU steps of one forward: summing its
+    gradient in-kernel (weight_grad_scope) equals autograd's own accumulation."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    B, hd, H, W = 2, 64, 12, 20
+    convs = [torch.nn.Conv2d(hd + 32, hd, (1, 5), padding=(0, 2)).to(DEV) for _ in range(3)]
+    head = torch.nn.Conv2d(hd, hd, 3, padding=1).to(DEV)
+    h0 = torch.randn(B, hd, H, W, device=DEV, generator=g).tanh()
+    x = torch.randn(B, 32, H, W, device=DEV, generator=g)
+    params = [p for c in convs + [head] for p in c.parameters()]
+
+    def run(scoped):
+        for p in params:
+            p.grad = None
+        ctxm = hip.weight_grad_scope() if scoped else torch.enable_grad()
+        with ctxm:
+            h = h0
+            for _ in range(3):
+                h = hip.sepconvgru_half(h, *convs, [x])
+                h = hip.conv2d([h], head.weight, head.bias, act="tanh")
+            loss = (h * h).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return [p.grad.detach().clone() for p in params]
+
+    ref, got = run(False), run(True)
+    for i, (a, r) in enumerate(zip(got, ref)):
+        assert rel(a, r) < 1e-5, f"param {i}"
