@@ -127,6 +127,62 @@ def broadcast_module(module, src=0, group=None):
             dist.broadcast(t.data, src=src, group=group)
 
 
+class FlatAdam:
+    """torch.optim.Adam (amsgrad off) over ONE flat parameter buffer: a single
+    fused HIP launch per step (csrc/optim.hip) instead of per-tensor kernels.
+    The step counter lives on the device (capturable); lr/betas/eps are baked
+    into a captured graph, as with torch's capturable Adam."""
+
+    def __init__(self, params, flat_param, flat_grad, lr=2e-4, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0):
+        from ..hip import _lib
+        self._lib = _lib
+        _lib.load()
+        self.params, self.flat_param, self.flat_grad = params, flat_param, flat_grad
+        self.exp_avg = torch.zeros_like(flat_param)
+        self.exp_avg_sq = torch.zeros_like(flat_param)
+        self.step_t = torch.zeros((), device=flat_param.device, dtype=torch.float32)
+        self.state = {"flat": {"step": self.step_t, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}}
+        self.param_groups = [{"params": params, "lr": lr, "betas": betas, "eps": eps,
+                              "weight_decay": weight_decay}]
+
+    def step(self):
+        g = self.param_groups[0]
+        self.step_t += 1
+        lib = self._lib
+        lib.check(lib.load().dro_adam_step(lib.ptr(self.flat_param), lib.ptr(self.flat_grad),
+                                           lib.ptr(self.exp_avg), lib.ptr(self.exp_avg_sq),
+                                           self.flat_param.numel(), lib.ptr(self.step_t), g["lr"],
+                                           g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"],
+                                           lib.stream_of(self.flat_param)), "dro_adam_step")
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_grad.zero_()
+
+    def state_dict(self):
+        return {"state": {k: v.clone() for k, v in self.state["flat"].items()},
+                "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}]}
+
+    def load_state_dict(self, sd):
+        """In place (a captured graph holds these buffers' addresses)."""
+        with torch.no_grad():
+            for k, v in sd["state"].items():
+                self.state["flat"][k].copy_(v)
+        self.param_groups[0].update(sd["param_groups"][0])
+
+
+def flatten_parameters(params, offsets, total, device):
+    """Move the parameters into one contiguous buffer (same layout as the flat
+    gradient buffer); each parameter becomes a view of it."""
+    flat = torch.empty(total, device=device, dtype=torch.float32)
+    with torch.no_grad():
+        for p in params:
+            off = offsets[p]
+            flat[off:off + p.numel()].copy_(p.data.reshape(-1))
+            p.data = flat[off:off + p.numel()].view_as(p)
+    return flat
+
+
 class DataParallelTrainer:
     """fit()-less step driver: `loss, metrics = trainer.step(batch)`.
 
@@ -140,8 +196,17 @@ class DataParallelTrainer:
         self.model = model
         broadcast_module(model, 0, group)
         self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb, group=group)
-        self.optimizer = torch.optim.Adam(self.grads.params, lr=lr, betas=betas, eps=eps,
-                                          foreach=True, capturable=capturable)
+        dev = self.grads.flat.device
+        if dev.type == "cuda":
+            # fused Adam over flat buffers (the product path on the GPU)
+            self.flat_params = flatten_parameters(self.grads.params, self.grads.offsets,
+                                                  self.grads.flat.numel(), dev)
+            self.optimizer = FlatAdam(self.grads.params, self.flat_params, self.grads.flat, lr=lr,
+                                      betas=betas, eps=eps)
+        else:
+            # CPU (gloo tests of the data-parallel host logic): PyTorch's Adam
+            self.optimizer = torch.optim.Adam(self.grads.params, lr=lr, betas=betas, eps=eps,
+                                              foreach=True, capturable=capturable)
 
     def _step_inner(self, batch, **fwd_kw):
         self.grads.zero()

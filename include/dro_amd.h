@@ -223,6 +223,17 @@ int dro_gru_backward_elem(int stage, int B, int hd, int H, int W, const float* d
                           const float* zr, const float* q, const float* h, const float* drh,
                           float* dq, float* dzr, float* dh, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Fused Adam over flat fp32 buffers (the data-parallel trainer's parameters,
+ * gradients and moments; torch.optim.Adam semantics, amsgrad off).  `step` is
+ * the device-side step counter AFTER the increment for this update.  All four
+ * buffers 16-byte aligned.  Replaces the optimizer step of the reference's
+ * training loop (trainers/horovod_trainer.py:113-116, torch.optim.Adam).
+ * ---------------------------------------------------------------------- */
+int dro_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                  const float* step, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,7 @@ def main():
         tr.step(batch, flip=False)
         torch.cuda.synchronize()
     rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key.startswith("aten::")]
-    rows.sort(key=lambda e: -e.device_time_total)
+    rows.sort(key=lambda e: -e.count)
     print(f"{'op':28s} {'calls':>6s} {'dev us':>9s}  shapes")
     for e in rows[:70]:
         print(f"{e.key[:28]:28s} {e.count:6d} {e.device_time_total:9.0f}  {str(e.input_shapes)[:150]}")
