@@ -25,7 +25,6 @@ def test_flat_adam_matches_torch_adam():
         opt.step()
         torch.cuda.synchronize()
         want = torch.cat([p.detach().reshape(-1) for p in ref])
-        upd_ref = want - torch.cat([p.reshape(-1) for p in [t.detach() for t in ref]])  # noqa: F841
         err = (flat_p - want).abs().max().item()
         assert err <= 1e-6 * want.abs().max().item() + 1e-7, (step, err)
     assert float(opt.step_t) == 5.0
