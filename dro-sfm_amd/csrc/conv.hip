@@ -95,6 +95,7 @@ struct IgArgs {
   int row_tiles;          // tile = pixel_tile * row_tiles + row_tile
   int chunks_per_split;   // split-K (gridDim.y > 1): partials to `part`
   float* part;            // [ksplit][rows][P] (igemm) / [splits][Cout][NK+1] (wgrad)
+  float* bpart;           // [splits][Cout] bias partials (halo weight gradient)
   int otiles;             // weight gradient: output-channel tiles
   long long pchunk;       // weight gradient: pixels per split
   // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
@@ -682,12 +683,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
 // block = 64 output channels x 32 input channels x all taps, K = the pixels of
 // a run of TH x TW pixel tiles.  Per tile the G tile [64 px][64 o] and the X
 // patch [32 c][halo] are staged once; tap (ty, tx) reads the patch shifted.
-// Virtual channel Cin is all ones inside the image, so its centre-tap result
-// is db[o] = sum_p G[o, p].  Waves: 2 (o halves) x 2 (pixel halves, summed
-// through LDS at the end, one tap at a time).  Partials [split][Cout][(Cin+1)*T].
+// Waves: 2 (o halves) x 2, the second pair splitting either the taps (3x3:
+// 5 + 4 per wave, no reduction) or the pixels (T = 5: summed through LDS at
+// the end, one tap at a time).  Blocks of channel tile 0 also sum G over their
+// pixels for the bias.  Partials: weights [split][Cout][Cin][T], bias [split][Cout].
 template <int KH, int KW>
 struct HaloShapeW {
   static constexpr int T = KH * KW;
+  static constexpr bool TAPSPLIT = T == 9;
+  static constexpr int TPW = TAPSPLIT ? 5 : T;   // accumulators (taps) per wave
   static constexpr int TH = HaloShape<32, KH, KW>::TH, TW = 64 / TH;
   static constexpr int HWd = TW + KW - 1;
   static constexpr int HALO = (TH + KH - 1) * HWd;
@@ -704,7 +708,8 @@ template <int KH, int KW>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
   using S = HaloShapeW<KH, KW>;
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
-  constexpr int NJ = S::NJ, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE;
+  constexpr int NJ = S::NJ, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE, TPW = S::TPW;
+  constexpr bool TAPSPLIT = S::TAPSPLIT;
   constexpr int PH = KH / 2, PW = KW / 2;
   __shared__ float smem[S::LDS];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
@@ -720,9 +725,12 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
   const int ntiles = a.g.B * a.tiles_img;
   const int tbeg = blockIdx.y * a.chunks_per_split;
   const int tend = min(ntiles, tbeg + a.chunks_per_split);
+  const bool do_bias = a.gbias && ct == 0;
 
-  float gr[16], xr[8 * NJ];
+  float gr[16], xr[8 * NJ], bsum[16];
   unsigned gmask = 0, xmask = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) bsum[j] = 0.f;
   auto load = [&](int tile) {
     const int b = tile / a.tiles_img, trem = tile - b * a.tiles_img;
     const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
@@ -744,7 +752,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int ch = c0 + wave + 4 * i;          // scalar
-      const bool real = ch < Cin, ones = ch == Cin;
+      const bool real = ch < Cin;
       const RowDesc d = row_desc(cb1, cb2, cb3, real ? ch : 0, HWu);
       const unsigned sbase = (unsigned)b * d.A + d.Bc;
 #pragma unroll
@@ -752,12 +760,9 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
         const int e = lane + 64 * j;
         const int hy = e / HWd, hx = e - hy * HWd;
         const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
-        const bool in = e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        const bool ok = real && in;
+        const bool ok = real && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
         xmask |= ok ? (1u << (i * NJ + j)) : 0u;
-        const float v = d.p[ok ? sbase + (d.M ? (unsigned)(yy * W + xx) : 0u) : 0u];
-        xr[i * NJ + j] = ones ? (in ? 1.f : 0.f) : v;
-        if (ones && in) xmask |= 1u << (i * NJ + j);
+        xr[i * NJ + j] = d.p[ok ? sbase + (d.M ? (unsigned)(yy * W + xx) : 0u) : 0u];
       }
     }
   };
@@ -765,7 +770,11 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
     float* Gs = smem + buf * STAGE;
     float* Xs = Gs + 64 * GPAD;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) Gs[lane * GPAD + wave * 16 + j] = (gmask >> j) & 1u ? gr[j] : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const float g = (gmask >> j) & 1u ? gr[j] : 0.f;
+      Gs[lane * GPAD + wave * 16 + j] = g;
+      if (do_bias) bsum[j] += g;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -776,11 +785,13 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
     }
   };
 
-  const int wo = wave & 1, wp = wave >> 1;
+  const int wo = wave & 1, w2 = wave >> 1;       // o half; tap group (3x3) or pixel half
   const int hi = lane >> 5;
-  f32x16 acc[T];
+  const int tap0 = TAPSPLIT ? w2 * 5 : 0;         // first tap of this wave
+  const int ntap = TAPSPLIT ? (w2 == 0 ? 5 : 4) : T;
+  f32x16 acc[TPW];
 #pragma unroll
-  for (int tp = 0; tp < T; ++tp)
+  for (int tp = 0; tp < TPW; ++tp)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[tp][r] = 0.f;
 
@@ -797,59 +808,81 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
     const float* Xs = Gs + 64 * GPAD;
     const float* ga = Gs + hi * GPAD + wo * 32 + (lane & 31);
     const float* xb = Xs + (lane & 31) * HPAD + hi;
+    constexpr int KS = TAPSPLIT ? 32 : 16;        // k-steps (pixel pairs) per wave
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int pp = 2 * (wp * 16 + s);           // even pixel of this k-step
+    for (int s = 0; s < KS; ++s) {
+      const int pp = 2 * ((TAPSPLIT ? 0 : w2 * 16) + s);   // even pixel of this k-step
       const float av = ga[pp * GPAD];
       const int poff = (pp / TW) * HWd + (pp % TW);
 #pragma unroll
-      for (int ty = 0; ty < KH; ++ty)
-#pragma unroll
-        for (int tx = 0; tx < KW; ++tx)
-          acc[ty * KW + tx] = mfma32(av, xb[poff + ty * HWd + tx], acc[ty * KW + tx]);
+      for (int k = 0; k < TPW; ++k) {
+        if (k < ntap) {
+          const int tap = tap0 + k;
+          const int ty = tap / KW, tx = tap - ty * KW;
+          acc[k] = mfma32(av, xb[poff + ty * HWd + tx], acc[k]);
+        }
+      }
     }
     if (more) store(buf ^ 1);
     __syncthreads();
   }
-  // sum the pixel halves one tap at a time, then write the partials
-  float* red = smem;   // [2 o halves][16][64]
-  float* wpart = a.part + (size_t)blockIdx.y * Cout * (Cin + 1) * T;
+  float* wpart = a.part + (size_t)blockIdx.y * Cout * Cin * T;
   const int c = c0 + (lane & 31);
+  if (TAPSPLIT) {
 #pragma unroll
-  for (int tp = 0; tp < T; ++tp) {
-    if (wp == 1) {
+    for (int k = 0; k < TPW; ++k) {
+      if (k < ntap) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[(wo * 16 + r) * 64 + lane] = acc[tp][r];
-    }
-    __syncthreads();
-    if (wp == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (o < Cout && c <= Cin)
-          wpart[((size_t)o * (Cin + 1) + c) * T + tp] = acc[tp][r] + red[(wo * 16 + r) * 64 + lane];
+        for (int r = 0; r < 16; ++r) {
+          const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (o < Cout && c < Cin) wpart[((size_t)o * Cin + c) * T + tap0 + k] = acc[k][r];
+        }
       }
     }
-    __syncthreads();
+  } else {   // sum the pixel halves one tap at a time
+    float* red = smem;   // [2 o halves][16][64]
+#pragma unroll
+    for (int tp = 0; tp < T; ++tp) {
+      if (w2 == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(wo * 16 + r) * 64 + lane] = acc[tp][r];
+      }
+      __syncthreads();
+      if (w2 == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (o < Cout && c < Cin)
+            wpart[((size_t)o * Cin + c) * T + tp] = acc[tp][r] + red[(wo * 16 + r) * 64 + lane];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float v = wave_sum(bsum[j]);
+      const int o = o0 + wave * 16 + j;
+      if (lane == 0 && o < Cout) a.bpart[(size_t)blockIdx.y * Cout + o] = v;
+    }
   }
 }
 
-// dW[o][c][tap] = sum_s part[s][o][c][tap]; db[o] = sum_s part[s][o][Cin][centre]
+// dW[o][c][tap] = sum_s part[s][o][c][tap]; db[o] = sum_s bpart[s][o]
 __global__ __launch_bounds__(256) void wgrad_halo_finish_kernel(IgArgs a, int splits) {
-  const int Cin = a.g.Cin, Cout = a.g.Cout, T = a.g.KH * a.g.KW;
-  const int centre = (a.g.KH / 2) * a.g.KW + a.g.KW / 2;
-  const long long per_o = (long long)(Cin + 1) * T;
-  const long long total = (long long)Cout * per_o;
+  const int Cout = a.g.Cout;
+  const long long total = (long long)Cout * a.g.Cin * a.g.KH * a.g.KW;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const int o = (int)(e / per_o);
-    const int rem = (int)(e - (long long)o * per_o);
-    const int c = rem / T, tap = rem - c * T;
-    if (c == Cin && (tap != centre || !a.gbias)) continue;
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * total + e];
-    float* d = c == Cin ? a.gbias + o : a.gweight + ((size_t)o * Cin + c) * T + tap;
-    *d = a.wacc ? *d + v : v;
+    a.gweight[e] = a.wacc ? a.gweight[e] + v : v;
+    if (a.gbias && e < Cout) {
+      float bv = 0.f;
+      for (int s = 0; s < splits; ++s) bv += a.bpart[(size_t)s * Cout + e];
+      a.gbias[e] = a.wacc ? a.gbias[e] + bv : bv;
+    }
   }
 }
 
@@ -1030,15 +1063,17 @@ WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
   pl.tiles_img = ((H + TH - 1) / TH) * pl.tiles_x;
   const int ntiles = B * pl.tiles_img;
   pl.otiles = (Cout + 63) / 64;
-  pl.ctiles = (Cin + 1 + 31) / 32;
+  pl.ctiles = (Cin + 31) / 32;
   const int blocks = pl.otiles * pl.ctiles;
-  int sp = (384 + blocks - 1) / blocks;
-  if (sp > 32) sp = 32;
-  if (sp > ntiles) sp = ntiles;
+  // ~one block per CU, >= 2 pixel tiles per split, <= 16 splits (partials traffic)
+  int sp = (256 + blocks - 1) / blocks;
+  if (sp > 16) sp = 16;
+  if (sp > ntiles / 2) sp = ntiles / 2;
   if (sp < 1) sp = 1;
   pl.tiles_per_split = (ntiles + sp - 1) / sp;
   pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
-  pl.part_bytes = align256((size_t)pl.splits * Cout * (Cin + 1) * KH * KW * sizeof(float));
+  pl.part_bytes = align256((size_t)pl.splits * Cout * Cin * KH * KW * sizeof(float)) +
+                  align256((size_t)pl.splits * Cout * sizeof(float));
   return pl;
 }
 
@@ -1388,12 +1423,13 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.tiles_img = wh.tiles_img;
     a.chunks_per_split = wh.tiles_per_split;
     a.part = reinterpret_cast<float*>(ws_wg);
+    a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)wh.splits * Cout * a.g.Cin * T * sizeof(float)));
     const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
     if (KH == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, s, a);
     else if (KW == 1) hipLaunchKernelGGL((wgrad_halo_kernel<5, 1>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_halo_kernel<3, 3>), grid, dim3(256), 0, s, a);
     if ((st = launch_status("wgrad_halo_kernel launch failed"))) return st;
-    const long long total = (long long)Cout * (a.g.Cin + 1) * T;
+    const long long total = (long long)Cout * a.g.Cin * T;
     long long blocks = (total + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
