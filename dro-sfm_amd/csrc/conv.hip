@@ -1065,10 +1065,10 @@ WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
   pl.otiles = (Cout + 63) / 64;
   pl.ctiles = (Cin + 31) / 32;
   const int blocks = pl.otiles * pl.ctiles;
-  // ~one block per CU, >= 2 pixel tiles per split, <= 16 splits (partials traffic)
-  int sp = (256 + blocks - 1) / blocks;
-  if (sp > 16) sp = 16;
-  if (sp > ntiles / 2) sp = ntiles / 2;
+  // ~1.5 blocks per CU (parallelism beats the partials' extra traffic here)
+  int sp = (384 + blocks - 1) / blocks;
+  if (sp > 32) sp = 32;
+  if (sp > ntiles) sp = ntiles;
   if (sp < 1) sp = 1;
   pl.tiles_per_split = (ntiles + sp - 1) / sp;
   pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
