@@ -564,6 +564,21 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   }
 }
 
+// sum of n partials p[0], p[stride], ... in a fixed order (4 interleaved
+// chains, combined at the end): the loads are independent and issue together
+__device__ __forceinline__ float split_sum(const float* __restrict__ p, size_t stride, int n) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    s0 += p[(size_t)i * stride];
+    s1 += p[(size_t)(i + 1) * stride];
+    s2 += p[(size_t)(i + 2) * stride];
+    s3 += p[(size_t)(i + 3) * stride];
+  }
+  for (; i < n; ++i) s0 += p[(size_t)i * stride];
+  return (s0 + s1) + (s2 + s3);
+}
+
 // split-K finish: sum the partials in split order, then the epilogue
 template <int MODE, int ACT, int EPI>
 __global__ __launch_bounds__(256) void igemm_finish_kernel(IgArgs a, int ksplit) {
@@ -573,7 +588,7 @@ __global__ __launch_bounds__(256) void igemm_finish_kernel(IgArgs a, int ksplit)
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     float v = 0.f;
-    for (int s = 0; s < ksplit; ++s) v += a.part[(size_t)s * total + i];
+    v = split_sum(a.part + i, (size_t)total, ksplit);
     const int row = (int)(i / P);
     const long long p = i - (long long)row * P;
     const int eb = (int)(p / (long long)HW);
@@ -876,11 +891,11 @@ __global__ __launch_bounds__(256) void wgrad_halo_finish_kernel(IgArgs a, int sp
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
     float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * total + e];
+    v = split_sum(a.part + e, (size_t)total, splits);
     a.gweight[e] = a.wacc ? a.gweight[e] + v : v;
     if (a.gbias && e < Cout) {
       float bv = 0.f;
-      for (int s = 0; s < splits; ++s) bv += a.bpart[(size_t)s * Cout + e];
+      bv = split_sum(a.bpart + e, (size_t)Cout, splits);
       a.gbias[e] = a.wacc ? a.gbias[e] + bv : bv;
     }
   }
@@ -898,7 +913,7 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits)
     const int o = (int)(e / NC), n = (int)(e - (long long)o * NC);
     const size_t src = (size_t)o * (NK + 1) + n;
     float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += a.part[(size_t)s * sstride + src];
+    v = split_sum(a.part + src, sstride, splits);
     if (n == NK) {
       a.gbias[o] = a.wacc ? a.gbias[o] + v : v;
     } else {
