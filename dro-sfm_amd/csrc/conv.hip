@@ -361,9 +361,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 // 32x32; BM = 32: 2 pixel halves x 2 channel halves (LDS reduction).
 // Static LDS: 2 stages of (weight tile + CK*HPAD) floats (HaloShape).
 // Compile-time shape of the halo kernel: kernel (KH, KW) -> pixel tile and
-// channels per chunk.  1x5: 4x16 tiles (halo 4x20); 5x1 and 3x3: 8x8 tiles
-// (halo 12x8 / 10x10).  CK: 16 (BM 32) / 8 (BM 64), halved for 3x3, so a
-// thread stages <= 16 weights and <= 4 channels per wave per chunk.
+// channels per chunk.  1x5: 4x16 tiles (halo 4x20); 5x1, 3x3 and 1x1: 8x8
+// tiles (halo 12x8 / 10x10 / none).  CK: 16 (BM 32) / 8 (BM 64), halved for
+// 3x3, doubled for 1x1, so a thread stages <= 16 weights per chunk.
 template <int BM, int KH, int KW>
 struct HaloShape {
   static constexpr int T = KH * KW;
@@ -373,7 +373,7 @@ struct HaloShape {
   static constexpr int HALO = (TH + KH - 1) * HWd;
   static constexpr int HPAD = HALO + ((32 - HALO % 64) + 64) % 64;   // channel stride = 32 mod 64 banks
   static constexpr int NJ = (HALO + 63) / 64;
-  static constexpr int CK = (BM == 32 ? 16 : 8) / (T > 5 ? 2 : 1);
+  static constexpr int CK = (BM == 32 ? 16 : 8) * (T == 1 ? 2 : 1) / (T > 5 ? 2 : 1);
   static constexpr int RUN0 = CK * T, RUN1 = BM * T;                 // weight runs (fwd / dgrad)
   static constexpr int WS0 = RUN0 | 1, WS1 = RUN1 | 1;               // odd LDS strides
   static constexpr int WTOT = BM * CK * T;
@@ -979,7 +979,8 @@ void halo_fill(IgPlan& pl) {
 }
 
 IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
-  const bool shape_ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
+  const bool shape_ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3) ||
+                        (KH == 1 && KW == 1);
   if (!shape_ok) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
   IgPlan pl = {};
   const long long P = (long long)B * H * W;
@@ -992,11 +993,13 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
   pl.bm = (long long)t64 * pl.ptiles >= 480 ? 64 : 32;
   pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
   if (pl.bm == 32) {
-    if (KH == 1) halo_fill<32, 1, 5>(pl);
+    if (KH == 1 && KW == 1) halo_fill<32, 1, 1>(pl);
+    else if (KH == 1) halo_fill<32, 1, 5>(pl);
     else if (KW == 1) halo_fill<32, 5, 1>(pl);
     else halo_fill<32, 3, 3>(pl);
   } else {
-    if (KH == 1) halo_fill<64, 1, 5>(pl);
+    if (KH == 1 && KW == 1) halo_fill<64, 1, 1>(pl);
+    else if (KH == 1) halo_fill<64, 1, 5>(pl);
     else if (KW == 1) halo_fill<64, 5, 1>(pl);
     else halo_fill<64, 3, 3>(pl);
   }
@@ -1071,7 +1074,7 @@ struct WhPlan {
 
 WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
   WhPlan pl = {};
-  pl.ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
+  pl.ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3) || (KH == 1 && KW == 1);
   if (!pl.ok) return pl;
   const int TH = (KW == 1 || (KH == 3 && KW == 3)) ? 8 : 4, TW = 64 / TH;
   pl.tiles_x = (W + TW - 1) / TW;
@@ -1201,11 +1204,13 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
 #define DRO_DCONV(BM_, KH_, KW_) \
     hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI>), grid, dim3(256), 0, s, a)
     if (pl.bm == 32) {
-      if (KH == 1) DRO_DCONV(32, 1, 5);
+      if (KH == 1 && KW == 1) DRO_DCONV(32, 1, 1);
+      else if (KH == 1) DRO_DCONV(32, 1, 5);
       else if (KW == 1) DRO_DCONV(32, 5, 1);
       else DRO_DCONV(32, 3, 3);
     } else {
-      if (KH == 1) DRO_DCONV(64, 1, 5);
+      if (KH == 1 && KW == 1) DRO_DCONV(64, 1, 1);
+      else if (KH == 1) DRO_DCONV(64, 1, 5);
       else if (KW == 1) DRO_DCONV(64, 5, 1);
       else DRO_DCONV(64, 3, 3);
     }
@@ -1440,7 +1445,8 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.part = reinterpret_cast<float*>(ws_wg);
     a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)wh.splits * Cout * a.g.Cin * T * sizeof(float)));
     const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
-    if (KH == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, s, a);
+    if (KH == 1 && KW == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 1>), grid, dim3(256), 0, s, a);
+    else if (KH == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, s, a);
     else if (KW == 1) hipLaunchKernelGGL((wgrad_halo_kernel<5, 1>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_halo_kernel<3, 3>), grid, dim3(256), 0, s, a);
     if ((st = launch_status("wgrad_halo_kernel launch failed"))) return st;

@@ -109,14 +109,14 @@ def test_conv_plans_within_kernel_limits(lib):
                 assert lib.dro_conv2d_plan(rows, kch, KH, KW, B, H, W, info) == 0
                 halo, bm, rt, pt, ks, cps, TH, TW, HWd, HPAD, tx, timg, CK, lds, part, _ = list(info)
                 assert bm in (32, 64) and rt * bm >= rows and ks >= 1 and cps >= 1
-                assert bool(halo) == ((KH, KW) in ((1, 5), (5, 1), (3, 3)))
+                assert bool(halo) == ((KH, KW) in ((1, 5), (5, 1), (3, 3), (1, 1)))
                 if not halo:
                     continue
                 T = KH * KW
                 assert TH * TW == 64 and HWd == TW + KW - 1
                 halo_n = (TH + KH - 1) * HWd
                 assert halo_n <= 256 and HPAD >= halo_n and HPAD % 64 == 32
-                assert (bm, CK) in ((32, 16), (32, 8), (64, 8), (64, 4))
+                assert (bm, CK) in ((32, 16), (32, 8), (64, 8), (64, 4), (32, 32), (64, 16))
                 assert (bm * CK * T + 255) // 256 <= 16            # weight slots per thread
                 odd = lambda n: n | 1
                 stage = max(bm * odd(CK * T), CK * odd(bm * T)) + CK * HPAD

@@ -22,7 +22,7 @@ def main():
         batch["intrinsics"].copy_(batch["_K0"])
         tr.step(batch, flip=False)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
         batch["intrinsics"].copy_(batch["_K0"])
         tr.step(batch, flip=False)
         torch.cuda.synchronize()
@@ -31,6 +31,12 @@ def main():
     print(f"{'op':28s} {'calls':>6s} {'dev us':>9s}  shapes")
     for e in rows[:70]:
         print(f"{e.key[:28]:28s} {e.count:6d} {e.device_time_total:9.0f}  {str(e.input_shapes)[:150]}")
+    st = [e for e in prof.key_averages(group_by_stack_n=6) if e.key in ("aten::add_", "aten::add", "aten::mul", "aten::zeros", "aten::fill_", "aten::copy_")]
+    st.sort(key=lambda e: -e.count)
+    for e in st[:25]:
+        print(f"== {e.key} x{e.count} dev {e.device_time_total:.0f}us")
+        for fr in (e.stack or [])[:6]:
+            print("     ", fr[:150])
     fns = [e for e in prof.key_averages() if "Backward" in e.key or "evaluate_function" in e.key]
     fns.sort(key=lambda e: -e.count)
     for e in fns[:30]:
