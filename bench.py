@@ -157,8 +157,15 @@ def main():
                     help="run the remaining library convolutions on PyTorch's native kernels")
     ap.add_argument("--conv-backend", choices=("hip", "miopen"), default="hip",
                     help="update-block convolutions: native f32-MFMA engine or MIOpen (A/B only)")
+    ap.add_argument("--wgrad-side-stream", action="store_true",
+                    help="direct weight-gradient kernels on a side stream (A/B)")
+    ap.add_argument("--no-direct-wgrad", action="store_true",
+                    help="weight gradients through autograd instead of in place on a side stream (A/B)")
     args = ap.parse_args()
     torch.backends.cudnn.enabled = not args.no_miopen
+    import dro_sfm_amd.hip.conv as _hconv
+    _hconv.set_direct_weight_grads(not args.no_direct_wgrad)
+    _hconv.set_weight_grad_stream(args.wgrad_side_stream)
     from dro_sfm_amd.networks.optim import update as _update
     _update.set_conv_backend(args.conv_backend)
 
@@ -216,7 +223,9 @@ def main():
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch, "ref_frames": NREF,
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
                    "optimizer": "Adam lr 2e-4", "execution": mode,
-                   "update_convs": args.conv_backend},
+                   "update_convs": args.conv_backend,
+                   "weight_grads": "autograd" if args.no_direct_wgrad else
+                   ("in place, side stream" if args.wgrad_side_stream else "in place")},
         "final_loss": round(float(loss), 6),
     }
     if rank == 0 and not args.no_roofline:

@@ -82,7 +82,10 @@ struct IgArgs {
   Slice z, h;             // EPI 1: out = (1-z) h + z q, q = tanh(acc + b); EPI 2: h for r*h
   float* aux;             // EPI 1: q (saved for the backward); EPI 2: r*h  (dense, [B, hd, H, W])
   int hd;                 // EPI 2: rows >= hd are the r gate
-  const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation
+  const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation (or w.r.t. the
+                          // output when folded: then G_pre = galpha * G * act'(gy))
+  const float* gy;        // folded activation: saved output y, dense [B, Cout, H, W]
+  float galpha;           // folded output scale
   float* gsrc[kMaxSrc];   // data-gradient targets per source (nullable)
   int gsrc_ctot[kMaxSrc], gsrc_coff[kMaxSrc], gsrc_acc[kMaxSrc];
   float* gweight;         // [Cout][Cin][KH][KW]
@@ -428,7 +431,11 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
   }
   const unsigned wlast = (unsigned)Cout * CinT - 1;
 
-  float xr[XPER * NJ], wv[S::WPER];
+  // MODE 1 with ACT != 0: the activation derivative is folded into G staging
+  constexpr bool FOLD = MODE == 1 && ACT != 0;
+  const float* __restrict__ Yp = a.gy;
+  const float galpha = a.galpha;
+  float xr[XPER * NJ], yr[FOLD ? XPER * NJ : 1], wv[S::WPER];
   unsigned xmask = 0;
   auto load = [&](int chunk) {
     const int c0 = chunk * CK;
@@ -454,7 +461,9 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
       for (int j = 0; j < NJ; ++j) {
         const bool ok = chok && ((xok >> j) & 1u);
         xmask |= ok ? (1u << (i * NJ + j)) : 0u;
-        xr[i * NJ + j] = p[ok ? sbase + (M ? (unsigned)xpix[j] : 0u) : 0u];
+        const unsigned off = ok ? sbase + (M ? (unsigned)xpix[j] : 0u) : 0u;
+        xr[i * NJ + j] = p[off];
+        if (FOLD) yr[i * NJ + j] = Yp[off];
       }
     }
     const unsigned gbase = MODE == 0 ? (unsigned)row0 * CinT + (unsigned)c0 * T
@@ -475,7 +484,10 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int cl = wave + 4 * i, e = lane + 64 * j;
-        if (e < HPAD) Xs[cl * HPAD + e] = (xmask >> (i * NJ + j)) & 1u ? xr[i * NJ + j] : 0.f;
+        float v = (xmask >> (i * NJ + j)) & 1u ? xr[i * NJ + j] : 0.f;
+        if (MODE == 1) v *= galpha;
+        if (FOLD) v *= act_bwd(yr[i * NJ + j], ACT);
+        if (e < HPAD) Xs[cl * HPAD + e] = v;
       }
     }
 #pragma unroll
@@ -719,7 +731,7 @@ struct HaloShapeW {
   static_assert(NJ <= 2 && TW % 2 == 0, "halo shape");
 };
 
-template <int KH, int KW>
+template <int KH, int KW, int GACT>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
   using S = HaloShapeW<KH, KW>;
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
@@ -742,7 +754,9 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
   const int tend = min(ntiles, tbeg + a.chunks_per_split);
   const bool do_bias = a.gbias && ct == 0;
 
-  float gr[16], xr[8 * NJ], bsum[16];
+  const float* __restrict__ Yp = a.gy;
+  const float galpha = a.galpha;
+  float gr[16], yr[GACT ? 16 : 1], xr[8 * NJ], bsum[16];
   unsigned gmask = 0, xmask = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) bsum[j] = 0.f;
@@ -760,7 +774,9 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
       const int o = o0 + wave * 16 + j;        // scalar
       const bool ok = pin && o < Cout;
       gmask |= ok ? (1u << j) : 0u;
-      gr[j] = Gp[ok ? ((unsigned)b * Cout + o) * HWu + pix : 0u];
+      const unsigned off = ok ? ((unsigned)b * Cout + o) * HWu + pix : 0u;
+      gr[j] = Gp[off];
+      if (GACT) yr[j] = Yp[off];
     }
     // X patch: wave w -> channels c0 + w + 4i, lanes over the halo
     xmask = 0;
@@ -786,7 +802,8 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
     float* Xs = Gs + 64 * GPAD;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const float g = (gmask >> j) & 1u ? gr[j] : 0.f;
+      float g = (gmask >> j) & 1u ? galpha * gr[j] : 0.f;
+      if (GACT) g *= act_bwd(yr[j], GACT);
       Gs[lane * GPAD + wave * 16 + j] = g;
       if (do_bias) bsum[j] += g;
     }
@@ -1417,7 +1434,14 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   char* ws_pre = ws;
   char* ws_ig = ws_pre + align256((size_t)Cout * P * sizeof(float));
   char* ws_wg = ws_ig + plan_igemm(a.g.Cin, Cout, KH, KW, B, H, W).part_bytes;
-  if (pre) {
+  // fold the activation derivative into the halo kernels' G staging when both
+  // gradients run there (dense y); otherwise form G first
+  const WhPlan wh = plan_wgrad_halo(a.g.Cin, Cout, KH, KW, B, H, W);
+  const bool halo_dgrad = plan_igemm(a.g.Cin, Cout, KH, KW, B, H, W).halo;
+  const bool fold = pre && wh.ok && halo_dgrad && (act == 0 || (y->total_channels == Cout && y->channel_offset == 0));
+  a.galpha = fold ? alpha : 1.f;
+  a.gy = (fold && act) ? y->data : nullptr;
+  if (pre && !fold) {
     const size_t total = (size_t)Cout * P;
     size_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -1434,9 +1458,10 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   if (any_dgrad) {
     a.rows = a.g.Cin;
     a.kch = Cout;
-    if ((st = launch_igemm<1, 0, 0>(a, P, ws_ig, s))) return st;
+    const int gact = fold ? act : 0;
+    DRO_ACT_SWITCH(gact, st = (launch_igemm<1, A_, 0>(a, P, ws_ig, s)));
+    if (st) return st;
   }
-  const WhPlan wh = plan_wgrad_halo(a.g.Cin, Cout, KH, KW, B, H, W);
   if (grad_weight && wh.ok) {
     a.otiles = wh.otiles;
     a.tiles_x = wh.tiles_x;
@@ -1445,10 +1470,13 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.part = reinterpret_cast<float*>(ws_wg);
     a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)wh.splits * Cout * a.g.Cin * T * sizeof(float)));
     const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
-    if (KH == 1 && KW == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 1>), grid, dim3(256), 0, s, a);
-    else if (KH == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, s, a);
-    else if (KW == 1) hipLaunchKernelGGL((wgrad_halo_kernel<5, 1>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<3, 3>), grid, dim3(256), 0, s, a);
+    const int gact = fold ? act : 0;
+#define DRO_WH(KH_, KW_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_>), grid, dim3(256), 0, s, a))
+    if (KH == 1 && KW == 1) { DRO_WH(1, 1); }
+    else if (KH == 1) { DRO_WH(1, 5); }
+    else if (KW == 1) { DRO_WH(5, 1); }
+    else { DRO_WH(3, 3); }
+#undef DRO_WH
     if ((st = launch_status("wgrad_halo_kernel launch failed"))) return st;
     const long long total = (long long)Cout * a.g.Cin * T;
     long long blocks = (total + 255) / 256;

@@ -47,6 +47,8 @@ def load():
          P, P, P, P, S)
     _sig(lib.dro_convex_upsample_forward, P, P, I, I, I, I, P, S)
     _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, P, P, S)
+    _sig(lib.dro_bilinear_upsample2x_forward, P, ctypes.c_longlong, I, I, P, S)
+    _sig(lib.dro_bilinear_upsample2x_backward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_conv2d_workspace_bytes, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_plan, I, I, I, I, I, I, I, P)
     _sig(lib.dro_conv2d_forward, P, I, P, P, I, I, I, I, I, I, I, F, P, I, I, P, Z, S)
@@ -66,6 +68,7 @@ EXPORTED = (
     "dro_plane_sweep_forward",
     "dro_photometric_workspace_bytes", "dro_photometric_forward", "dro_photometric_backward",
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
+    "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_gru_backward_elem", "dro_adam_step",

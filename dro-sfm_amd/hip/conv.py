@@ -12,6 +12,16 @@ first backward call of that weight returns the buffer, later ones add into it
 and return None; autograd consumes it only after every producer has run), and
 weight concatenations are built once.  Without the scope every call returns
 its own gradient, as plain autograd would.
+
+Direct weight gradients (the trainer's path): when the parameters a conv reads
+are flagged `_dro_direct` and their `.grad` tensors are back-to-back views of
+one flat buffer (trainers/dp_trainer.GradBuckets lays fused groups out
+adjacently), the weight/bias gradient kernels accumulate straight into those
+views (in stream order by default, or on a side HIP stream concurrently with
+the data-gradient chain: set_weight_grad_stream); autograd receives None for
+the parameters, and a side stream is joined into the caller's stream at the end
+of backward (engine final callback).  Fused weights (z|r gates, shared-input heads) are then
+views of the flat parameter buffer instead of per-forward concatenations.
 """
 import contextlib
 import ctypes
@@ -91,6 +101,96 @@ def cached_cat(key, make):
     return v
 
 
+_DIRECT = [True]
+
+
+def set_direct_weight_grads(enabled):
+    """Enable/disable the side-stream direct weight-gradient path (A/B runs)."""
+    _DIRECT[0] = bool(enabled)
+
+
+def _flat_view(tensors):
+    """[sum(dim 0), *rest] view over tensors stored back to back (contiguous, same
+    trailing shape) in one storage, or None.  Never tracked by autograd."""
+    t0 = tensors[0]
+    base, off, n = t0.untyped_storage().data_ptr(), t0.storage_offset(), 0
+    for t in tensors:
+        if (not t.is_contiguous() or t.untyped_storage().data_ptr() != base or t.storage_offset() != off + n
+                or t.shape[1:] != t0.shape[1:] or t.dtype != t0.dtype):
+            return None
+        n += t.numel()
+    shape = (sum(t.shape[0] for t in tensors),) + tuple(t0.shape[1:])
+    if len(tensors) == 1:
+        return t0.detach()
+    return t0.detach().as_strided(shape, torch.empty(shape, device="meta").stride(), off)
+
+
+def _direct_targets(wparts, bparts, mark=True):
+    """(fused weight, fused bias, grad-weight view, grad-bias view) when the
+    direct path applies to these parameters, else None."""
+    if not _DIRECT[0] or not torch.is_grad_enabled():
+        return None
+    ps = list(wparts) + list(bparts or ())
+    for p in ps:
+        if not (getattr(p, "_dro_direct", False) and p.requires_grad and p.grad is not None):
+            return None
+    gw = _flat_view([p.grad for p in wparts])
+    gb = _flat_view([p.grad for p in bparts]) if bparts else None
+    w = _flat_view(list(wparts))
+    b = _flat_view(list(bparts)) if bparts else None
+    if gw is None or w is None or (bparts and (gb is None or b is None)):
+        return None
+    if mark:
+        _mark_direct(ps)
+    return w, b, gw, gb
+
+
+def _mark_direct(params):
+    for p in params:
+        p._dro_direct_used = True
+
+
+_SIDE = {}
+_JOIN = [False]
+_USE_SIDE = [False]
+
+
+def set_weight_grad_stream(side):
+    """Run the direct weight-gradient kernels on a side stream (True) or in order
+    on the current stream (False, default: measured faster under hipGraph replay,
+    where cross-stream edges add ~4 us bubbles per fork)."""
+    _USE_SIDE[0] = bool(side)
+
+
+def _fork_side():
+    """The weight-gradient stream: the current stream, or a side stream forked
+    from it whose join back is queued once per backward pass as an engine final
+    callback."""
+    main = torch.cuda.current_stream()
+    if not _USE_SIDE[0]:
+        return main
+    side = _SIDE.get(main.device)
+    if side is None:
+        side = _SIDE[main.device] = torch.cuda.Stream(device=main.device)
+    side.wait_stream(main)
+    if not _JOIN[0]:
+        _JOIN[0] = True
+
+        def join():
+            main.wait_stream(side)
+            _JOIN[0] = False
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+    return side
+
+
+def _on_side(side, tensors):
+    if not _USE_SIDE[0]:
+        return
+    for t in tensors:
+        if t is not None:
+            t.record_stream(side)
+
+
 def _grad_buffers(scope, key, weight, nbias, device):
     """(gw, gb, accumulate, first) for one backward call."""
     if scope is None:
@@ -123,8 +223,9 @@ def _dense_out(srcs, C):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, weight, bias, act, alpha, scope, *srcs):
+    def forward(ctx, weight, bias, act, alpha, scope, direct, nsrc, *rest):
         lib = _lib.load()
+        srcs = rest[:nsrc]
         require_device(weight, bias, *srcs, what="conv2d")
         Cout, Cin, KH, KW = weight.shape
         if sum(s.shape[1] for s in srcs) != Cin:
@@ -139,6 +240,8 @@ class _Conv2d(torch.autograd.Function):
         ctx.save_for_backward(weight, out if act else None, *srcs)
         ctx.meta = (act, alpha, bias is not None)
         ctx.scope = scope
+        ctx.direct = direct
+        ctx.nrest = len(rest) - nsrc
         return out
 
     @staticmethod
@@ -150,8 +253,30 @@ class _Conv2d(torch.autograd.Function):
         B, _, H, W = srcs[0].shape
         need = ctx.needs_input_grad
         gout = gout.contiguous()
-        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[5 + i] else None
+        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[7 + i] else None
                 for i, s in enumerate(srcs)]
+        ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
+        if ctx.direct is not None:
+            # data gradients here, weight gradients on the side stream into .grad
+            gw, gb = ctx.direct[2], ctx.direct[3]
+            ptrs, ctot, coff = _grad_targets(gsrc)
+            acc = (ctypes.c_int * len(srcs))()
+            if any(g is not None for g in gsrc):
+                ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
+                check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
+                                              act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
+                                              ptr(gout), ptrs, ctot, coff, acc, None, None, 0, ptr(ws), nws,
+                                              stream_of(gout)), "dro_conv2d_backward(data)")
+            side = _fork_side()
+            _on_side(side, [gout, y, weight, *srcs])
+            with torch.cuda.stream(side):
+                ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
+                check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
+                                              act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
+                                              ptr(gout), None, None, None, None, ptr(gw),
+                                              ptr(gb) if has_bias else None, 1, ptr(ws), nws,
+                                              stream_of(gout)), "dro_conv2d_backward(weight)")
+            return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
         want_w = need[0] or (has_bias and need[1])
         if want_w:
             gw, gb, wacc, first = _grad_buffers(ctx.scope, ("conv", weight.data_ptr(), Cout),
@@ -160,7 +285,6 @@ class _Conv2d(torch.autograd.Function):
             gw, gb, wacc, first = None, None, 0, False
         ptrs, ctot, coff = _grad_targets(gsrc)
         acc = (ctypes.c_int * len(srcs))()
-        ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
         ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
         check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
@@ -168,14 +292,30 @@ class _Conv2d(torch.autograd.Function):
                                       stream_of(gout)), "dro_conv2d_backward")
         rw = gw if (first and need[0]) else None
         rb = gb if (first and has_bias and need[1]) else None
-        return (rw, rb, None, None, None, *gsrc)
+        return (rw, rb, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
 
 
-def conv2d(srcs, weight, bias=None, act=None, alpha=1.0):
-    """act(conv2d(cat(srcs, 1), weight, bias, padding=k//2)) * alpha on f32 MFMA."""
+def conv2d(srcs, weight, bias=None, act=None, alpha=1.0, parts=None):
+    """act(conv2d(cat(srcs, 1), weight, bias, padding=k//2)) * alpha on f32 MFMA.
+
+    parts=(weights, biases): the weight/bias are the dim-0 concatenation of these
+    parameters (weight/bias may then be None: built here, as a flat-buffer view
+    on the direct path or a torch.cat otherwise)."""
     if torch.is_tensor(srcs):
         srcs = [srcs]
-    return _Conv2d.apply(weight, bias, ACT[act], float(alpha), current_scope(), *srcs)
+    if parts is None:
+        parts = ((weight,), (bias,) if bias is not None else ())
+    wparts, bparts = parts
+    direct = _direct_targets(wparts, bparts)
+    if direct is not None:
+        params = [*wparts, *bparts]
+        return _Conv2d.apply(direct[0], direct[1], ACT[act], float(alpha), None, direct, len(srcs),
+                             *srcs, *params)
+    if weight is None:
+        key = ("cat",) + tuple(id(p) for p in wparts)
+        weight, bias = cached_cat(key, lambda: (torch.cat(list(wparts), 0),
+                                                torch.cat(list(bparts), 0) if bparts else None))
+    return _Conv2d.apply(weight, bias, ACT[act], float(alpha), current_scope(), None, len(srcs), *srcs)
 
 
 class _SepGRUHalf(torch.autograd.Function):
@@ -184,7 +324,7 @@ class _SepGRUHalf(torch.autograd.Function):
     Forward: 2 launches (gates + r*h; candidate + blend)."""
 
     @staticmethod
-    def forward(ctx, h, wz, bz, wr, br, wq, bq, scope, *xs):
+    def forward(ctx, h, wz, bz, wr, br, wq, bq, scope, direct, *xs):
         lib = _lib.load()
         require_device(h, wz, wq, *xs, what="sepconvgru")
         h = h.contiguous()
@@ -193,6 +333,8 @@ class _SepGRUHalf(torch.autograd.Function):
         cin = wz.shape[1]
         key = ("zr", wz.data_ptr(), wr.data_ptr())
         wzr, bzr = scope.cats.get(key, (None, None)) if scope is not None else (None, None)
+        if direct is not None:
+            wzr, bzr = direct[0][0], direct[0][1]
         if wzr is None:
             wzr = torch.cat([wz, wr], 0).contiguous()
             bzr = torch.cat([bz, br], 0).contiguous()
@@ -216,6 +358,7 @@ class _SepGRUHalf(torch.autograd.Function):
               "dro_convgru_blend_forward")
         ctx.save_for_backward(h, rh, wzr, wq, zr, q, *xs)
         ctx.scope = scope
+        ctx.direct = direct
         ctx.keys = (key, ("q", wq.data_ptr()))
         return hn
 
@@ -237,8 +380,10 @@ class _SepGRUHalf(torch.autograd.Function):
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(1)")
         # candidate conv over [r*h, x]: d(r*h), dx (overwrite), dWq, dbq
         drh = torch.empty_like(h)
-        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[8 + i] else None
+        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[9 + i] else None
                for i, x in enumerate(xs)]
+        if ctx.direct is not None:
+            return _SepGRUHalf._backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs)
         gwq, gbq, qacc, qfirst = _grad_buffers(ctx.scope, ctx.keys[1], wq, hd, h.device)
         ptrs, ctot, coff = _grad_targets([drh, *dxs])
         acc = (ctypes.c_int * n)()
@@ -259,10 +404,63 @@ class _SepGRUHalf(torch.autograd.Function):
                                       ptr(gwzr), ptr(gbzr), zacc, ptr(ws), nws, st), "dro_conv2d_backward(zr)")
         gz = (gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:]) if zfirst else (None,) * 4
         gq = (gwq, gbq) if qfirst else (None, None)
-        return (dh if need[0] else None, *gz, *gq, None, *dxs)
+        return (dh if need[0] else None, *gz, *gq, None, None, *dxs)
+
+    @staticmethod
+    def _backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs):
+        """Data-gradient chain on the current stream; dWq/dbq and dWz|r/dbz|r
+        accumulate into the flat .grad views on the side stream."""
+        B, hd, H, W = h.shape
+        KH, KW = wq.shape[2:]
+        cin = wq.shape[1]
+        st = stream_of(h)
+        n = 1 + len(xs)
+        (_, _), (gwzr, gbzr), (gwq, gbq) = ctx.direct
+        main = torch.cuda.current_stream()
+        drh = torch.empty_like(h)
+        ptrs, ctot, coff = _grad_targets([drh, *dxs])
+        acc = (ctypes.c_int * n)()
+        ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
+        check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
+                                      0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
+                                      None, None, 0, ptr(ws), nws, st), "dro_conv2d_backward(q data)")
+        side = _fork_side()                       # dq and r*h are final here
+        _on_side(side, [dq, rh, wq, *xs])
+        with torch.cuda.stream(side):
+            wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
+            check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
+                                          0, ctypes.c_float(1.0), None, ptr(dq), None, None, None, None,
+                                          ptr(gwq), ptr(gbq), 1, ptr(wsw), nwsw, stream_of(h)),
+                  "dro_conv2d_backward(q weight)")
+        check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
+                                        ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
+        ptrs, ctot, coff = _grad_targets([dh, *dxs])
+        acc = (ctypes.c_int * n)(*([1] * n))
+        ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
+        check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
+                                      0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
+                                      None, None, 0, ptr(ws), nws, st), "dro_conv2d_backward(zr data)")
+        if side is not main:
+            side.wait_stream(main)                # dz|dr are final after stage 2
+        _on_side(side, [dzr, h, wzr])
+        with torch.cuda.stream(side):
+            wsw, nwsw = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
+            check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
+                                          0, ctypes.c_float(1.0), None, ptr(dzr), None, None, None, None,
+                                          ptr(gwzr), ptr(gbzr), 1, ptr(wsw), nwsw, stream_of(h)),
+                  "dro_conv2d_backward(zr weight)")
+        need = ctx.needs_input_grad
+        return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
 
 
 def sepconvgru_half(h, convz, convr, convq, xs):
     """h' for one SepConvGRU direction; xs: the input sources (virtual concat)."""
+    direct = None
+    zr = _direct_targets((convz.weight, convr.weight), (convz.bias, convr.bias), mark=False)
+    if zr is not None:
+        qd = _direct_targets((convq.weight,), (convq.bias,), mark=False)
+        if qd is not None:
+            direct = ((zr[0], zr[1]), (zr[2], zr[3]), (qd[2], qd[3]))
+            _mark_direct([convz.weight, convz.bias, convr.weight, convr.bias, convq.weight, convq.bias])
     return _SepGRUHalf.apply(h, convz.weight, convz.bias, convr.weight, convr.bias, convq.weight,
-                             convq.bias, current_scope(), *xs)
+                             convq.bias, current_scope(), direct, *xs)

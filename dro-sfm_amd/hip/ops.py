@@ -233,3 +233,36 @@ class _ConvexUpsample(torch.autograd.Function):
 def convex_upsample(inv, mask, ratio=8):
     """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74): [B,1,h,w] -> [B,1,rh,rw]."""
     return _ConvexUpsample.apply(inv, mask, int(ratio))
+
+
+# ------------------------------------------------------------------ bilinear 2x upsample
+class _Bilinear2x(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        lib = _lib.load()
+        require_device(x, what="bilinear_upsample2x")
+        N, C, h, w = x.shape
+        x = x.contiguous()
+        out = torch.empty(N, C, 2 * h, 2 * w, device=x.device, dtype=torch.float32)
+        check(lib.dro_bilinear_upsample2x_forward(ptr(x), N * C, h, w, ptr(out), stream_of(x)),
+              "dro_bilinear_upsample2x_forward")
+        ctx.shape = (N, C, h, w)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        N, C, h, w = ctx.shape
+        gout = gout.contiguous()
+        gx = torch.empty(N, C, h, w, device=gout.device, dtype=torch.float32)
+        check(lib.dro_bilinear_upsample2x_backward(ptr(gout), N * C, h, w, ptr(gx), stream_of(gout)),
+              "dro_bilinear_upsample2x_backward")
+        return gx
+
+
+def bilinear_upsample2x(x):
+    """F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False) for float32
+    NCHW (reference networks/optim/extractor.py:91-97); deterministic backward."""
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("bilinear_upsample2x: expects a float32 NCHW tensor")
+    return _Bilinear2x.apply(x)

@@ -11,10 +11,14 @@ Batch normalisation runs on PyTorch's native kernels, not MIOpen: measured on
 MI355X (tools/diag_miopen2.py), MIOpen's training-mode BN (one-pass variance)
 put 1e-2 relative error on encoder gradients against the fp64 oracle, while
 the native kernels stay at the fp32 floor (~1e-3 through the recurrent net).
+The 2x bilinear upsampling of the fusion head is a HIP kernel
+(hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ... import hip
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -90,10 +94,10 @@ class ResNetEncoder(nn.Module):
         s4 = self.layer1(x)
         s8 = self.layer2(s4)
         x = self.layer3(s8)
-        x = self.upconv1(F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False))
+        x = self.upconv1(hip.bilinear_upsample2x(x))
         x = self.upconv1_fusion(torch.cat([x, s8], 1))
         if self.stride == 4:
-            x = self.upconv2(F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False))
+            x = self.upconv2(hip.bilinear_upsample2x(x))
             x = self.upconv2_fusion(torch.cat([x, s4], 1))
         x = self.out_conv(x)
         if chunks is not None:

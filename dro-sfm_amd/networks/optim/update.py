@@ -61,12 +61,21 @@ def conv(srcs, weight, bias, act=None, alpha=1.0):
 
 
 def conv_cat(x, convs, act=None):
-    """One convolution computing several nn.Conv2d that share the input x (the
-    concatenated weights are built once per forward, hip.weight_grad_scope)."""
-    w, b = hip.cached_cat(("cat",) + tuple(id(c) for c in convs),
-                          lambda: (torch.cat([c.weight for c in convs], 0),
-                                   torch.cat([c.bias for c in convs], 0)))
-    return torch.split(conv(x, w, b, act), [c.out_channels for c in convs], 1)
+    """One convolution computing several nn.Conv2d that share the input x.  The
+    fused weight is a view of the trainer's flat parameter buffer when the
+    group is laid out adjacently (fused_groups), else a concatenation built
+    once per forward (hip.weight_grad_scope)."""
+    if _BACKEND == "hip":
+        y = hip.conv2d(_as_list(x), None, None, act=act,
+                       parts=(tuple(c.weight for c in convs), tuple(c.bias for c in convs)))
+    else:
+        y = conv(x, torch.cat([c.weight for c in convs], 0), torch.cat([c.bias for c in convs], 0), act)
+    return torch.split(y, [c.out_channels for c in convs], 1)
+
+
+def fused_groups(*convs):
+    """Parameter groups read as one fused tensor: [weights], [biases]."""
+    return [[c.weight for c in convs], [c.bias for c in convs]]
 
 
 def mask_seq(hidden_dim, ratio):
@@ -122,6 +131,10 @@ class SepConvGRU(nn.Module):
         z, r = conv_cat([h, *xs], (cz, cr), "sigmoid")
         q = conv([r * h, *xs], cq.weight, cq.bias, "tanh")
         return (1 - z) * h + z * q
+
+    def dro_param_groups(self):
+        """z|r gates of each direction are one fused conv (trainer layout hint)."""
+        return fused_groups(self.convz1, self.convr1) + fused_groups(self.convz2, self.convr2)
 
     def forward(self, h, x):
         """x: the input tensor, or a list of tensors read as their channel concat."""
@@ -197,6 +210,9 @@ class BasicUpdateBlockDepth(nn.Module):
         self.depth_gru = SepConvGRU(hidden_dim=hidden_dim, input_dim=hidden_dim + context_dim)
         self.depth_head = DepthHead(hidden_dim, hidden_dim=hidden_dim, scale=False)
         self.mask = mask_seq(hidden_dim, ratio)
+
+    def dro_param_groups(self):
+        return fused_groups(self.depth_head.conv1, self.mask[0])
 
     def heads(self, net):
         """DepthHead.conv1 and mask.0 read the same state: one launch."""

@@ -43,10 +43,10 @@ def init_distributed(backend=None):
 class GradBuckets:
     """Flat gradient storage + bucketed, backward-overlapped all-reduce."""
 
-    def __init__(self, params, bucket_mb=25.0, group=None):
+    def __init__(self, params, bucket_mb=25.0, group=None, groups=()):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.params = [p for p in params if p.requires_grad]
+        self.params = _adjacent_order([p for p in params if p.requires_grad], groups)
         if any(p.dtype != torch.float32 for p in self.params):
             raise RuntimeError("GradBuckets: fp32 parameters only")
         self.flat = torch.zeros(sum(p.numel() for p in self.params), device=self.params[0].device)
@@ -59,6 +59,9 @@ class GradBuckets:
         self.active = None            # params that receive gradients (learned on step 1)
         self.buckets, self._pending, self._seen = [], [], set()
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        for p in self.params:
+            # hip convs may accumulate this gradient in place (hip/conv.py, direct path)
+            p._dro_direct = True
 
     def _build(self, active):
         self.active = [p for p in self.params if p in active]
@@ -72,7 +75,10 @@ class GradBuckets:
         if cur:
             self.buckets.append(cur)
         self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b}
-        self._need = [len(b) for b in self.buckets]
+        # gradients written in place by the hip convs (side stream, joined at the end
+        # of backward) fire no hook: their buckets are reduced in finish()
+        self._deferred = [any(_direct_used(p) for p in b) for b in self.buckets]
+        self._need = [sum(not _direct_used(p) for p in b) for b in self.buckets]
 
     def _slice(self, bucket):
         """One contiguous flat slice covering a bucket (slots of inactive params
@@ -82,6 +88,10 @@ class GradBuckets:
         return self.flat[lo:hi]
 
     def _on_grad(self, p):
+        if _direct_used(p):
+            # written in place by the hip convs (the hook also fires for the None
+            # autograd receives); its bucket is reduced in finish()
+            return
         if self.active is None:
             self._seen.add(p)
             return
@@ -89,7 +99,7 @@ class GradBuckets:
         if b is None:
             return
         self._left[b] -= 1
-        if self._left[b] == 0 and self.world > 1:
+        if self._left[b] == 0 and self.world > 1 and not self._deferred[b]:
             self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
                                                  group=self.group, async_op=True))
 
@@ -102,7 +112,7 @@ class GradBuckets:
     def finish(self):
         """Complete every bucket's all-reduce and average over ranks."""
         if self.active is None:
-            seen = self._seen
+            seen = self._seen | {p for p in self.params if _direct_used(p)}
             if self.world > 1:
                 flags = torch.tensor([float(p in seen) for p in self.params], device=self.flat.device)
                 dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
@@ -112,11 +122,54 @@ class GradBuckets:
                 for b in self.buckets:
                     dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM, group=self.group)
         else:
+            if self.world > 1:
+                for b, d in zip(self.buckets, self._deferred):
+                    if d:
+                        self._pending.append(dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM,
+                                                             group=self.group, async_op=True))
             for work in self._pending:
                 work.wait()
             self._pending = []
         if self.world > 1:
             self.flat.div_(self.world)
+
+
+def _direct_used(p):
+    return getattr(p, "_dro_direct_used", False)
+
+
+def _adjacent_order(params, groups):
+    """params in registration order, except that each group (a list of
+    parameters read as one fused tensor, e.g. SepConvGRU's z|r weights) is
+    placed back to back at its first member's position."""
+    if not groups:
+        return list(params)
+    present = set(params)
+    lead = {}
+    for g in groups:
+        g = [p for p in g if p in present]
+        if len(g) > 1:
+            for p in g:
+                lead[p] = g
+    out, done = [], set()
+    for p in params:
+        if p in done:
+            continue
+        for q in lead.get(p, [p]):
+            if q not in done:
+                out.append(q)
+                done.add(q)
+    return out
+
+
+def param_groups(model):
+    """Fused-parameter groups declared by modules (`dro_param_groups()`)."""
+    groups = []
+    for m in model.modules():
+        fn = getattr(m, "dro_param_groups", None)
+        if callable(fn):
+            groups.extend(fn())
+    return groups
 
 
 def broadcast_module(module, src=0, group=None):
@@ -195,7 +248,8 @@ class DataParallelTrainer:
                  capturable=False):
         self.model = model
         broadcast_module(model, 0, group)
-        self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb, group=group)
+        self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb, group=group,
+                                 groups=param_groups(model))
         dev = self.grads.flat.device
         if dev.type == "cuda":
             # fused Adam over flat buffers (the product path on the GPU)

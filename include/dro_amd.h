@@ -134,6 +134,14 @@ int dro_convex_upsample_backward(const float* inv, const float* mask, const floa
                                  int B, int h, int w, int ratio,
                                  float* grad_inv, float* grad_mask, void* stream);
 
+/* Bilinear 2x upsampling, align_corners=False (F.interpolate(scale_factor=2,
+ * mode="bilinear") in networks/optim/extractor.py:91-97 of the reference).
+ *   x [planes, h, w] -> out [planes, 2h, 2w]; backward gathers (deterministic). */
+int dro_bilinear_upsample2x_forward(const float* x, long long planes, int h, int w,
+                                    float* out, void* stream);
+int dro_bilinear_upsample2x_backward(const float* grad_out, long long planes, int h, int w,
+                                     float* grad_x, void* stream);
+
 /* ------------------------------------------------------------------------
  * Stride-1 'same' convolutions on f32 MFMA for the recurrent update blocks.
  * Replace the nn.Conv2d + activation + torch.cat chains of

@@ -74,3 +74,32 @@ def _graph_vs_eager():
         # the same Adam update was applied (tolerance: lr-scaled grad noise)
         for p, q in zip(m.parameters(), pg):
             assert float((p.detach() - q).abs().max()) < 1e-5, flip
+
+
+def test_direct_weight_grads_match_autograd_path():
+    """The trainer path (hip convs accumulate weight gradients in place into the
+    flat .grad views on a side stream; fused weights are views of the flat
+    parameter buffer) gives the same loss and gradients as the autograd path
+    (per-call gradient buffers returned to autograd, torch.cat'd weights)."""
+    import dro_sfm_amd.hip.conv as hc
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer
+    batch = _batch()
+    K0 = batch["intrinsics"].clone()
+    out = {}
+    try:
+        with torch.backends.cudnn.flags(enabled=False):
+            for direct in (False, True):
+                hc.set_direct_weight_grads(direct)
+                m = _setup()
+                tr = DataParallelTrainer(m)
+                batch["intrinsics"].copy_(K0)
+                loss = tr.step(batch, flip=False)[0].clone()
+                torch.cuda.synchronize()
+                used = sum(bool(getattr(p, "_dro_direct_used", False)) for p in m.parameters())
+                out[direct] = (loss, tr.grads.flat.clone(), used)
+    finally:
+        hc.set_direct_weight_grads(True)
+    (l0, g0, u0), (l1, g1, u1) = out[False], out[True]
+    assert u0 == 0 and u1 > 20
+    assert O.rel_err(l1.cpu(), l0.cpu()) < 1e-6
+    assert float((g1 - g0).norm() / g0.norm()) < 1e-4

@@ -30,9 +30,13 @@ for step in "$@"; do
     bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchmi) run bench_miopen 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --conv-backend miopen ;;
+    benchnd) run bench_nodirect 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-direct-wgrad ;;
+    benchside) run bench_side 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
+    benche) run bench_eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --eager ;;
     benchn) run bench_native 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-miopen ;;
     prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
+    py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
   esac
 done
