@@ -109,8 +109,83 @@ def roofline_photometric(B, device, iters=20):
             "algorithmic_bytes": int(total_bytes), "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)}
 
 
+ROOFLINE_KERNEL = "dconv_kernel<32, 1, 5, 0, 2, 2>"
+ROOFLINE_FINISH = "igemm_finish_kernel<0, 2, 2>"
+# HBM bytes per launch of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+# passes (tools/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
+def _latest_traffic_file():
+    import glob
+    import re
+    files = glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                   "r*_roofline_traffic.json"))
+    rnd = lambda f: int(re.search(r"r(\d+)_roofline", os.path.basename(f)).group(1))
+    return max(files, key=rnd) if files else None
+
+
+TRAFFIC_FILE = _latest_traffic_file()
+MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_32x32x2_f32)
+
+
+def roofline_conv(device, iters=50, traffic_file=None):
+    """Dominant kernel class of the step: the f32-MFMA direct convolution engine
+    (csrc/conv.hip; dconv + wgrad kernels are ~40% of the step's kernel time).
+    Measured at its busiest shape, the depth SepConvGRU z|r gate conv forward
+    (update.py:59-66 of the reference; 1x5, sigmoid, r*h epilogue):
+    dro_convgru_gates_forward at B=2, 24x80, Cin=160 (h 64 + context 32 + feat
+    63 + inv depth 1), Cout=128 -> dconv_kernel<32,1,5,0,2,2> over 480 blocks
+    (split-K 2) + igemm_finish_kernel<0,2,2> (split sum + sigmoid + r*h).  The
+    HIP events bracket both launches (the rocprof summary lists the two
+    averages; their sum is the event time).
+    Algorithmic flops per call: 2 * Cout * Cin * KH*KW * B*H*W."""
+    import ctypes
+    from dro_sfm_amd.hip import _lib
+    from dro_sfm_amd.hip.conv import _slices, _workspace
+    lib = _lib.load()
+    B, hd, Hf, Wf, cin, KH, KW = 2, 64, H // 8, W // 8, 160, 1, 5
+    g = torch.Generator(device=device)
+    g.manual_seed(11)
+    h = torch.randn(B, hd, Hf, Wf, generator=g, device=device).tanh()
+    srcs = [h] + [torch.randn(B, c, Hf, Wf, generator=g, device=device) for c in (32, 63, 1)]
+    wzr = 0.05 * torch.randn(2 * hd, cin, KH, KW, generator=g, device=device)
+    bzr = 0.05 * torch.randn(2 * hd, generator=g, device=device)
+    zr = torch.empty(B, 2 * hd, Hf, Wf, device=device)
+    rh = torch.empty_like(h)
+    ws, nws = _workspace(B, Hf, Wf, cin, 2 * hd, KH, KW, device)
+    sl = _slices(srcs)
+    stream = torch.cuda.current_stream(device)
+    st = ctypes.c_void_p(stream.cuda_stream)
+
+    def launch():
+        _lib.check(lib.dro_convgru_gates_forward(sl, 4, _lib.ptr(wzr), _lib.ptr(bzr), B, Hf, Wf, hd, KH, KW,
+                                                 _lib.ptr(zr), _lib.ptr(rh), _lib.ptr(ws), nws, st),
+                   "dro_convgru_gates_forward")
+    for _ in range(5):
+        launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    flops = 2.0 * 2 * hd * cin * KH * KW * B * Hf * Wf
+    achieved = flops / (us * 1e-6) / 1e12
+    info = (ctypes.c_longlong * 16)()
+    _lib.check(lib.dro_conv2d_plan(2 * hd, cin, KH, KW, B, Hf, Wf, info), "dro_conv2d_plan")
+    traffic = None
+    if traffic_file and os.path.exists(traffic_file):
+        with open(traffic_file) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    return {"bound": "mfma", "kernel": f"{ROOFLINE_KERNEL} + {ROOFLINE_FINISH} (SepConvGRU z|r gates "
+            f"fwd, B=2 24x80 Cin 160 Cout 128 1x5)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
+            "flops_per_launch": int(flops), "avg_launch_us": round(us, 2), "launches": iters,
+            "split_k": int(info[4])}
+
+
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(model, steps=2):
+def cpu_baseline(model, budget_s=12.0, max_steps=40):
     """Reference algorithm on the host cores: the CPU oracle (a restatement of the
     reference's PyTorch path, pinned to its golden vectors) running the same
     training step -- forward, loss, backward, Adam -- on the same weights."""
@@ -127,7 +202,8 @@ def cpu_baseline(model, steps=2):
     opt = torch.optim.Adam(leaves, lr=2e-4)
     batch = make_batch(2, 1234, "cpu")
     times = []
-    for s in range(steps + 1):
+    s = 0
+    while s == 0 or (sum(times) < budget_s and len(times) < max_steps) or len(times) < 2:
         t0 = time.perf_counter()
         opt.zero_grad()
         out = O.train_step_loss(params, VERSION, MIN_D, MAX_D, batch, kind="selfsup", loss_kw={})
@@ -135,9 +211,12 @@ def cpu_baseline(model, steps=2):
         opt.step()
         if s > 0:
             times.append(time.perf_counter() - t0)
+        s += 1
+    steps = len(times)
     sec = sum(times) / len(times)
     return {"value": round(2 / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed steps (+1 warmup) of the full training step, B=2, 192x640, "
+            "sample": f"{steps} timed steps (+1 warmup; ~{budget_s:.0f} s budget) of the full training "
+                      f"step, B=2, 192x640, "
                       f"N=2, {VERSION}, CPU oracle oracle/dro_oracle.py, torch {torch.__version__}",
             "sec_per_step": round(sec, 3)}
 
@@ -161,8 +240,16 @@ def main():
                     help="direct weight-gradient kernels on a side stream (A/B)")
     ap.add_argument("--no-direct-wgrad", action="store_true",
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
+    ap.add_argument("--roofline-iters", type=int, default=50)
     args = ap.parse_args()
     torch.backends.cudnn.enabled = not args.no_miopen
+    if args.roofline_only:
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        print(json.dumps({"roofline": roofline_conv(dev, args.roofline_iters, TRAFFIC_FILE)}), flush=True)
+        return
     import dro_sfm_amd.hip.conv as _hconv
     _hconv.set_direct_weight_grads(not args.no_direct_wgrad)
     _hconv.set_weight_grad_stream(args.wgrad_side_stream)
@@ -229,7 +316,8 @@ def main():
         "final_loss": round(float(loss), 6),
     }
     if rank == 0 and not args.no_roofline:
-        result["roofline"] = roofline_photometric(args.batch, device)
+        result["roofline"] = roofline_conv(device, args.roofline_iters, TRAFFIC_FILE)
+        result["roofline_photometric"] = roofline_photometric(args.batch, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model)
     if rank == 0:

@@ -32,9 +32,14 @@ for step in "$@"; do
     benchmi) run bench_miopen 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --conv-backend miopen ;;
     benchnd) run bench_nodirect 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-direct-wgrad ;;
     benchside) run bench_side 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
+    benchsf) run bench_splitfinish 600 env DRO_SPLIT_FINISH=1 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     benche) run bench_eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --eager ;;
     benchn) run bench_native 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-miopen ;;
     prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
+    roof) run roofline_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/roof" -o run -- python bench.py --roofline-only ;;
+    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python bench.py --roofline-only &&
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python bench.py --roofline-only &&
+         run pmc_traffic 60 python tools/pmc_traffic.py "$OUT" ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
