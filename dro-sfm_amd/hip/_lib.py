@@ -45,6 +45,9 @@ def load():
          P, P, S)
     _sig(lib.dro_photometric_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I,
          P, P, P, P, S)
+    _sig(lib.dro_supervised_workspace_bytes, I, I, I, I, I, restype=Z)
+    _sig(lib.dro_supervised_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, S)
+    _sig(lib.dro_supervised_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, P, P, S)
     _sig(lib.dro_convex_upsample_forward, P, P, I, I, I, I, P, S)
     _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, P, P, S)
     _sig(lib.dro_bilinear_upsample2x_forward, P, ctypes.c_longlong, I, I, P, S)
@@ -67,6 +70,7 @@ EXPORTED = (
     "dro_warp_cost_forward", "dro_warp_cost_workspace_bytes", "dro_warp_cost_backward",
     "dro_plane_sweep_forward",
     "dro_photometric_workspace_bytes", "dro_photometric_forward", "dro_photometric_backward",
+    "dro_supervised_workspace_bytes", "dro_supervised_forward", "dro_supervised_backward",
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_conv2d_forward", "dro_convgru_gates_forward",

@@ -200,6 +200,71 @@ def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=
     return (loss, metrics, sel) if return_selection else (loss, metrics)
 
 
+# ------------------------------------------------------------------------- supervised loss
+class _Supervised(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gt_inv, inv_depths, pose, gt_pose, K, ref_K, min_depth, max_depth):
+        lib = _lib.load()
+        require_device(gt_inv, inv_depths, gt_pose, K, ref_K, what="supervised_loss")
+        n, B, _, H, W = inv_depths.shape
+        N = gt_pose.shape[0]
+        if gt_inv.shape != (B, 1, H, W) or K.shape != (B, 3, 3) or ref_K.shape != (B, 3, 3):
+            raise RuntimeError("supervised_loss: gt_inv [B,1,H,W] and inv_depths [n,B,1,H,W] must "
+                               "share B,H,W; K/ref_K [B,3,3]")
+        pose_flat, pose_mode, restore = _pose_layout(pose, (N, n, B))
+        gt_flat, gt_mode, _ = _pose_layout(gt_pose, (N, B))
+        if gt_mode != POSE_MATRIX:
+            raise RuntimeError("supervised_loss: gt_pose must be [N,B,3|4,4] matrices")
+        require_device(pose_flat, what="supervised_loss")
+        gt_inv, inv_depths = gt_inv.contiguous(), inv_depths.contiguous()
+        K, ref_K = K.contiguous(), ref_K.contiguous()
+        ws = torch.empty(lib.dro_supervised_workspace_bytes(B, N, n, H, W) // 4 + 1,
+                         device=gt_inv.device, dtype=torch.float32)
+        out = torch.empty(3, device=gt_inv.device, dtype=torch.float32)
+        check(lib.dro_supervised_forward(ptr(gt_inv), ptr(inv_depths), ptr(K), ptr(ref_K),
+                                         ptr(gt_flat), ptr(pose_flat), pose_mode, B, N, n, H, W,
+                                         min_depth, max_depth, ptr(out), ptr(ws),
+                                         stream_of(gt_inv)), "dro_supervised_forward")
+        ctx.save_for_backward(gt_inv, inv_depths, pose_flat, gt_flat, K, ref_K)
+        ctx.cfg = (pose_mode, min_depth, max_depth)
+        ctx.restore = restore
+        metrics = out[1:].detach()
+        ctx.mark_non_differentiable(metrics)
+        return out[0:1], metrics
+
+    @staticmethod
+    def backward(ctx, gloss, _gmetrics):
+        lib = _lib.load()
+        gt_inv, inv_depths, pose_flat, gt_flat, K, ref_K = ctx.saved_tensors
+        pose_mode, min_depth, max_depth = ctx.cfg
+        n, B, _, H, W = inv_depths.shape
+        N = gt_flat.shape[0]
+        gloss = gloss.contiguous()
+        g_inv = torch.empty_like(inv_depths)
+        g_pose = torch.empty_like(pose_flat)
+        ws = torch.empty(lib.dro_supervised_workspace_bytes(B, N, n, H, W) // 4 + 1,
+                         device=gt_inv.device, dtype=torch.float32)
+        check(lib.dro_supervised_backward(ptr(gt_inv), ptr(inv_depths), ptr(K), ptr(ref_K),
+                                          ptr(gt_flat), ptr(pose_flat), pose_mode, B, N, n, H, W,
+                                          min_depth, max_depth, ptr(gloss), ptr(g_inv),
+                                          ptr(g_pose), ptr(ws), stream_of(gt_inv)),
+              "dro_supervised_backward")
+        need = ctx.needs_input_grad
+        return (None, g_inv if need[1] else None, ctx.restore(g_pose) if need[2] else None,
+                None, None, None, None, None)
+
+
+def supervised_loss(gt_inv, inv_depths, pose, gt_pose, K, ref_K=None, *, min_depth, max_depth):
+    """Fused SupervisedDepthPoseLoss (supervised_loss.py:343-371, 'sparse-l1').
+
+    gt_inv [B,1,H,W]; inv_depths [n,B,1,H,W]; pose [N,n,B,6] euler vectors or
+    [N,n,B,3|4,4] matrices; gt_pose [N,B,3|4,4].  Returns (loss [1], detached
+    metrics [2] = (depth_loss, pose_loss)).
+    """
+    return _Supervised.apply(gt_inv, inv_depths, pose, gt_pose, K, K if ref_K is None else ref_K,
+                             float(min_depth), float(max_depth))
+
+
 # ------------------------------------------------------------------------- convex upsample
 class _ConvexUpsample(torch.autograd.Function):
     @staticmethod

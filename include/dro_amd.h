@@ -125,6 +125,34 @@ int dro_photometric_backward(const float* image, const float* context, const flo
                              void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Supervised depth + pose loss (sparse-l1).
+ * Replaces SupervisedDepthPoseLoss.forward (losses/supervised_loss.py:343-371):
+ * calculate_loss (:244-277) + calc_pose_loss (:293-325) with get_ref_coords
+ * (:279-291), for predictions at the ground-truth resolution.
+ *   gt_inv [B,1,H,W]; inv_depths [n,B,1,H,W]; K, ref_K [B,3,3];
+ *   gt_pose [N,B,12] (row-major [R|t], the Tcw of each context frame);
+ *   pose [N,n,B,6|12] predicted poses; min_depth/max_depth as in the loss.
+ *   out [3] = {loss, depth_loss metric, pose_loss metric}.
+ * `workspace` (dro_supervised_workspace_bytes) is scratch only; forward and
+ * backward share no state. */
+size_t dro_supervised_workspace_bytes(int B, int N, int n, int H, int W);
+
+int dro_supervised_forward(const float* gt_inv, const float* inv_depths, const float* K,
+                           const float* ref_K, const float* gt_pose, const float* pose,
+                           int pose_mode, int B, int N, int n, int H, int W,
+                           float min_depth, float max_depth, float* out,
+                           void* workspace, void* stream);
+
+/* grad_out: device pointer to d(total)/d(loss) (1 float).  Writes
+ * grad_inv_depths [n,B,1,H,W] and grad_pose [N,n,B,6|12]. */
+int dro_supervised_backward(const float* gt_inv, const float* inv_depths, const float* K,
+                            const float* ref_K, const float* gt_pose, const float* pose,
+                            int pose_mode, int B, int N, int n, int H, int W,
+                            float min_depth, float max_depth, const float* grad_out,
+                            float* grad_inv_depths, float* grad_pose, void* workspace,
+                            void* stream);
+
+/* ------------------------------------------------------------------------
  * Convex 8x upsampling: DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74).
  *   inv [B,1,h,w]; mask [B,9*r*r,h,w] -> out [B,1,h*r,w*r]
  * ---------------------------------------------------------------------- */

@@ -1,0 +1,188 @@
+"""Supervised depth + pose loss (csrc/supervised.hip) against the reference
+golden vectors and the CPU oracle (oracle/dro_oracle.py:221-251, which
+follows losses/supervised_loss.py:244-371).
+
+Tolerance: 1e-4 relative (max|a-b| / max|b|) for the loss scalars and the
+gradients (BASELINE.json north_star).  Near-ties of the |difference| <= 1
+clamp and of the [-1, 1] masks could flip a pixel between fp32 orders; the
+synthetic poses keep every coordinate well away from them.
+"""
+import ctypes
+import os
+
+import pytest
+import torch
+
+from common import SCANNET_K_320, kitti_K, load_fixture
+from oracle import dro_oracle as O
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-4
+DEV = "cuda"
+
+
+def rel(a, b):
+    return O.rel_err(a.detach().cpu(), b.detach().cpu())
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import dro_sfm_amd.hip as H
+    from dro_sfm_amd.hip import _lib
+    _lib.load()
+    return H
+
+
+def _gt_inv(gt_depth):
+    return torch.where(gt_depth <= 0, torch.zeros_like(gt_depth), 1.0 / gt_depth.clamp(min=1e-6))
+
+
+def _oracle(invs, gt_inv, gt_poses, vecs, K, mind, maxd):
+    """Oracle loss + grads; vecs [B,N,n,6] euler (the layout the net emits)."""
+    invs = [i.detach().cpu().clone().requires_grad_(True) for i in invs]
+    v = vecs.detach().cpu().clone().requires_grad_(True)
+    N, n = v.shape[1], v.shape[2]
+    poses = [[v[:, j, i] for i in range(n)] for j in range(N)]
+    out = O.supervised_depth_pose_loss(invs, gt_inv.cpu(), [g.cpu() for g in gt_poses], poses,
+                                       K.cpu(), K.cpu(), mind, maxd)
+    out["loss"].sum().backward()
+    return out, torch.stack([i.grad for i in invs]), v.grad
+
+
+def _run(hip, invs, gt_inv, gt_poses, vecs, K, mind, maxd, as_matrix=False):
+    """HIP loss + grads.  vecs [B,N,n,6] -> kernel layout [N,n,B,6]."""
+    inv_t = torch.stack(list(invs)).to(DEV).clone().requires_grad_(True)
+    v = vecs.to(DEV).permute(1, 2, 0, 3).contiguous().clone().requires_grad_(True)
+    pose = (O.vec_to_transform(v.reshape(-1, 6).cpu()).to(DEV).reshape(*v.shape[:3], 4, 4)
+            if as_matrix else v)
+    gt = torch.stack([g.to(DEV) for g in gt_poses])
+    loss, metrics = hip.supervised_loss(gt_inv.to(DEV), inv_t, pose, gt, K.to(DEV),
+                                        min_depth=mind, max_depth=maxd)
+    loss.sum().backward()
+    return loss, metrics, inv_t.grad, v.grad.permute(2, 0, 1, 3)
+
+
+@pytest.mark.gpu
+def test_supervised_golden(hip):
+    d = load_fixture(os.path.join(G, "sup_loss.npz"))
+    N, n = d["poses"].shape[1], d["poses"].shape[2]
+    gt_inv = _gt_inv(d["gt_depth"])
+    loss, metrics, g_inv, g_pose = _run(hip, d["inv_depths"], gt_inv,
+                                        [d["gt_poses"][:, j] for j in range(N)], d["poses"], d["K"],
+                                        float(d["min_depth"]), float(d["max_depth"]))
+    assert rel(loss, d["loss"]) < TOL
+    assert rel(metrics[0], d["depth_loss"]) < TOL
+    assert rel(metrics[1], d["pose_loss"]) < TOL
+    assert rel(g_inv, d["g_inv_depths"]) < TOL
+    assert rel(g_pose, d["g_poses"]) < TOL
+
+
+def _scene(B, N, n, H, W, K, mind, maxd, seed, valid_frac=1.0):
+    g = torch.Generator().manual_seed(seed)
+    gt_depth = mind + (maxd / 4.0 - mind) * 1.2 * torch.rand(B, 1, H, W, generator=g)
+    if valid_frac < 1.0:
+        gt_depth = gt_depth * (torch.rand(B, 1, H, W, generator=g) < valid_frac)
+    gt_inv = _gt_inv(gt_depth)
+    invs = [(gt_inv + 0.02 * torch.randn(B, 1, H, W, generator=g)) for _ in range(n)]
+    gt_vec = torch.cat([0.2 * torch.randn(B, N, 3, generator=g),
+                        0.02 * torch.randn(B, N, 3, generator=g)], -1)
+    gt_poses = [O.vec_to_transform(gt_vec[:, j]) for j in range(N)]
+    vecs = gt_vec.unsqueeze(2) + torch.cat([0.05 * torch.randn(B, N, n, 3, generator=g),
+                                            0.005 * torch.randn(B, N, n, 3, generator=g)], -1)
+    return invs, gt_inv, gt_poses, vecs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["scannet_view3", "scannet_view5", "kitti_sparse"])
+@pytest.mark.parametrize("as_matrix", [False, True])
+def test_supervised_vs_oracle(hip, cfg, as_matrix):
+    if cfg.startswith("scannet"):
+        B, N, n, H, W, mind, maxd, frac = 2, (2 if cfg == "scannet_view3" else 4), 4, 240, 320, 0.2, 10.0, 1.0
+        K = torch.tensor(SCANNET_K_320).unsqueeze(0).repeat(B, 1, 1)
+    else:  # KITTI 192x640, sparse LiDAR-like GT (5 % valid), it12-h: n = 4
+        B, N, n, H, W, mind, maxd, frac = 1, 2, 4, 192, 640, 0.2, 80.0, 0.05
+        K = kitti_K(B)
+    invs, gt_inv, gt_poses, vecs = _scene(B, N, n, H, W, K, mind, maxd, seed=7, valid_frac=frac)
+    ref, rg_inv, rg_pose = _oracle(invs, gt_inv, gt_poses, vecs, K, mind, maxd)
+    loss, metrics, g_inv, g_pose = _run(hip, invs, gt_inv, gt_poses, vecs, K, mind, maxd, as_matrix)
+    assert rel(loss, ref["loss"]) < TOL
+    assert rel(metrics[0], ref["depth_loss"]) < TOL
+    assert rel(metrics[1], ref["pose_loss"]) < TOL
+    assert rel(g_inv, rg_inv) < TOL
+    assert rel(g_pose, rg_pose) < TOL
+
+
+@pytest.mark.gpu
+def test_supervised_edge_cases(hip):
+    B, N, n, H, W = 2, 2, 3, 48, 64
+    K = torch.tensor(SCANNET_K_320).unsqueeze(0).repeat(B, 1, 1) * 0.2
+    K[:, 2, 2] = 1.0
+    invs, gt_inv, gt_poses, vecs = _scene(B, N, n, H, W, K, 0.2, 10.0, seed=3)
+    # no valid ground truth anywhere: loss and every gradient are exactly 0
+    zero = torch.zeros_like(gt_inv)
+    loss, metrics, g_inv, g_pose = _run(hip, invs, zero, gt_poses, vecs, K, 0.2, 10.0)
+    assert float(loss) == 0.0 and float(metrics.abs().sum()) == 0.0
+    assert float(g_inv.abs().sum()) == 0.0 and float(g_pose.abs().sum()) == 0.0
+    # predicted poses that throw every point out of the image (both coordinates:
+    # the reference masks u and v separately): pose term 0
+    far = vecs.clone()
+    far[..., 0:2] += 100.0
+    ref, _, rg_pose = _oracle(invs, gt_inv, gt_poses, far, K, 0.2, 10.0)
+    loss, metrics, _, g_pose = _run(hip, invs, gt_inv, gt_poses, far, K, 0.2, 10.0)
+    assert float(ref["pose_loss"]) == 0.0 and float(metrics[1]) == 0.0
+    assert float(g_pose.abs().sum()) == 0.0 and float(rg_pose.abs().sum()) == 0.0
+    assert rel(loss, ref["loss"]) < TOL
+    # single prediction, odd sizes (ragged last pixel block)
+    invs, gt_inv, gt_poses, vecs = _scene(1, 1, 1, 37, 53, K[:1], 0.2, 10.0, seed=5)
+    ref, rg_inv, rg_pose = _oracle(invs, gt_inv, gt_poses, vecs, K[:1], 0.2, 10.0)
+    loss, _, g_inv, g_pose = _run(hip, invs, gt_inv, gt_poses, vecs, K[:1], 0.2, 10.0)
+    assert rel(loss, ref["loss"]) < TOL
+    assert rel(g_inv, rg_inv) < TOL and rel(g_pose, rg_pose) < TOL
+
+
+@pytest.mark.gpu
+def test_supervised_deterministic(hip):
+    B, N, n, H, W = 2, 2, 4, 240, 320
+    K = torch.tensor(SCANNET_K_320).unsqueeze(0).repeat(B, 1, 1)
+    invs, gt_inv, gt_poses, vecs = _scene(B, N, n, H, W, K, 0.2, 10.0, seed=11)
+    a = _run(hip, invs, gt_inv, gt_poses, vecs, K, 0.2, 10.0)
+    b = _run(hip, invs, gt_inv, gt_poses, vecs, K, 0.2, 10.0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_supervised_rejects_bad_input(hip):
+    B, N, n, H, W = 1, 1, 2, 16, 16
+    K = torch.eye(3).unsqueeze(0)
+    gt = torch.ones(B, 1, H, W)
+    invs = torch.ones(n, B, 1, H, W)
+    pose = torch.zeros(N, n, B, 6)
+    gtp = torch.eye(4).expand(N, B, 4, 4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        hip.supervised_loss(gt, invs, pose, gtp, K, min_depth=0.1, max_depth=10.0)
+    with pytest.raises(RuntimeError, match="share B,H,W"):
+        hip.supervised_loss(gt[..., :8].to(DEV), invs.to(DEV), pose.to(DEV), gtp.to(DEV), K.to(DEV),
+                            min_depth=0.1, max_depth=10.0)
+    with pytest.raises(RuntimeError, match="min_depth"):
+        hip.supervised_loss(gt.to(DEV), invs.to(DEV), pose.to(DEV), gtp.to(DEV), K.to(DEV),
+                            min_depth=10.0, max_depth=1.0)
+
+
+def test_supervised_capi_rejects_null_and_sizes():
+    """No GPU needed: argument checks happen before any launch."""
+    import torch  # noqa: F401,F811
+    from dro_sfm_amd.hip import _lib
+    lib = _lib.load()
+    P = ctypes.c_void_p
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, P)
+    assert lib.dro_supervised_forward(None, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.1, 10.0, p, p,
+                                      None) == -1
+    assert lib.dro_supervised_forward(p, p, p, p, p, p, 0, 1, 1, 1, 1, 8, 0.1, 10.0, p, p,
+                                      None) == -2
+    assert lib.dro_supervised_forward(p, p, p, p, p, p, 5, 1, 1, 1, 8, 8, 0.1, 10.0, p, p,
+                                      None) == -3
+    assert lib.dro_supervised_backward(p, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.1, 10.0, p, None, p,
+                                       p, None) == -1
+    assert lib.dro_supervised_workspace_bytes(2, 2, 4, 240, 320) >= 2 * 4 * 2 * 75 * 12 * 4
