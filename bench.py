@@ -28,13 +28,44 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "training images/sec (KITTI 192x640 mf self-sup)"
-VERSION = "it8-seq4-inter-out"
-H, W, NREF, MIN_D, MAX_D = 192, 640, 2, 0.5, 80.0
 KITTI_K = [[371.8, 0.0, 314.1], [0.0, 369.4, 88.5], [0.0, 0.0, 1.0]]
-LOSS_KW = dict(ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
-               photometric_reduce_op="min", disp_norm=True, clip_loss=0.0, progressive_scaling=0.0,
-               padding_mode="zeros", automask_loss=True, num_scales=4, rotation_mode="euler",
-               upsample_depth_maps=True, min_depth=MIN_D, max_depth=MAX_D)
+SCANNET_K = [[289.0, 0.0, 160.0], [0.0, 290.0, 120.0], [0.0, 0.0, 1.0]]
+# BASELINE.json configs; `kitti_selfsup` (configs[1]) is the metric's workload and
+# the default.  The others are single-GPU runs of configs[2] / the per-GPU shard of
+# configs[4], reported with --workload.
+WORKLOADS = {
+    "kitti_selfsup": dict(name="KITTI 192x640 mf self-sup (configs[1])", kind="selfsup",
+                          version="it8-seq4-inter-out", H=192, W=640, nref=2, batch=2, min_d=0.5,
+                          max_d=80.0, K=KITTI_K,
+                          metric="training images/sec (KITTI 192x640 mf self-sup)"),
+    "scannet_sup": dict(name="ScanNet 240x320 view3 supervised (configs[2])", kind="sup",
+                        version="it12-h-out", H=240, W=320, nref=2, batch=8, min_d=0.2, max_d=10.0,
+                        K=SCANNET_K, metric="training images/sec (ScanNet 240x320 view3 sup)"),
+    "scannet_selfsup5": dict(name="ScanNet 240x320 view5 self-sup, one rank of configs[4]",
+                             kind="selfsup", version="it12-h-out", H=240, W=320, nref=4, batch=4,
+                             min_d=0.2, max_d=10.0, K=SCANNET_K,
+                             metric="training images/sec (ScanNet 240x320 view5 self-sup)"),
+}
+WL = dict(WORKLOADS["kitti_selfsup"])
+VERSION = WL["version"]
+H, W, NREF, MIN_D, MAX_D = WL["H"], WL["W"], WL["nref"], WL["min_d"], WL["max_d"]
+
+
+def set_workload(name):
+    global WL, VERSION, H, W, NREF, MIN_D, MAX_D
+    WL = dict(WORKLOADS[name])
+    VERSION = WL["version"]
+    H, W, NREF, MIN_D, MAX_D = WL["H"], WL["W"], WL["nref"], WL["min_d"], WL["max_d"]
+
+
+def loss_kw():
+    return dict(ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
+                photometric_reduce_op="min", disp_norm=True, clip_loss=0.0, progressive_scaling=0.0,
+                padding_mode="zeros", automask_loss=True, num_scales=4, rotation_mode="euler",
+                upsample_depth_maps=True, min_depth=MIN_D, max_depth=MAX_D,
+                supervised_method="sparse-l1", supervised_num_scales=4)
+
+
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -42,6 +73,15 @@ def smooth_images(n, gen, device):
     lo = torch.rand(n, 3, H // 8, W // 8, generator=gen, device=device)
     up = torch.nn.functional.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False)
     return (up + 0.1 * torch.rand(n, 3, H, W, generator=gen, device=device)).clamp(0, 1)
+
+
+def _vec_to_mat(vec):
+    """[B,6] (t, euler xyz) -> [B,4,4] (geometry/pose_utils.py:40-85)."""
+    from dro_sfm_amd.geometry.pose import euler2mat
+    T = torch.eye(4, device=vec.device).repeat(vec.shape[0], 1, 1)
+    T[:, :3, :3] = euler2mat(vec[:, 3:])
+    T[:, :3, 3] = vec[:, :3]
+    return T
 
 
 def make_batch(B, seed, device):
@@ -52,15 +92,26 @@ def make_batch(B, seed, device):
     for j in range(NREF):
         shift = (-1) ** j * (2 + j)
         refs.append((0.97 * torch.roll(img, shift, 3) + 0.03 * smooth_images(B, g, device)).clamp(0, 1))
-    K = torch.tensor(KITTI_K, device=device).unsqueeze(0).repeat(B, 1, 1)
-    return {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
-            "intrinsics": K, "_K0": K.clone()}
+    K = torch.tensor(WL["K"], device=device).unsqueeze(0).repeat(B, 1, 1)
+    batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
+             "intrinsics": K, "_K0": K.clone()}
+    if WL["kind"] == "sup":
+        # dense GT depth U[min, max/4*1.2] (ScanNet-like) and GT context poses
+        batch["depth"] = MIN_D + (MAX_D / 4 * 1.2 - MIN_D) * torch.rand(B, 1, H, W, generator=g,
+                                                                         device=device)
+        vec = torch.cat([0.1 * torch.randn(B, 3, generator=g, device=device),
+                         0.01 * torch.randn(B, 3, generator=g, device=device)], 1)
+        batch["pose_context"] = [_vec_to_mat((-1) ** j * vec) for j in range(NREF)]
+    return batch
 
 
 def build_model(device, flip_prob):
-    from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF
     from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
-    model = SelfSupModelMF(flip_lr_prob=flip_prob, **LOSS_KW)
+    if WL["kind"] == "sup":
+        from dro_sfm_amd.models.SupModelMF import SupModelMF as Model
+    else:
+        from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF as Model
+    model = Model(flip_lr_prob=flip_prob, **loss_kw())
     model.add_depth_net(DepthPoseNet(version=VERSION, min_depth=MIN_D, max_depth=MAX_D))
     return model.to(device)
 
@@ -73,7 +124,7 @@ def roofline_photometric(B, device, iters=20):
       fwd: image 12 + context 12N + inv 4n + sel n   bytes/px
       bwd: image 12 + context 12N + inv 4n + sel n + grad_inv 4n bytes/px."""
     import dro_sfm_amd.hip as hip
-    n = 9
+    n = 9 if VERSION.startswith("it8") else 4
     g = torch.Generator(device=device)
     g.manual_seed(5)
     img = smooth_images(B, g, device)
@@ -81,7 +132,7 @@ def roofline_photometric(B, device, iters=20):
     invs = (0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g, device=device)).requires_grad_(True)
     pose = torch.cat([0.1 * torch.randn(NREF, n, B, 3, generator=g, device=device),
                       0.02 * torch.randn(NREF, n, B, 3, generator=g, device=device)], 3).requires_grad_(True)
-    K = torch.tensor(KITTI_K, device=device).unsqueeze(0).repeat(B, 1, 1)
+    K = torch.tensor(WL["K"], device=device).unsqueeze(0).repeat(B, 1, 1)
     for _ in range(3):
         loss, _ = hip.photometric_loss(img, ctx, invs, pose, K)
         loss.backward()
@@ -107,6 +158,78 @@ def roofline_photometric(B, device, iters=20):
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
             "algorithmic_bytes": int(total_bytes), "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)}
+
+
+def _event_loop(fn, iters, device):
+    """Average ms of fn() over iters launches, HIP events on the launch stream."""
+    stream = torch.cuda.current_stream(device)
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def roofline_plane_sweep(device, D=64, B=2, C=128, iters=20):
+    """D = 64 depth-hypothesis stress of configs[1]: one
+    plane_sweep_kernel launch builds the cost volume [B, D, C, h, w] of D
+    fronto-parallel planes (disp = linspace(0, 1, D) through disp_to_depth) at
+    the feature resolution.  Algorithmic bytes per launch: fmap + fmap_ref read
+    once (2 * 4 * B*C*P) + the volume written once (4 * B*D*C*P)."""
+    import dro_sfm_amd.hip as hip
+    h, w = H // 8, W // 8
+    g = torch.Generator(device=device)
+    g.manual_seed(17)
+    fmap = torch.randn(B, C, h, w, generator=g, device=device)
+    fref = torch.randn(B, C, h, w, generator=g, device=device)
+    disp = torch.linspace(0, 1, D, device=device)
+    pose = torch.cat([0.1 * torch.randn(B, 3, generator=g, device=device),
+                      0.01 * torch.randn(B, 3, generator=g, device=device)], 1)
+    K = torch.tensor(WL["K"], device=device).unsqueeze(0).repeat(B, 1, 1)
+    ms = _event_loop(lambda: hip.plane_sweep_cost(fmap, fref, disp, pose, K, min_depth=MIN_D,
+                                                  max_depth=MAX_D), iters, device)
+    P = h * w
+    nbytes = 2 * 4 * B * C * P + 4 * B * D * C * P
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": f"plane_sweep_kernel (D={D}, B={B}, C={C}, {h}x{w})",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "algorithmic_bytes": int(nbytes), "avg_launch_us": round(ms * 1e3, 2), "launches": iters}
+
+
+def roofline_supervised(B, device, n=4, iters=20):
+    """Fused supervised loss (csrc/supervised.hip) forward + backward at the
+    workload shape.  Algorithmic bytes: fwd gt_inv + n inv maps read (4 + 4n per
+    px), bwd the same plus n gradient maps written (4 + 8n per px)."""
+    import dro_sfm_amd.hip as hip
+    g = torch.Generator(device=device)
+    g.manual_seed(19)
+    gt = MIN_D + (MAX_D / 4 - MIN_D) * torch.rand(B, 1, H, W, generator=g, device=device)
+    gt_inv = 1.0 / gt
+    invs = (gt_inv.unsqueeze(0) + 0.02 * torch.randn(n, B, 1, H, W, generator=g, device=device))
+    invs.requires_grad_(True)
+    vec = torch.cat([0.1 * torch.randn(NREF, n, B, 3, generator=g, device=device),
+                     0.01 * torch.randn(NREF, n, B, 3, generator=g, device=device)], 3)
+    vec.requires_grad_(True)
+    gtp = torch.stack([_vec_to_mat(vec[j, 0].detach() + 0.01) for j in range(NREF)])
+    K = torch.tensor(WL["K"], device=device).unsqueeze(0).repeat(B, 1, 1)
+
+    def fb():
+        loss, _ = hip.supervised_loss(gt_inv, invs, vec, gtp, K, min_depth=MIN_D, max_depth=MAX_D)
+        loss.backward()
+    ms = _event_loop(fb, iters, device)
+    HW = H * W
+    nbytes = B * HW * ((4 + 4 * n) + (4 + 8 * n))
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "sup_loss_kernel fwd+bwd (+ finalize kernels)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "algorithmic_bytes": int(nbytes), "fwd_bwd_ms": round(ms, 4)}
 
 
 ROOFLINE_KERNEL = "dconv_kernel<32, 1, 5, 0, 2, 2>"
@@ -141,7 +264,8 @@ def roofline_conv(device, iters=50, traffic_file=None):
     from dro_sfm_amd.hip import _lib
     from dro_sfm_amd.hip.conv import _slices, _workspace
     lib = _lib.load()
-    B, hd, Hf, Wf, cin, KH, KW = 2, 64, H // 8, W // 8, 160, 1, 5
+    # fixed at the metric's (KITTI 192x640, configs[1]) shape whatever --workload is
+    B, hd, Hf, Wf, cin, KH, KW = 2, 64, 192 // 8, 640 // 8, 160, 1, 5
     g = torch.Generator(device=device)
     g.manual_seed(11)
     h = torch.randn(B, hd, Hf, Wf, generator=g, device=device).tanh()
@@ -200,13 +324,14 @@ def cpu_baseline(model, budget_s=12.0, max_steps=40):
             v.requires_grad_(True)
             leaves.append(v)
     opt = torch.optim.Adam(leaves, lr=2e-4)
-    batch = make_batch(2, 1234, "cpu")
+    B = WL["batch"]
+    batch = make_batch(B, 1234, "cpu")
     times = []
     s = 0
     while s == 0 or (sum(times) < budget_s and len(times) < max_steps) or len(times) < 2:
         t0 = time.perf_counter()
         opt.zero_grad()
-        out = O.train_step_loss(params, VERSION, MIN_D, MAX_D, batch, kind="selfsup", loss_kw={})
+        out = O.train_step_loss(params, VERSION, MIN_D, MAX_D, batch, kind=WL["kind"], loss_kw={})
         out["loss"].sum().backward()
         opt.step()
         if s > 0:
@@ -214,10 +339,10 @@ def cpu_baseline(model, budget_s=12.0, max_steps=40):
         s += 1
     steps = len(times)
     sec = sum(times) / len(times)
-    return {"value": round(2 / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(B / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{steps} timed steps (+1 warmup; ~{budget_s:.0f} s budget) of the full training "
-                      f"step, B=2, 192x640, "
-                      f"N=2, {VERSION}, CPU oracle oracle/dro_oracle.py, torch {torch.__version__}",
+                      f"step, B={B}, {H}x{W}, "
+                      f"N={NREF}, {VERSION}, CPU oracle oracle/dro_oracle.py, torch {torch.__version__}",
             "sec_per_step": round(sec, 3)}
 
 
@@ -227,7 +352,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=2, help="target frames per GPU")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="kitti_selfsup",
+                    help="BASELINE.json config (default: the metric's, configs[1])")
+    ap.add_argument("--batch", type=int, default=None, help="target frames per GPU (default: the workload's)")
     ap.add_argument("--flip-prob", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -244,6 +371,9 @@ def main():
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
     args = ap.parse_args()
+    set_workload(args.workload)
+    if args.batch is None:
+        args.batch = WL["batch"]
     torch.backends.cudnn.enabled = not args.no_miopen
     if args.roofline_only:
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
@@ -302,11 +432,11 @@ def main():
         elapsed = float(t)
     images = world * args.batch * args.steps
     result = {
-        "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s",
+        "metric": WL["metric"], "value": round(images / elapsed, 3), "unit": "images/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "KITTI 192x640 mf self-sup (configs[1])", "model": f"DepthPoseNet {VERSION}",
+        "config": {"workload": WL["name"], "model": f"DepthPoseNet {VERSION}",
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch, "ref_frames": NREF,
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
                    "optimizer": "Adam lr 2e-4", "execution": mode,
@@ -317,7 +447,12 @@ def main():
     }
     if rank == 0 and not args.no_roofline:
         result["roofline"] = roofline_conv(device, args.roofline_iters, TRAFFIC_FILE)
-        result["roofline_photometric"] = roofline_photometric(args.batch, device)
+        if WL["kind"] == "selfsup":
+            result["roofline_photometric"] = roofline_photometric(args.batch, device)
+        else:
+            result["roofline_supervised"] = roofline_supervised(args.batch, device)
+        if args.workload == "kitti_selfsup":
+            result["roofline_plane_sweep"] = roofline_plane_sweep(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model)
     if rank == 0:

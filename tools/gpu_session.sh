@@ -40,6 +40,8 @@ for step in "$@"; do
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python bench.py --roofline-only &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python bench.py --roofline-only &&
          run pmc_traffic 60 python tools/pmc_traffic.py "$OUT" ;;
+    w:*) wl=${step#w:}; run "bench_$wl" 900 python bench.py --workload "$wl" --steps 10 --warmup 3 ;;
+    tprof) run torch_prof 600 python tools/torch_prof.py ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
