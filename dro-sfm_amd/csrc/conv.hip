@@ -155,9 +155,10 @@ struct RowDesc {
   bool M;
 };
 
-__device__ __forceinline__ RowDesc row_desc(int cb1, int cb2, int cb3, int ch, unsigned HW) {
+__device__ __forceinline__ RowDesc row_desc_at(KSlice base, int cb1, int cb2, int cb3, int ch,
+                                               unsigned HW) {
   const int si = (ch >= cb1) + (ch >= cb2) + (ch >= cb3);
-  const KSlice ks = kernarg_srcs() + si;
+  const KSlice ks = base + si;
   const int cl = ch - (si == 0 ? 0 : si == 1 ? cb1 : si == 2 ? cb2 : cb3);
   const int ctot = ks->ctot, coff = ks->coff, bc = ks->bcast;
   RowDesc d;
@@ -166,6 +167,10 @@ __device__ __forceinline__ RowDesc row_desc(int cb1, int cb2, int cb3, int ch, u
   d.Bc = bc ? (unsigned)(coff + cl) : (unsigned)(coff + cl) * HW;
   d.M = !bc;
   return d;
+}
+
+__device__ __forceinline__ RowDesc row_desc(int cb1, int cb2, int cb3, int ch, unsigned HW) {
+  return row_desc_at(kernarg_srcs(), cb1, cb2, cb3, ch, HW);
 }
 
 __device__ __forceinline__ void grad_put(float* dst, int ctot, int coff, int accf, int cl, int eb,
@@ -705,6 +710,41 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ batched weight gradient
+// One weight used by up to kMaxUse convolutions of a training step (the
+// recurrent update blocks apply every weight once per iteration): the weight
+// gradient of all uses is ONE launch whose pixel tiles run over
+// (use, image, tile).  Each use brings its own sources, output gradient and
+// saved activation output, read from this table in the kernel-argument
+// segment with a wave-uniform use index.
+constexpr int kMaxUse = 16;
+struct WgMulti {
+  IgArgs a;               // geometry, cbase, weight-gradient targets, plan (a.src = use 0)
+  int nuse;
+  int use_tiles;          // pixel tiles per use = B * tiles_img
+  Slice usrc[kMaxUse][kMaxSrc];
+  const float* uG[kMaxUse];
+  const float* uy[kMaxUse];
+};
+
+template <bool MULTI>
+struct WgParam {
+  typedef IgArgs T;
+  static __device__ __forceinline__ const IgArgs& ig(const IgArgs& x) { return x; }
+};
+template <>
+struct WgParam<true> {
+  typedef WgMulti T;
+  static __device__ __forceinline__ const IgArgs& ig(const WgMulti& x) { return x.a; }
+};
+
+typedef const float* FPtr;
+typedef __attribute__((address_space(4))) const FPtr* KFPtr;
+
+__device__ __forceinline__ __attribute__((address_space(4))) const char* kernarg_base() {
+  return (__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
 // ------------------------------------------------------------------ halo-tiled weight gradient
 // dW[o, c, tap] = sum_p G[o, p] X[c, p + d(tap)] for (KH, KW) in {1x5, 5x1, 3x3}:
 // block = 64 output channels x 32 input channels x all taps, K = the pixels of
@@ -731,8 +771,9 @@ struct HaloShapeW {
   static_assert(NJ <= 2 && TW % 2 == 0, "halo shape");
 };
 
-template <int KH, int KW, int GACT>
-__global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
+template <int KH, int KW, int GACT, bool MULTI>
+__global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>::T P) {
+  const IgArgs& a = WgParam<MULTI>::ig(P);
   using S = HaloShapeW<KH, KW>;
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
   constexpr int NJ = S::NJ, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE, TPW = S::TPW;
@@ -741,7 +782,6 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
   __shared__ float smem[S::LDS];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W, Cin = a.g.Cin, Cout = a.g.Cout;
-  const float* __restrict__ Gp = a.G;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x;
@@ -749,18 +789,27 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
   const int o0 = ot * 64, c0 = ct * BC;
   const size_t HW = (size_t)H * W;
   const unsigned HWu = (unsigned)HW;
-  const int ntiles = a.g.B * a.tiles_img;
+  int ntiles = a.g.B * a.tiles_img;
+  if constexpr (MULTI) ntiles = P.use_tiles * P.nuse;
   const int tbeg = blockIdx.y * a.chunks_per_split;
   const int tend = min(ntiles, tbeg + a.chunks_per_split);
   const bool do_bias = a.gbias && ct == 0;
-
-  const float* __restrict__ Yp = a.gy;
   const float galpha = a.galpha;
   float gr[16], yr[GACT ? 16 : 1], xr[8 * NJ], bsum[16];
   unsigned gmask = 0, xmask = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) bsum[j] = 0.f;
   auto load = [&](int tile) {
+    const float* __restrict__ Gp = a.G;
+    const float* __restrict__ Yp = a.gy;
+    KSlice sbase = kernarg_srcs();
+    if constexpr (MULTI) {   // wave-uniform use index: its sources, G and y from the kernarg table
+      const int u = tile / P.use_tiles;
+      tile -= u * P.use_tiles;
+      Gp = *(KFPtr)(kernarg_base() + offsetof(WgMulti, uG) + u * sizeof(FPtr));
+      if (GACT) Yp = *(KFPtr)(kernarg_base() + offsetof(WgMulti, uy) + u * sizeof(FPtr));
+      sbase = (KSlice)(kernarg_base() + offsetof(WgMulti, usrc)) + u * kMaxSrc;
+    }
     const int b = tile / a.tiles_img, trem = tile - b * a.tiles_img;
     const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
     // G tile: lane = pixel of the tile, wave w -> output channels o0 + 16w + j
@@ -784,8 +833,8 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
     for (int i = 0; i < 8; ++i) {
       const int ch = c0 + wave + 4 * i;          // scalar
       const bool real = ch < Cin;
-      const RowDesc d = row_desc(cb1, cb2, cb3, real ? ch : 0, HWu);
-      const unsigned sbase = (unsigned)b * d.A + d.Bc;
+      const RowDesc d = row_desc_at(sbase, cb1, cb2, cb3, real ? ch : 0, HWu);
+      const unsigned xbase = (unsigned)b * d.A + d.Bc;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int e = lane + 64 * j;
@@ -793,7 +842,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(IgArgs a) {
         const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
         const bool ok = real && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
         xmask |= ok ? (1u << (i * NJ + j)) : 0u;
-        xr[i * NJ + j] = d.p[ok ? sbase + (d.M ? (unsigned)(yy * W + xx) : 0u) : 0u];
+        xr[i * NJ + j] = d.p[ok ? xbase + (d.M ? (unsigned)(yy * W + xx) : 0u) : 0u];
       }
     }
   };
@@ -1471,7 +1520,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)wh.splits * Cout * a.g.Cin * T * sizeof(float)));
     const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
     const int gact = fold ? act : 0;
-#define DRO_WH(KH_, KW_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_>), grid, dim3(256), 0, s, a))
+#define DRO_WH(KH_, KW_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_, false>), grid, dim3(256), 0, s, a))
     if (KH == 1 && KW == 1) { DRO_WH(1, 1); }
     else if (KH == 1) { DRO_WH(1, 5); }
     else if (KW == 1) { DRO_WH(5, 1); }
@@ -1499,6 +1548,108 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     if ((st = launch_status("wgrad_finish_kernel launch failed"))) return st;
   }
   return DRO_OK;
+}
+
+// ------------------------------------------------------------------ batched weight gradient (host)
+// Split policy for a whole training step's uses of one weight: ~2 blocks per
+// CU, at least 4 pixel tiles per split, at most 64 splits.
+static WhPlan plan_wgrad_multi(int Cin, int Cout, int KH, int KW, int nuse, int B, int H, int W) {
+  WhPlan pl = plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W);
+  if (!pl.ok) return pl;
+  const int ntiles = nuse * B * pl.tiles_img;
+  const int blocks = pl.otiles * pl.ctiles;
+  int sp = (512 + blocks - 1) / blocks;
+  if (sp > 64) sp = 64;
+  if (sp > ntiles / 4) sp = ntiles / 4;
+  if (sp < 1) sp = 1;
+  pl.tiles_per_split = (ntiles + sp - 1) / sp;
+  pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
+  pl.part_bytes = align256((size_t)pl.splits * Cout * Cin * KH * KW * sizeof(float)) +
+                  align256((size_t)pl.splits * Cout * sizeof(float));
+  return pl;
+}
+
+extern "C" size_t dro_conv2d_weight_grad_multi_workspace_bytes(int nuse, int B, int H, int W, int Cin,
+                                                              int Cout, int KH, int KW) {
+  if (nuse < 1) nuse = 1;
+  return plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W).part_bytes;
+}
+
+extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse, int nsrc, int B, int H,
+                                            int W, int Cout, int KH, int KW, int act, float alpha,
+                                            float* grad_weight, float* grad_bias, int accumulate,
+                                            void* workspace, size_t workspace_bytes, void* stream) {
+  if (!uses || !grad_weight) {
+    set_error("conv2d_weight_grad_multi: NULL uses/grad_weight");
+    return DRO_E_NULL;
+  }
+  if (nuse < 1 || nuse > kMaxUse) {
+    set_error("conv2d_weight_grad_multi: need 1..16 uses per call");
+    return DRO_E_SHAPE;
+  }
+  if (act < 0 || act > 3) {
+    set_error("conv2d_weight_grad_multi: unknown activation");
+    return DRO_E_MODE;
+  }
+  WgMulti m = {};
+  int st;
+  for (int u = 0; u < nuse; ++u) {
+    IgArgs t = {};
+    if ((st = conv_setup_geom(t, uses[u].srcs, nsrc, B, H, W, Cout, KH, KW))) return st;
+    if (!uses[u].dout || (act != 0 && !uses[u].y)) {
+      set_error("conv2d_weight_grad_multi: NULL dout (or y with an activation)");
+      return DRO_E_NULL;
+    }
+    if (u == 0) {
+      m.a = t;
+    } else {
+      for (int i = 0; i < kMaxSrc; ++i)
+        if (t.cbase[i] != m.a.cbase[i]) {
+          set_error("conv2d_weight_grad_multi: uses split the input channels differently");
+          return DRO_E_SHAPE;
+        }
+    }
+    for (int i = 0; i < kMaxSrc; ++i) m.usrc[u][i] = t.src[i];
+    m.uG[u] = uses[u].dout;
+    m.uy[u] = act ? uses[u].y : nullptr;
+  }
+  const int Cin = m.a.g.Cin, T = KH * KW;
+  const WhPlan wh = plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W);
+  if (!wh.ok) {
+    set_error("conv2d_weight_grad_multi: kernel shape not supported (1x1, 1x5, 5x1, 3x3)");
+    return DRO_E_SHAPE;
+  }
+  if ((st = check_ws(workspace, workspace_bytes, wh.part_bytes, "conv2d_weight_grad_multi"))) return st;
+  IgArgs& a = m.a;
+  a.G = uses[0].dout;
+  a.gy = m.uy[0];
+  a.galpha = alpha;
+  a.gweight = grad_weight;
+  a.gbias = grad_bias;
+  a.wacc = accumulate ? 1 : 0;
+  a.otiles = wh.otiles;
+  a.tiles_x = wh.tiles_x;
+  a.tiles_img = wh.tiles_img;
+  a.chunks_per_split = wh.tiles_per_split;
+  char* ws = static_cast<char*>(workspace);
+  a.part = reinterpret_cast<float*>(ws);
+  a.bpart = reinterpret_cast<float*>(ws + align256((size_t)wh.splits * Cout * Cin * T * sizeof(float)));
+  m.nuse = nuse;
+  m.use_tiles = B * wh.tiles_img;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
+#define DRO_WHM(KH_, KW_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_, true>), grid, dim3(256), 0, s, m))
+  if (KH == 1 && KW == 1) { DRO_WHM(1, 1); }
+  else if (KH == 1) { DRO_WHM(1, 5); }
+  else if (KW == 1) { DRO_WHM(5, 1); }
+  else { DRO_WHM(3, 3); }
+#undef DRO_WHM
+  if ((st = launch_status("wgrad_halo_kernel<multi> launch failed"))) return st;
+  const long long total = (long long)Cout * Cin * T;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
+  return launch_status("wgrad_halo_finish_kernel launch failed");
 }
 
 // ------------------------------------------------------------------ SepConvGRU elementwise backward

@@ -58,6 +58,8 @@ def load():
     _sig(lib.dro_convgru_gates_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, Z, S)
     _sig(lib.dro_convgru_blend_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, Z, S)
     _sig(lib.dro_conv2d_backward, P, I, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, I, P, Z, S)
+    _sig(lib.dro_conv2d_weight_grad_multi_workspace_bytes, I, I, I, I, I, I, I, I, restype=Z)
+    _sig(lib.dro_conv2d_weight_grad_multi, P, I, I, I, I, I, I, I, I, I, F, P, P, I, P, Z, S)
     _sig(lib.dro_adam_step, P, P, P, P, ctypes.c_longlong, P, F, F, F, F, F, S)
     _sig(lib.dro_gru_backward_elem, I, I, I, I, I, P, P, P, P, P, P, P, P, S)
     _lib = lib
@@ -75,6 +77,7 @@ EXPORTED = (
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
+    "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",
     "dro_gru_backward_elem", "dro_adam_step",
 )
 

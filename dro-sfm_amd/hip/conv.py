@@ -22,6 +22,13 @@ the data-gradient chain: set_weight_grad_stream); autograd receives None for
 the parameters, and a side stream is joined into the caller's stream at the end
 of backward (engine final callback).  Fused weights (z|r gates, shared-input heads) are then
 views of the flat parameter buffer instead of per-forward concatenations.
+
+Batched weight gradients (direct path, default on): the recurrent update
+blocks apply every weight once per iteration, so instead of one weight-gradient
+launch + one split reduction per use, each use is queued (sources, output
+gradient, saved output kept alive) and all uses of a weight are reduced by ONE
+dro_conv2d_weight_grad_multi launch at the end of backward (engine final
+callback, before the trainer's gradient all-reduce).  set_batched_weight_grads.
 """
 import contextlib
 import ctypes
@@ -204,6 +211,73 @@ def _grad_buffers(scope, key, weight, nbias, device):
     return ent[0], ent[1], 1, False
 
 
+class DroWgradUse(ctypes.Structure):
+    _fields_ = [("srcs", ctypes.c_void_p), ("dout", ctypes.c_void_p), ("y", ctypes.c_void_p)]
+
+
+_BATCH = [True]
+_PENDING = {}
+_PENDING_CB = [False]
+_MULTI_SHAPES = {(1, 1), (1, 5), (5, 1), (3, 3)}
+_MAX_USES = 16
+
+
+def set_batched_weight_grads(enabled):
+    """Batch the direct-path weight gradients of each weight over a backward
+    pass (True, default) or launch them per use (False, A/B runs)."""
+    _BATCH[0] = bool(enabled)
+
+
+def _queue_weight_grad(srcs, wshape, act, alpha, dout, y, gw, gb):
+    """Queue one use's weight(+bias) gradient for the end-of-backward batch;
+    False when this conv shape is not batched (the caller launches it)."""
+    Cout, Cin, KH, KW = wshape
+    if not _BATCH[0] or (KH, KW) not in _MULTI_SHAPES:
+        return False
+    B, _, H, W = srcs[0].shape
+    key = (gw.data_ptr(), gb.data_ptr() if gb is not None else 0, B, H, W, act, float(alpha),
+           tuple(t.shape[1] for t in srcs))
+    ent = _PENDING.get(key)
+    if ent is None:
+        ent = _PENDING[key] = ((B, H, W, Cin, Cout, KH, KW, act, float(alpha), gw, gb, len(srcs)), [])
+    ent[1].append((list(srcs), dout, y))
+    if not _PENDING_CB[0]:
+        _PENDING_CB[0] = True
+        stream = torch.cuda.current_stream()
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: flush_weight_grads(stream))
+    return True
+
+
+def flush_weight_grads(stream=None):
+    """Launch every queued weight gradient (one launch + one reduction per
+    weight per 16 uses), in first-use order; releases the kept tensors."""
+    _PENDING_CB[0] = False
+    if not _PENDING:
+        return
+    lib = _lib.load()
+    items = list(_PENDING.values())
+    _PENDING.clear()
+    stream = stream or torch.cuda.current_stream()
+    with torch.cuda.stream(stream):
+        for meta, uses in items:
+            B, H, W, Cin, Cout, KH, KW, act, alpha, gw, gb, nsrc = meta
+            for c0 in range(0, len(uses), _MAX_USES):
+                chunk = uses[c0:c0 + _MAX_USES]
+                n = len(chunk)
+                sl = [_slices(srcs) for srcs, _, _ in chunk]
+                arr = (DroWgradUse * n)()
+                for i, (_, dout, y) in enumerate(chunk):
+                    arr[i].srcs = ctypes.cast(sl[i], ctypes.c_void_p)
+                    arr[i].dout = dout.data_ptr()
+                    arr[i].y = y.data_ptr() if y is not None else None
+                nb = int(lib.dro_conv2d_weight_grad_multi_workspace_bytes(n, B, H, W, Cin, Cout, KH, KW))
+                ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=gw.device)
+                check(lib.dro_conv2d_weight_grad_multi(arr, n, nsrc, B, H, W, Cout, KH, KW, act,
+                                                       ctypes.c_float(alpha), ptr(gw), ptr(gb), 1,
+                                                       ptr(ws), nb, stream_of(gw)),
+                      "dro_conv2d_weight_grad_multi")
+
+
 _WS = {}
 
 
@@ -267,6 +341,8 @@ class _Conv2d(torch.autograd.Function):
                                               act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
                                               ptr(gout), ptrs, ctot, coff, acc, None, None, 0, ptr(ws), nws,
                                               stream_of(gout)), "dro_conv2d_backward(data)")
+            if _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None):
+                return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
             side = _fork_side()
             _on_side(side, [gout, y, weight, *srcs])
             with torch.cuda.stream(side):
@@ -424,14 +500,16 @@ class _SepGRUHalf(torch.autograd.Function):
         check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
                                       None, None, 0, ptr(ws), nws, st), "dro_conv2d_backward(q data)")
-        side = _fork_side()                       # dq and r*h are final here
-        _on_side(side, [dq, rh, wq, *xs])
-        with torch.cuda.stream(side):
-            wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-            check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
-                                          0, ctypes.c_float(1.0), None, ptr(dq), None, None, None, None,
-                                          ptr(gwq), ptr(gbq), 1, ptr(wsw), nwsw, stream_of(h)),
-                  "dro_conv2d_backward(q weight)")
+        batched = _queue_weight_grad([rh, *xs], wq.shape, 0, 1.0, dq, None, gwq, gbq)
+        side = main if batched else _fork_side()  # dq and r*h are final here
+        _on_side(side, [] if batched else [dq, rh, wq, *xs])
+        with torch.cuda.stream(side) if not batched else contextlib.nullcontext():
+            if not batched:
+                wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
+                check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
+                                              0, ctypes.c_float(1.0), None, ptr(dq), None, None, None,
+                                              None, ptr(gwq), ptr(gbq), 1, ptr(wsw), nwsw, stream_of(h)),
+                      "dro_conv2d_backward(q weight)")
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
         ptrs, ctot, coff = _grad_targets([dh, *dxs])
@@ -440,6 +518,9 @@ class _SepGRUHalf(torch.autograd.Function):
         check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
                                       None, None, 0, ptr(ws), nws, st), "dro_conv2d_backward(zr data)")
+        if _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
+            need = ctx.needs_input_grad
+            return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
         if side is not main:
             side.wait_stream(main)                # dz|dr are final after stage 2
         _on_side(side, [dzr, h, wzr])

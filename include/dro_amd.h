@@ -249,6 +249,28 @@ int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, in
                         float* grad_bias, int grad_weight_accumulate, void* workspace,
                         size_t workspace_bytes, void* stream);
 
+/* Weight (+ bias) gradient of ONE weight over several convolutions that use it
+ * (the recurrent update blocks apply each weight once per iteration): one
+ * launch (+ one split reduction) for all uses instead of one pair per use.
+ * Every use has the same geometry and channel split (nsrc slices); act/alpha
+ * as in dro_conv2d_forward (the activation derivative is taken from each use's
+ * saved output y).  grad_weight [Cout][Cin][KH][KW] / grad_bias [Cout]
+ * (nullable) are overwritten or, with accumulate, added to.  1 <= nuse <= 16;
+ * kernel shapes 1x1, 1x5, 5x1, 3x3.  Deterministic (fixed reduction order). */
+typedef struct dro_wgrad_use {
+  const dro_slice* srcs;  /* the nsrc input slices of this use */
+  const float* dout;      /* dense [B,Cout,H,W] gradient w.r.t. this use's output */
+  const float* y;         /* dense [B,Cout,H,W] saved output (act != 0), else NULL */
+} dro_wgrad_use;
+
+size_t dro_conv2d_weight_grad_multi_workspace_bytes(int nuse, int B, int H, int W, int Cin, int Cout,
+                                                    int KH, int KW);
+
+int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse, int nsrc, int B, int H, int W,
+                                 int Cout, int KH, int KW, int act, float alpha, float* grad_weight,
+                                 float* grad_bias, int accumulate, void* workspace,
+                                 size_t workspace_bytes, void* stream);
+
 /* SepConvGRU backward, elementwise parts (update.py:67-70): with zr the saved
  * sigmoid gates [B,2hd,H,W] (z first), q the saved candidate [B,hd,H,W].
  * Outputs are gradients w.r.t. the gates' PRE-activations (feed them to

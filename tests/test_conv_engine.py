@@ -176,3 +176,96 @@ def test_weight_grad_scope_matches_autograd(hip):
     ref, got = run(False), run(True)
     for i, (a, r) in enumerate(zip(got, ref)):
         assert rel(a, r) < 1e-5, f"param {i}"
+
+
+MULTI_CASES = [
+    # (sources [(kind, C)], Cout, (KH, KW), act, alpha, uses, B, H, W)
+    ([("dense", 64), ("dense", 32), ("dense", 63), ("dense", 1)], 128, (1, 5), None, 1.0, 8, 2, 24, 80),
+    ([("dense", 64), ("slice", 32), ("dense", 58), ("bcast", 6)], 64, (5, 1), None, 1.0, 3, 4, 24, 80),
+    ([("slice", 64)], 96, (3, 3), "relu", 1.0, 5, 2, 24, 80),
+    ([("dense", 128)], 6, (3, 3), "tanh", 1.0, 17, 2, 12, 20),
+    ([("slice", 128)], 576, (1, 1), None, 0.25, 4, 2, 24, 80),
+    ([("dense", 37), ("slice", 11)], 45, (3, 3), "sigmoid", 1.0, 2, 3, 7, 13),
+]
+
+
+@pytest.mark.parametrize("case", range(len(MULTI_CASES)))
+def test_weight_grad_multi(hip, case):
+    """dro_conv2d_weight_grad_multi: the weight + bias gradient of ONE weight over
+    several uses (own sources, output gradients and saved outputs) in one
+    launch, accumulated onto the existing gradient, equals the fp64 sum of the
+    per-use autograd gradients (more than 16 uses: chunked by the caller)."""
+    import ctypes
+    from dro_sfm_amd.hip import _lib
+    from dro_sfm_amd.hip.conv import DroWgradUse, _slices
+    lib = _lib.load()
+    spec, Cout, (KH, KW), act, alpha, uses, B, H, W = MULTI_CASES[case]
+    g = torch.Generator().manual_seed(100 + case)
+    Cin = sum(c for _, c in spec)
+    w = 0.1 * torch.randn(Cout, Cin, KH, KW, generator=g)
+    b = 0.1 * torch.randn(Cout, generator=g)
+    gw_ref = torch.zeros(Cout, Cin, KH, KW, dtype=torch.float64)
+    gb_ref = torch.zeros(Cout, dtype=torch.float64)
+    dev_uses = []
+    for _ in range(uses):
+        bases, views = zip(*[make_src(k, B, c, H, W, g) for k, c in spec])
+        dout = torch.randn(B, Cout, H, W, generator=g)
+        wd = w.double().requires_grad_(True)
+        bd = b.double().requires_grad_(True)
+        x = torch.cat([v(t.double()) for v, t in zip(views, bases)], 1)
+        y = alpha * ACTS[act](F.conv2d(x, wd, bd, padding=(KH // 2, KW // 2)))
+        (y * dout.double()).sum().backward()
+        gw_ref += wd.grad
+        gb_ref += bd.grad
+        srcs = [v(t.to(DEV)) for v, t in zip(views, bases)]
+        dev_uses.append((srcs, dout.to(DEV), y.detach().float().to(DEV) if act else None))
+    init_w = torch.randn(Cout, Cin, KH, KW, generator=g)
+    init_b = torch.randn(Cout, generator=g)
+    gw, gb = init_w.to(DEV), init_b.to(DEV)
+    keep = []
+    for c0 in range(0, uses, 16):
+        chunk = dev_uses[c0:c0 + 16]
+        arr = (DroWgradUse * len(chunk))()
+        for i, (srcs, dout, y) in enumerate(chunk):
+            sl = _slices(srcs)
+            keep.append(sl)
+            arr[i].srcs = ctypes.cast(sl, ctypes.c_void_p)
+            arr[i].dout = dout.data_ptr()
+            arr[i].y = y.data_ptr() if y is not None else None
+        nb = lib.dro_conv2d_weight_grad_multi_workspace_bytes(len(chunk), B, H, W, Cin, Cout, KH, KW)
+        ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+        st = lib.dro_conv2d_weight_grad_multi(arr, len(chunk), len(spec), B, H, W, Cout, KH, KW,
+                                              {None: 0, "relu": 1, "sigmoid": 2, "tanh": 3}[act],
+                                              ctypes.c_float(alpha), gw.data_ptr(), gb.data_ptr(), 1,
+                                              ws.data_ptr(), nb, None)
+        assert st == 0, lib.dro_last_error()
+    torch.cuda.synchronize()
+    assert rel(gw - init_w.to(DEV), gw_ref) < TOL
+    assert rel(gb - init_b.to(DEV), gb_ref) < TOL
+
+
+def test_weight_grad_multi_rejects(hip):
+    import ctypes
+    from dro_sfm_amd.hip import _lib
+    from dro_sfm_amd.hip.conv import DroWgradUse, _slices
+    lib = _lib.load()
+    B, H, W = 1, 8, 8
+    x1 = torch.randn(B, 8, H, W, device=DEV)
+    a, b_ = torch.randn(B, 3, H, W, device=DEV), torch.randn(B, 5, H, W, device=DEV)
+    dout = torch.randn(B, 4, H, W, device=DEV)
+    gw = torch.zeros(4, 8, 3, 3, device=DEV)
+    s1, s2 = _slices([x1]), _slices([a, b_])
+    arr = (DroWgradUse * 17)()
+    for i in range(17):
+        arr[i].srcs = ctypes.cast(s1, ctypes.c_void_p)
+        arr[i].dout = dout.data_ptr()
+    args = (B, H, W, 4, 3, 3, 0, ctypes.c_float(1.0), gw.data_ptr(), None, 1, None, 0, None)
+    assert lib.dro_conv2d_weight_grad_multi(arr, 17, 1, *args) == -2          # > 16 uses
+    assert lib.dro_conv2d_weight_grad_multi(arr, 1, 1, B, H, W, 4, 7, 7, 0, ctypes.c_float(1.0),
+                                            gw.data_ptr(), None, 1, None, 0, None) == -2   # 7x7
+    two = (DroWgradUse * 2)()
+    two[0].srcs, two[0].dout = ctypes.cast(s2, ctypes.c_void_p), dout.data_ptr()
+    two[1].srcs, two[1].dout = ctypes.cast(s2, ctypes.c_void_p), dout.data_ptr()
+    assert lib.dro_conv2d_weight_grad_multi(two, 2, 2, *args) == -1           # no workspace
+    assert lib.dro_conv2d_weight_grad_multi(arr, 1, 1, B, H, W, 4, 3, 3, 1, ctypes.c_float(1.0),
+                                            gw.data_ptr(), None, 1, None, 0, None) == -1   # relu, no y

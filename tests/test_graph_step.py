@@ -88,18 +88,22 @@ def test_direct_weight_grads_match_autograd_path():
     out = {}
     try:
         with torch.backends.cudnn.flags(enabled=False):
-            for direct in (False, True):
+            # autograd path; direct per use; direct batched over the backward pass
+            for mode, (direct, batched) in enumerate(((False, False), (True, False), (True, True))):
                 hc.set_direct_weight_grads(direct)
+                hc.set_batched_weight_grads(batched)
                 m = _setup()
                 tr = DataParallelTrainer(m)
                 batch["intrinsics"].copy_(K0)
                 loss = tr.step(batch, flip=False)[0].clone()
                 torch.cuda.synchronize()
                 used = sum(bool(getattr(p, "_dro_direct_used", False)) for p in m.parameters())
-                out[direct] = (loss, tr.grads.flat.clone(), used)
+                out[mode] = (loss, tr.grads.flat.clone(), used)
     finally:
         hc.set_direct_weight_grads(True)
-    (l0, g0, u0), (l1, g1, u1) = out[False], out[True]
-    assert u0 == 0 and u1 > 20
-    assert O.rel_err(l1.cpu(), l0.cpu()) < 1e-6
+        hc.set_batched_weight_grads(True)
+    (l0, g0, u0), (l1, g1, u1), (l2, g2, u2) = out[0], out[1], out[2]
+    assert u0 == 0 and u1 > 20 and u2 == u1
+    assert O.rel_err(l1.cpu(), l0.cpu()) < 1e-6 and O.rel_err(l2.cpu(), l0.cpu()) < 1e-6
     assert float((g1 - g0).norm() / g0.norm()) < 1e-4
+    assert float((g2 - g0).norm() / g0.norm()) < 1e-4
