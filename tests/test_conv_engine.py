@@ -266,6 +266,6 @@ def test_weight_grad_multi_rejects(hip):
     two = (DroWgradUse * 2)()
     two[0].srcs, two[0].dout = ctypes.cast(s2, ctypes.c_void_p), dout.data_ptr()
     two[1].srcs, two[1].dout = ctypes.cast(s2, ctypes.c_void_p), dout.data_ptr()
-    assert lib.dro_conv2d_weight_grad_multi(two, 2, 2, *args) == -1           # no workspace
+    assert lib.dro_conv2d_weight_grad_multi(two, 2, 2, *args) == -2           # no workspace
     assert lib.dro_conv2d_weight_grad_multi(arr, 1, 1, B, H, W, 4, 3, 3, 1, ctypes.c_float(1.0),
                                             gw.data_ptr(), None, 1, None, 0, None) == -1   # relu, no y
