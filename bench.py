@@ -232,10 +232,9 @@ def roofline_supervised(B, device, n=4, iters=20):
             "algorithmic_bytes": int(nbytes), "fwd_bwd_ms": round(ms, 4)}
 
 
-ROOFLINE_KERNEL = "dconv_kernel<32, 1, 5, 0, 2, 2>"
-ROOFLINE_FINISH = "igemm_finish_kernel<0, 2, 2>"
 # HBM bytes per launch of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-# passes (tools/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
+# passes (tools/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md); used only
+# when the file was measured on the same kernel(s) this build launches
 def _latest_traffic_file():
     import glob
     import re
@@ -246,6 +245,27 @@ def _latest_traffic_file():
 
 
 TRAFFIC_FILE = _latest_traffic_file()
+# the roofline conv: depth SepConvGRU z|r gate forward at the KITTI metric shape
+RF_B, RF_HD, RF_H, RF_W, RF_CIN, RF_KH, RF_KW = 2, 64, 192 // 8, 640 // 8, 160, 1, 5
+
+
+def roofline_kernels():
+    """Names of the kernels one roofline call launches, from the engine's own
+    launch plan (dro_conv2d_plan): the halo conv and, with a K split over
+    blocks, its finish kernel."""
+    import ctypes
+    from dro_sfm_amd.hip import _lib
+    lib = _lib.load()
+    info = (ctypes.c_longlong * 16)()
+    _lib.check(lib.dro_conv2d_plan(2 * RF_HD, RF_CIN, RF_KH, RF_KW, RF_B, RF_H, RF_W, info),
+               "dro_conv2d_plan")
+    bm, ks, kin = int(info[1]), int(info[4]), int(info[15])
+    names = [f"dconv_kernel<{bm}, {RF_KH}, {RF_KW}, 0, 2, 2, {kin}>"]
+    if ks > 1:
+        names.append("igemm_finish_kernel<0, 2, 2>")
+    return names, ks, kin
+
+
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_32x32x2_f32)
 
 
@@ -264,8 +284,8 @@ def roofline_conv(device, iters=50, traffic_file=None):
     from dro_sfm_amd.hip import _lib
     from dro_sfm_amd.hip.conv import _slices, _workspace
     lib = _lib.load()
-    # fixed at the metric's (KITTI 192x640, configs[1]) shape whatever --workload is
-    B, hd, Hf, Wf, cin, KH, KW = 2, 64, 192 // 8, 640 // 8, 160, 1, 5
+    B, hd, Hf, Wf, cin, KH, KW = RF_B, RF_HD, RF_H, RF_W, RF_CIN, RF_KH, RF_KW
+    kernels, ks, kin = roofline_kernels()
     g = torch.Generator(device=device)
     g.manual_seed(11)
     h = torch.randn(B, hd, Hf, Wf, generator=g, device=device).tanh()
@@ -295,17 +315,17 @@ def roofline_conv(device, iters=50, traffic_file=None):
     us = e0.elapsed_time(e1) * 1e3 / iters
     flops = 2.0 * 2 * hd * cin * KH * KW * B * Hf * Wf
     achieved = flops / (us * 1e-6) / 1e12
-    info = (ctypes.c_longlong * 16)()
-    _lib.check(lib.dro_conv2d_plan(2 * hd, cin, KH, KW, B, Hf, Wf, info), "dro_conv2d_plan")
     traffic = None
     if traffic_file and os.path.exists(traffic_file):
         with open(traffic_file) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
-    return {"bound": "mfma", "kernel": f"{ROOFLINE_KERNEL} + {ROOFLINE_FINISH} (SepConvGRU z|r gates "
-            f"fwd, B=2 24x80 Cin 160 Cout 128 1x5)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
+            tf = json.load(f)
+        if tf.get("kernels") == kernels:       # measured on this very launch sequence
+            traffic = tf.get("hbm_bytes_per_launch")
+    return {"bound": "mfma", "kernel": " + ".join(kernels) + " (SepConvGRU z|r gates fwd, B=2 24x80 "
+            "Cin 160 Cout 128 1x5)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
             "flops_per_launch": int(flops), "avg_launch_us": round(us, 2), "launches": iters,
-            "split_k": int(info[4])}
+            "split_k_blocks": ks, "split_k_waves": kin}
 
 
 # ----------------------------------------------------------------------------- CPU baseline

@@ -392,24 +392,31 @@ struct HaloShape {
   static_assert(NJ <= 4 && WPER <= 16 && CK % 4 == 0 && TH * TW == 64, "halo shape");
 };
 
-template <int BM, int KH, int KW, int MODE, int ACT, int EPI>
-__global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
+// KS > 1: intra-block K split.  The block is KS groups of 4 waves; group g
+// stages and multiplies chunks g, g+KS, ... in its own LDS region, and the
+// groups' accumulators are summed in group order at the end (more waves per
+// tile to hide the staging latency, no split-K partials or finish launch).
+template <int BM, int KH, int KW, int MODE, int ACT, int EPI, int KS>
+__global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   using S = HaloShape<BM, KH, KW>;
+  static_assert(KS == 1 || S::LDS >= 4 * 16 * 64, "cross-group reduction area");
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
   constexpr int CK = S::CK, NJ = S::NJ, XPER = CK / 4;
   constexpr int RUN = MODE == 0 ? S::RUN0 : S::RUN1, WS = MODE == 0 ? S::WS0 : S::WS1;
   constexpr int WSZ = MODE == 0 ? S::WSZ0 : S::WSZ1, STAGE = S::STAGE;
   constexpr int WM = BM / 32;
   constexpr int PH = KH / 2, PW = KW / 2;
-  __shared__ float smem[S::LDS];
+  __shared__ float smem_all[KS * S::LDS];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W;
   const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch;
   const int CinT = Cin * T;
   const float* __restrict__ Wt = a.weight;
   const float* __restrict__ Gp = a.G;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar)
+  const int tid = threadIdx.x & 255, lane = tid & 63;
+  const int grp = KS == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave in the group (scalar)
+  float* smem = smem_all + grp * S::LDS;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
   const int row0 = rt * BM;
@@ -522,33 +529,39 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  if (cbeg < cend) {
-    load(cbeg);
+  // group grp handles chunks cbeg + grp, cbeg + grp + KS, ...; every group
+  // runs the same number of iterations (barriers are block wide)
+  const int nit = (cend - cbeg + KS - 1) / KS;
+  if (cbeg + grp < cend) {
+    load(cbeg + grp);
     store(0);
   }
   __syncthreads();
-  for (int c = cbeg; c < cend; ++c) {
-    const int buf = (c - cbeg) & 1;
-    const bool more = c + 1 < cend;
-    if (more) load(c + 1);
-    const float* wa = smem + buf * STAGE + abase;
-    const float* xb = smem + buf * STAGE + WSZ + bbase;
+  for (int it = 0; it < nit; ++it) {
+    const int c = cbeg + it * KS + grp;
+    const int buf = it & 1;
+    const bool more = c + KS < cend;
+    if (more) load(c + KS);
+    if (KS == 1 || c < cend) {
+      const float* wa = smem + buf * STAGE + abase;
+      const float* xb = smem + buf * STAGE + WSZ + bbase;
 #pragma unroll
-    for (int ty = 0; ty < KH; ++ty) {
+      for (int ty = 0; ty < KH; ++ty) {
 #pragma unroll
-      for (int tx = 0; tx < KW; ++tx) {
-        constexpr int dummy = 0;
-        (void)dummy;
-        const int tap = ty * KW + tx;
-        const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
+        for (int tx = 0; tx < KW; ++tx) {
+          const int tap = ty * KW + tx;
+          const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
-          acc = mfma32(wa[tap + s * ASTEP], xb[toff + 2 * s * HPAD], acc);
+          for (int s = 0; s < NS; ++s)
+            acc = mfma32(wa[tap + s * ASTEP], xb[toff + 2 * s * HPAD], acc);
+        }
       }
     }
     if (more) store(buf ^ 1);
     __syncthreads();
   }
+  // reductions in a fixed order, every wave still resident (barriers below)
+  const bool holder = WM == 2 || wk == 0;
   if (WM == 1) {   // sum the two channel halves (LDS reused after the final barrier)
     float* red = smem;   // [2 pixel halves][16][64]
     if (wk == 1) {
@@ -556,10 +569,27 @@ __global__ __launch_bounds__(256) void dconv_kernel(IgArgs a) {
       for (int r = 0; r < 16; ++r) red[(wc * 16 + r) * 64 + lane] = acc[r];
     }
     __syncthreads();
-    if (wk == 1) return;
+    if (wk == 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] += red[(wc * 16 + r) * 64 + lane];
+      for (int r = 0; r < 16; ++r) acc[r] += red[(wc * 16 + r) * 64 + lane];
+    }
   }
+  if (KS > 1) {    // groups 1..KS-1 park their sums; group 0 adds them in group order
+    __syncthreads();
+    if (grp > 0 && holder) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) smem[(wave * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (grp == 0 && holder) {
+      for (int g = 1; g < KS; ++g) {
+        const float* red = smem_all + g * S::LDS;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += red[(wave * 16 + r) * 64 + lane];
+      }
+    }
+  }
+  if (grp > 0 || !holder) return;
 
   const int oy = ty0 + qy, ox = tx0 + qx;
   if (oy >= H || ox >= W) return;
@@ -1025,6 +1055,7 @@ size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 struct IgPlan {
   bool halo;
   int bm, row_tiles, ptiles, ksplit, chunks_per_split;
+  int kin;                // intra-block K split (wave groups per tile; halo kernels)
   int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
   size_t lds_bytes;
   size_t part_bytes;
@@ -1071,11 +1102,17 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
   }
   const int nchunks = (kch + pl.CK - 1) / pl.CK;
   const long long blocks = (long long)pl.row_tiles * pl.ptiles;
+  // K split inside the block first (4 or 2 wave groups per tile: no partials,
+  // no finish launch), over blocks only when the grid is still very short
+  int kin = blocks < 256 ? 4 : (blocks < 512 ? 2 : 1);
+  while (kin > 1 && kin > nchunks) kin >>= 1;
+  pl.kin = kin;
   int ks = 1;
-  if (blocks < 480) {   // split K over blocks (one chunk minimum per split)
-    ks = (int)((480 + blocks - 1) / blocks);
+  if (blocks < 120) {
+    ks = (int)((480 + blocks * kin - 1) / (blocks * kin));
     if (ks > 16) ks = 16;
-    if (ks > nchunks) ks = nchunks;
+    if (ks > nchunks / kin) ks = nchunks / kin;
+    if (ks < 1) ks = 1;
   }
   pl.chunks_per_split = (nchunks + ks - 1) / ks;
   pl.ksplit = (nchunks + pl.chunks_per_split - 1) / pl.chunks_per_split;
@@ -1089,6 +1126,7 @@ IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W) {
   const int T = KH * KW;
   const long long P = (long long)B * H * W;
   pl.halo = false;
+  pl.kin = 1;
   pl.ptiles = (int)((P + kBN - 1) / kBN);
   const int t64 = (rows + 63) / 64;
   pl.bm = (long long)t64 * pl.ptiles >= 448 ? 64 : 32;
@@ -1267,8 +1305,15 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.CK = pl.CK;
     const int KH = a.g.KH;
     const int KW = a.g.KW;
-#define DRO_DCONV(BM_, KH_, KW_) \
-    hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI>), grid, dim3(256), 0, s, a)
+#define DRO_DCONV(BM_, KH_, KW_)                                                                    \
+    do {                                                                                            \
+      if (pl.kin == 4)                                                                              \
+        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 4>), grid, dim3(1024), 0, s, a); \
+      else if (pl.kin == 2)                                                                         \
+        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 2>), grid, dim3(512), 0, s, a);  \
+      else                                                                                          \
+        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 1>), grid, dim3(256), 0, s, a);  \
+    } while (0)
     if (pl.bm == 32) {
       if (KH == 1 && KW == 1) DRO_DCONV(32, 1, 1);
       else if (KH == 1) DRO_DCONV(32, 1, 5);
@@ -1328,7 +1373,7 @@ extern "C" int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, 
   const IgPlan pl = plan_igemm(rows, kch, KH, KW, B, H, W);
   const long long v[16] = {pl.halo, pl.bm, pl.row_tiles, pl.ptiles, pl.ksplit, pl.chunks_per_split,
                            pl.TH, pl.TW, pl.HWd, pl.HPAD, pl.tiles_x, pl.tiles_img, pl.CK,
-                           (long long)pl.lds_bytes, (long long)pl.part_bytes, 0};
+                           (long long)pl.lds_bytes, (long long)pl.part_bytes, pl.kin};
   for (int i = 0; i < 16; ++i) info[i] = v[i];
   return DRO_OK;
 }

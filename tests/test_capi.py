@@ -107,8 +107,9 @@ def test_conv_plans_within_kernel_limits(lib):
         for B, H, W in IMAGES:
             for rows, kch in ((Cout, Cin), (Cin, Cout)):
                 assert lib.dro_conv2d_plan(rows, kch, KH, KW, B, H, W, info) == 0
-                halo, bm, rt, pt, ks, cps, TH, TW, HWd, HPAD, tx, timg, CK, lds, part, _ = list(info)
+                halo, bm, rt, pt, ks, cps, TH, TW, HWd, HPAD, tx, timg, CK, lds, part, kin = list(info)
                 assert bm in (32, 64) and rt * bm >= rows and ks >= 1 and cps >= 1
+                assert kin in (1, 2, 4) and (halo or kin == 1)
                 assert bool(halo) == ((KH, KW) in ((1, 5), (5, 1), (3, 3), (1, 1)))
                 if not halo:
                     continue
@@ -121,6 +122,9 @@ def test_conv_plans_within_kernel_limits(lib):
                 odd = lambda n: n | 1
                 stage = max(bm * odd(CK * T), CK * odd(bm * T)) + CK * HPAD
                 assert lds == max(2 * stage * 4, 2 * 16 * 64 * 4) <= 64 * 1024
+                # kin wave groups: one LDS region each (<= 160 KiB per block), and
+                # room for the cross-group reduction (4 waves x 16 x 64 floats)
+                assert lds * kin <= 160 * 1024 and (kin == 1 or lds >= 4 * 16 * 64 * 4)
                 assert tx == -(-W // TW) and timg == -(-H // TH) * tx and pt == B * timg
                 nck = -(-kch // CK)
                 assert cps * ks >= nck and cps * (ks - 1) < nck

@@ -15,7 +15,10 @@ import json
 import os
 import sys
 
-KERNELS = ("dconv_kernel<32, 1, 5, 0, 2, 2>", "igemm_finish_kernel<0, 2, 2>")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+KERNELS = tuple(bench.roofline_kernels()[0])
 
 
 def per_launch(d, counter):
@@ -45,7 +48,7 @@ def main():
     res = {"kernels": list(KERNELS), "fetch_size_kb_per_launch": fkb, "write_size_kb_per_launch": wkb,
            "fetch_bytes_corrected": 2 * fkb * 1024, "write_bytes": wkb * 1024,
            "hbm_bytes_per_launch": int(2 * fkb * 1024 + wkb * 1024), "launches": [nf, nw],
-           "unit": "per call (dconv + finish launch pair)",
+           "unit": "per call (every kernel the call launches)",
            "per_kernel_kb": [fmed, wmed],
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                      "`bench.py --roofline-only`; FETCH_SIZE x2 (gfx950 correction)"}
