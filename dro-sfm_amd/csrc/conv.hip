@@ -451,33 +451,10 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   unsigned xmask = 0;
   auto load = [&](int chunk) {
     const int c0 = chunk * CK;
-    xmask = 0;
-#pragma unroll
-    for (int i = 0; i < XPER; ++i) {
-      const int ch = c0 + wave + 4 * i;          // scalar
-      const bool chok = ch < kch;
-      const float* p;
-      unsigned sbase;
-      bool M;
-      if (MODE == 0) {
-        const RowDesc d = row_desc(cb1, cb2, cb3, chok ? ch : 0, HWu);
-        p = d.p;
-        sbase = (unsigned)b * d.A + d.Bc;
-        M = d.M;
-      } else {
-        p = Gp;
-        sbase = ((unsigned)b * (unsigned)Cout + (unsigned)(chok ? ch : 0)) * HWu;
-        M = true;
-      }
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const bool ok = chok && ((xok >> j) & 1u);
-        xmask |= ok ? (1u << (i * NJ + j)) : 0u;
-        const unsigned off = ok ? sbase + (M ? (unsigned)xpix[j] : 0u) : 0u;
-        xr[i * NJ + j] = p[off];
-        if (FOLD) yr[i * NJ + j] = Yp[off];
-      }
-    }
+    // weights first (no descriptor needed), then every channel's source
+    // descriptor (independent scalar loads, one wait), then the input patch:
+    // decoding a descriptor next to its own loads serialised the chunk on one
+    // scalar round trip per channel
     const unsigned gbase = MODE == 0 ? (unsigned)row0 * CinT + (unsigned)c0 * T
                                      : (unsigned)c0 * CinT + (unsigned)row0 * T;
 #pragma unroll
@@ -486,6 +463,36 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       const int run = e / RUN, rem = e - run * RUN;
       const unsigned g = gbase + (unsigned)run * CinT + (unsigned)rem;
       wv[i] = Wt[g < wlast ? g : wlast];
+    }
+    const float* ps[XPER];
+    unsigned sb[XPER];
+    bool Ms[XPER], cok[XPER];
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int ch = c0 + wave + 4 * i;          // scalar
+      cok[i] = ch < kch;
+      if (MODE == 0) {
+        const RowDesc d = row_desc(cb1, cb2, cb3, cok[i] ? ch : 0, HWu);
+        ps[i] = d.p;
+        sb[i] = (unsigned)b * d.A + d.Bc;
+        Ms[i] = d.M;
+      } else {
+        ps[i] = Gp;
+        sb[i] = ((unsigned)b * (unsigned)Cout + (unsigned)(cok[i] ? ch : 0)) * HWu;
+        Ms[i] = true;
+      }
+    }
+    xmask = 0;
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bool ok = cok[i] && ((xok >> j) & 1u);
+        xmask |= ok ? (1u << (i * NJ + j)) : 0u;
+        const unsigned off = ok ? sb[i] + (Ms[i] ? (unsigned)xpix[j] : 0u) : 0u;
+        xr[i * NJ + j] = ps[i][off];
+        if (FOLD) yr[i * NJ + j] = Yp[off];
+      }
     }
   };
   auto store = [&](int buf) {
@@ -858,21 +865,28 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
       if (GACT) yr[j] = Yp[off];
     }
     // X patch: wave w -> channels c0 + w + 4i, lanes over the halo
-    xmask = 0;
+    // every channel's descriptor first (independent scalar loads, one wait),
+    // then the patch loads
+    RowDesc ds[8];
+    bool real[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int ch = c0 + wave + 4 * i;          // scalar
-      const bool real = ch < Cin;
-      const RowDesc d = row_desc_at(sbase, cb1, cb2, cb3, real ? ch : 0, HWu);
-      const unsigned xbase = (unsigned)b * d.A + d.Bc;
+      real[i] = ch < Cin;
+      ds[i] = row_desc_at(sbase, cb1, cb2, cb3, real[i] ? ch : 0, HWu);
+    }
+    xmask = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned xbase = (unsigned)b * ds[i].A + ds[i].Bc;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int e = lane + 64 * j;
         const int hy = e / HWd, hx = e - hy * HWd;
         const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
-        const bool ok = real && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const bool ok = real[i] && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
         xmask |= ok ? (1u << (i * NJ + j)) : 0u;
-        xr[i * NJ + j] = d.p[ok ? xbase + (d.M ? (unsigned)(yy * W + xx) : 0u) : 0u];
+        xr[i * NJ + j] = ds[i].p[ok ? xbase + (ds[i].M ? (unsigned)(yy * W + xx) : 0u) : 0u];
       }
     }
   };

@@ -42,6 +42,7 @@ for step in "$@"; do
          run pmc_traffic 60 python tools/pmc_traffic.py "$OUT" ;;
     w:*) wl=${step#w:}; run "bench_$wl" 900 python bench.py --workload "$wl" --steps 10 --warmup 3 ;;
     tprof) run torch_prof 600 python tools/torch_prof.py ;;
+    pmcsq) run pmc_sq 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python bench.py --roofline-only ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
