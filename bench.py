@@ -387,6 +387,8 @@ def main():
                     help="direct weight-gradient kernels on a side stream (A/B)")
     ap.add_argument("--no-direct-wgrad", action="store_true",
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
+    ap.add_argument("--serial-encoders", action="store_true",
+                    help="context encoders on the main stream instead of side streams (A/B)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
@@ -405,6 +407,8 @@ def main():
     _hconv.set_weight_grad_stream(args.wgrad_side_stream)
     from dro_sfm_amd.networks.optim import update as _update
     _update.set_conv_backend(args.conv_backend)
+    from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
+    _dpn.set_concurrent_encoders(not args.serial_encoders)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -461,6 +465,7 @@ def main():
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_convs": args.conv_backend,
+                   "encoders": "serial" if args.serial_encoders else "concurrent streams",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},
         "final_loss": round(float(loss), 6),

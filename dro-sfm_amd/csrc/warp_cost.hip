@@ -287,6 +287,70 @@ __global__ __launch_bounds__(256) void plane_sweep_kernel(WarpArgs a, const floa
   }
 }
 
+// Quad variant (w % 4 == 0, 16-byte aligned planes): a thread owns 4 adjacent
+// pixels of one row for one (b, plane) and a run of kSweepCPT channels.  The
+// 4 projections are computed once for all its channels; every tap load is
+// unconditional from a clamped index with a zero weight for out-of-image
+// taps (fma(x, 0, v) == v, so the sum equals the guarded one bit for bit);
+// fmap is read and the cost written as float4 (16 B per lane).
+// HBM bound: the volume write (4*B*D*C*P bytes) dominates the traffic.
+constexpr int kSweepCPT = 32;
+
+__global__ __launch_bounds__(256) void plane_sweep_quad_kernel(WarpArgs a, const float* __restrict__ disp,
+                                                               int D, float* __restrict__ cost) {
+  const int P = a.h * a.w, P4 = P >> 2;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.z / D, d = blockIdx.z - (blockIdx.z / D) * D;
+  const int c0 = blockIdx.y * kSweepCPT;
+  if (q >= P4) return;
+  const int cn = min(kSweepCPT, a.C - c0);
+  float ki[9], kr[9];
+  cams(a, b, ki, kr);
+  float dd;
+  const float depth = decode_depth(disp[d], DRO_DEPTH_DISP, a.min_disp, a.span, &dd);
+  float R[9], t[3];
+  load_pose(a.pose + (size_t)b * pose_stride(a.pose_mode), a.pose_mode, R, t);
+  int idx[4][4];
+  float wgt[4][4];
+  const int p0 = 4 * q, y = p0 / a.w, x0 = p0 - y * a.w;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    Proj pr;
+    project(ki, kr, R, t, (float)(x0 + k), (float)y, depth, a.h, a.w, pr);
+    Taps T;
+    bilinear_taps(pr.ix, pr.iy, a.h, a.w, T);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      idx[k][e] = T.ok[e] ? T.idx[e] : 0;
+      wgt[k][e] = T.ok[e] ? T.wgt[e] : 0.f;
+    }
+  }
+  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p0;
+  const float* fr = a.fmap_ref + ((size_t)b * a.C + c0) * P;
+  float* out = cost + (((size_t)b * D + d) * a.C + c0) * P + p0;
+#pragma unroll 4
+  for (int c = 0; c < cn; ++c) {
+    const float* pl = fr + (size_t)c * P;
+    const float4 f = *reinterpret_cast<const float4*>(fm + (size_t)c * P);
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float val = 0.f;
+      val += pl[idx[k][0]] * wgt[k][0];
+      val += pl[idx[k][1]] * wgt[k][1];
+      val += pl[idx[k][2]] * wgt[k][2];
+      val += pl[idx[k][3]] * wgt[k][3];
+      v[k] = val;
+    }
+    float4 o;
+    o.x = (f.x - v[0]) * (f.x - v[0]);
+    o.y = (f.y - v[1]) * (f.y - v[1]);
+    o.z = (f.z - v[2]) * (f.z - v[2]);
+    o.w = (f.w - v[3]) * (f.w - v[3]);
+    *reinterpret_cast<float4*>(out + (size_t)c * P) = o;
+  }
+}
+
 int launch_pose_finalize(const float* partial, int nblk, int npose, const float* pose,
                          int pose_mode, float* gpose, hipStream_t s) {
   hipLaunchKernelGGL(pose_finalize_kernel, dim3((npose + 63) / 64), dim3(64), 0, s, partial, nblk,
@@ -433,6 +497,13 @@ extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref,
   WarpArgs a = make_args(fmap, fmap_ref, nullptr, DRO_DEPTH_DISP, min_disp, max_disp, K, ref_K,
                          scale, pose, pose_mode, B, 1, C, h, w, 0);
   const int P = h * w;
+  const bool quad = (w % 4) == 0 && ((uintptr_t)fmap % 16) == 0 && ((uintptr_t)cost % 16) == 0;
+  if (quad) {
+    dim3 grid((P / 4 + 255) / 256, (C + kSweepCPT - 1) / kSweepCPT, B * D);
+    hipLaunchKernelGGL(plane_sweep_quad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D,
+                       cost);
+    return launch_status("plane_sweep_quad_kernel launch failed");
+  }
   dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B * D);
   hipLaunchKernelGGL(plane_sweep_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D, cost);
   return launch_status("plane_sweep_kernel launch failed");

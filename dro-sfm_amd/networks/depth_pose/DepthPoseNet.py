@@ -14,8 +14,16 @@ Execution plan (what changes versus the reference, never the math):
     and the whole pose update block (cost, encoder, GRU, head) run once over
     N*B samples instead of N Python iterations;
   * convex upsampling is one HIP launch (hip.convex_upsample);
+  * the two context encoders (cnet_depth, cnet_pose) run on two side HIP
+    streams concurrently with the feature encoder and the initial heads: the
+    three ResNet trunks are independent and individually too small to fill
+    the GPU at B=2.  Autograd runs each op's backward on its forward stream, so
+    the encoders' backward overlaps too; a hipGraph capture records the
+    fork/join as parallel branches (set_concurrent_encoders(False) to
+    serialise, for A/B runs);
   * no host synchronisation anywhere: the step can be captured in a hipGraph.
 """
+import contextlib
 import logging
 
 import torch
@@ -27,6 +35,10 @@ from ..optim.update import (BasicUpdateBlockDepth, BasicUpdateBlockPose, DepthHe
                             UpMaskNet)
 
 
+def _null():
+    return contextlib.nullcontext()
+
+
 def parse_version(version):
     """'it{I}[-h][-seq{S}][-inter][-out]' (DepthPoseNet.py:22-34)."""
     assert version and "it" in version, f"bad DepthPoseNet version {version!r}"
@@ -35,6 +47,22 @@ def parse_version(version):
     seq = next((int(f.split("seq")[1]) for f in fields if "seq" in f), 4)
     return {"outer": total // seq, "seq": seq, "high": "h" in version,
             "out_norm": "out" in version, "inter": "inter" in version}
+
+
+_CONCURRENT = [True]
+_SIDE_STREAMS = {}
+
+
+def set_concurrent_encoders(enabled):
+    """Run cnet_depth / cnet_pose on side streams beside fnet (default True)."""
+    _CONCURRENT[0] = bool(enabled)
+
+
+def _side_streams(device):
+    ss = _SIDE_STREAMS.get(device)
+    if ss is None:
+        ss = _SIDE_STREAMS[device] = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
+    return ss
 
 
 class DepthPoseNet(nn.Module):
@@ -95,6 +123,26 @@ class DepthPoseNet(nn.Module):
         C, hd, cd = self.foutput_dim, self.hdim, self.cdim
         K = intrinsics.float().contiguous()
 
+        # context encoders first, on side streams (they depend on the images only)
+        side = None
+        if self.iters > 0:
+            if _CONCURRENT[0] and target_image.is_cuda:
+                main = torch.cuda.current_stream(target_image.device)
+                side = _side_streams(target_image.device)
+                for st in side:
+                    st.wait_stream(main)
+                for t in [target_image, *ref_imgs]:
+                    for st in side:
+                        t.record_stream(st)
+            with torch.cuda.stream(side[0]) if side else _null():
+                ctx_d = self.cnet_depth(target_image)
+                h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
+            with torch.cuda.stream(side[1]) if side else _null():
+                pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
+                                   torch.stack(list(ref_imgs))], 2).flatten(0, 1)
+                ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
+                h_p, x_p = torch.tanh(ctx_p[:, :hd]), torch.relu(ctx_p[:, hd:hd + cd])
+
         fmaps = self.fnet(torch.cat([target_image] + list(ref_imgs), 0))
         assert target_image.shape[2] // fmaps.shape[2] == self.feat_ratio
         h, w = fmaps.shape[2:]
@@ -110,13 +158,12 @@ class DepthPoseNet(nn.Module):
                                                               self.feat_ratio))]
         pose_preds = [poses]
 
-        if self.iters > 0:
-            ctx_d = self.cnet_depth(target_image)
-            h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
-            pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
-                               torch.stack(list(ref_imgs))], 2).flatten(0, 1)
-            ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
-            h_p, x_p = torch.tanh(ctx_p[:, :hd]), torch.relu(ctx_p[:, hd:hd + cd])
+        if side:                                          # join: the update blocks read h/x
+            main = torch.cuda.current_stream(target_image.device)
+            for st in side:
+                main.wait_stream(st)
+            for t in (h_d, x_d, h_p, x_p):
+                t.record_stream(main)
 
         for _ in range(self.iters):
             disp = disp.detach()

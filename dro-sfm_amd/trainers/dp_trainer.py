@@ -99,7 +99,16 @@ class GradBuckets:
         if b is None:
             return
         self._left[b] -= 1
+        if self.flat.is_cuda:
+            # the hook runs on the stream that produced this gradient (the context
+            # encoders' backward runs on side streams): remember it for the bucket
+            self._bstreams[b].add(torch.cuda.current_stream())
         if self._left[b] == 0 and self.world > 1 and not self._deferred[b]:
+            if self.flat.is_cuda:
+                cur = torch.cuda.current_stream()
+                for st in self._bstreams[b]:
+                    if st != cur:
+                        cur.wait_stream(st)
             self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
                                                  group=self.group, async_op=True))
 
@@ -108,6 +117,7 @@ class GradBuckets:
         self._pending = []
         if self.active is not None:
             self._left = list(self._need)
+            self._bstreams = [set() for _ in self.buckets]
 
     def finish(self):
         """Complete every bucket's all-reduce and average over ranks."""

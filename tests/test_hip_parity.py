@@ -86,6 +86,27 @@ def test_plane_sweep(hip):
     assert rel(vol, d["cost"]) < TOL
 
 
+@pytest.mark.parametrize("w", [80, 21])
+def test_plane_sweep_equals_per_plane_warp_cost(hip, w):
+    """D=64 sweep at the KITTI feature size (24x80: float4 quad kernel; 24x21:
+    the per-pixel kernel) against one warp_cost call per plane with that
+    plane's constant disparity map: bit-identical (same projection, same tap
+    sums; out-of-image taps weigh zero instead of being skipped)."""
+    g = torch.Generator().manual_seed(9)
+    B, C, h, D = 2, 128, 24, 64
+    fmap = torch.randn(B, C, h, w, generator=g).to(DEV)
+    fref = torch.randn(B, C, h, w, generator=g).to(DEV)
+    pose = torch.cat([0.3 * torch.randn(B, 3, generator=g), 0.02 * torch.randn(B, 3, generator=g)], 1).to(DEV)
+    K = kitti_K(B, W=8 * w, H=8 * h).to(DEV)
+    disp = torch.linspace(0, 1, D).to(DEV)
+    vol = hip.plane_sweep_cost(fmap, fref, disp, pose, K, min_depth=0.5, max_depth=80.0)
+    for d in (0, 17, 40, 63):
+        dm = disp[d].expand(B, 1, h, w).contiguous()
+        ref = hip.warp_cost(fmap, fref, dm, pose, K, depth_mode=hip.DEPTH_DISP, min_depth=0.5,
+                            max_depth=80.0, reduce_mean=False).squeeze(0)
+        assert torch.equal(vol[:, d], ref), d
+
+
 def test_warp_cost_kitti_size_vs_oracle(hip):
     """Metric-config size: B=2, C=128, 24x80, N=2 refs, depth mean + per-ref pose cost."""
     g = torch.Generator().manual_seed(7)
