@@ -177,7 +177,7 @@ def _event_loop(fn, iters, device):
 
 def roofline_plane_sweep(device, D=64, B=2, C=128, iters=20):
     """D = 64 depth-hypothesis stress of configs[1]: one
-    plane_sweep_kernel launch builds the cost volume [B, D, C, h, w] of D
+    plane_sweep_wide_kernel launch builds the cost volume [B, D, C, h, w] of D
     fronto-parallel planes (disp = linspace(0, 1, D) through disp_to_depth) at
     the feature resolution.  Algorithmic bytes per launch: fmap + fmap_ref read
     once (2 * 4 * B*C*P) + the volume written once (4 * B*D*C*P)."""
@@ -196,7 +196,7 @@ def roofline_plane_sweep(device, D=64, B=2, C=128, iters=20):
     P = h * w
     nbytes = 2 * 4 * B * C * P + 4 * B * D * C * P
     achieved = nbytes / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": f"plane_sweep_kernel (D={D}, B={B}, C={C}, {h}x{w})",
+    return {"bound": "hbm", "kernel": f"plane_sweep_wide_kernel (D={D}, B={B}, C={C}, {h}x{w})",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "algorithmic_bytes": int(nbytes), "avg_launch_us": round(ms * 1e3, 2), "launches": iters}
@@ -387,8 +387,8 @@ def main():
                     help="direct weight-gradient kernels on a side stream (A/B)")
     ap.add_argument("--no-direct-wgrad", action="store_true",
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
-    ap.add_argument("--serial-encoders", action="store_true",
-                    help="context encoders on the main stream instead of side streams (A/B)")
+    ap.add_argument("--concurrent-encoders", action="store_true",
+                    help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
@@ -408,7 +408,7 @@ def main():
     from dro_sfm_amd.networks.optim import update as _update
     _update.set_conv_backend(args.conv_backend)
     from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
-    _dpn.set_concurrent_encoders(not args.serial_encoders)
+    _dpn.set_concurrent_encoders(args.concurrent_encoders)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -465,7 +465,7 @@ def main():
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_convs": args.conv_backend,
-                   "encoders": "serial" if args.serial_encoders else "concurrent streams",
+                   "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},
         "final_loss": round(float(loss), 6),

@@ -1119,6 +1119,12 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
   // K split inside the block first (4 or 2 wave groups per tile: no partials,
   // no finish launch), over blocks only when the grid is still very short
   int kin = blocks < 256 ? 4 : (blocks < 512 ? 2 : 1);
+  static const int kin_env = [] {   // tuning override: DRO_CONV_KIN=1|2|4
+    const char* e = getenv("DRO_CONV_KIN");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  if (kin_env) kin = kin_env;
   while (kin > 1 && kin > nchunks) kin >>= 1;
   pl.kin = kin;
   int ks = 1;

@@ -251,58 +251,23 @@ __global__ void pose_finalize_kernel(const float* __restrict__ partial, int nblk
 }
 
 // ------------------------------------------------------------------ plane sweep (forward only)
-__global__ __launch_bounds__(256) void plane_sweep_kernel(WarpArgs a, const float* __restrict__ disp,
-                                                          int D, float* __restrict__ cost) {
-  const int P = a.h * a.w;
-  const int p = blockIdx.x * kWave + (threadIdx.x & 63);
-  const int b = blockIdx.z / D, d = blockIdx.z % D;
-  const int c0 = (blockIdx.y * kGroups + (threadIdx.x >> 6)) * kCPT;
-  if (p >= P || c0 >= a.C) return;
-  const int cn = min(kCPT, a.C - c0);
-  float ki[9], kr[9];
-  cams(a, b, ki, kr);
-  float dd;
-  const float depth = decode_depth(disp[d], DRO_DEPTH_DISP, a.min_disp, a.span, &dd);
-  float R[9], t[3];
-  load_pose(a.pose + (size_t)b * pose_stride(a.pose_mode), a.pose_mode, R, t);
-  Proj q;
-  project(ki, kr, R, t, (float)(p % a.w), (float)(p / a.w), depth, a.h, a.w, q);
-  Taps T;
-  bilinear_taps(q.ix, q.iy, a.h, a.w, T);
-  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
-  const float* fr = a.fmap_ref + ((size_t)b * a.C + c0) * P;
-  float* out = cost + (((size_t)b * D + d) * a.C + c0) * P + p;
-#pragma unroll
-  for (int c = 0; c < kCPT; ++c) {
-    if (c < cn) {
-      const float* pl = fr + (size_t)c * P;
-      float val = 0.f;
-      if (T.ok[0]) val += pl[T.idx[0]] * T.wgt[0];
-      if (T.ok[1]) val += pl[T.idx[1]] * T.wgt[1];
-      if (T.ok[2]) val += pl[T.idx[2]] * T.wgt[2];
-      if (T.ok[3]) val += pl[T.idx[3]] * T.wgt[3];
-      const float df = fm[(size_t)c * P] - val;
-      out[(size_t)c * P] = df * df;
-    }
-  }
-}
-
-// Quad variant (w % 4 == 0, 16-byte aligned planes): a thread owns 4 adjacent
-// pixels of one row for one (b, plane) and a run of kSweepCPT channels.  The
-// 4 projections are computed once for all its channels; every tap load is
-// unconditional from a clamped index with a zero weight for out-of-image
-// taps (fma(x, 0, v) == v, so the sum equals the guarded one bit for bit);
-// fmap is read and the cost written as float4 (16 B per lane).
-// HBM bound: the volume write (4*B*D*C*P bytes) dominates the traffic.
+// Sweep kernel: lanes run along 64 consecutive pixels (every tap gather of a
+// wave touches consecutive addresses, every store is a 256-B row segment),
+// each of the 4 waves owns kSweepCPT channels of one (b, plane).  The
+// projection is computed once per pixel for all of a wave's channels; tap
+// loads are unconditional from clamped indices with zero weights for
+// out-of-image taps (fma(x, 0, v) == v: the sum equals the guarded one bit
+// for bit), issued 8 channels at a time.  HBM bound: the volume write
+// (4*B*D*C*P bytes) dominates the traffic.
 constexpr int kSweepCPT = 32;
 
-__global__ __launch_bounds__(256) void plane_sweep_quad_kernel(WarpArgs a, const float* __restrict__ disp,
+__global__ __launch_bounds__(256) void plane_sweep_wide_kernel(WarpArgs a, const float* __restrict__ disp,
                                                                int D, float* __restrict__ cost) {
-  const int P = a.h * a.w, P4 = P >> 2;
-  const int q = blockIdx.x * 256 + threadIdx.x;
+  const int P = a.h * a.w;
+  const int p = blockIdx.x * kWave + (threadIdx.x & 63);
   const int b = blockIdx.z / D, d = blockIdx.z - (blockIdx.z / D) * D;
-  const int c0 = blockIdx.y * kSweepCPT;
-  if (q >= P4) return;
+  const int c0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * kSweepCPT;
+  if (p >= P || c0 >= a.C) return;
   const int cn = min(kSweepCPT, a.C - c0);
   float ki[9], kr[9];
   cams(a, b, ki, kr);
@@ -310,44 +275,41 @@ __global__ __launch_bounds__(256) void plane_sweep_quad_kernel(WarpArgs a, const
   const float depth = decode_depth(disp[d], DRO_DEPTH_DISP, a.min_disp, a.span, &dd);
   float R[9], t[3];
   load_pose(a.pose + (size_t)b * pose_stride(a.pose_mode), a.pose_mode, R, t);
-  int idx[4][4];
-  float wgt[4][4];
-  const int p0 = 4 * q, y = p0 / a.w, x0 = p0 - y * a.w;
+  Proj pr;
+  project(ki, kr, R, t, (float)(p % a.w), (float)(p / a.w), depth, a.h, a.w, pr);
+  Taps T;
+  bilinear_taps(pr.ix, pr.iy, a.h, a.w, T);
+  int idx[4];
+  float wgt[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    Proj pr;
-    project(ki, kr, R, t, (float)(x0 + k), (float)y, depth, a.h, a.w, pr);
-    Taps T;
-    bilinear_taps(pr.ix, pr.iy, a.h, a.w, T);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      idx[k][e] = T.ok[e] ? T.idx[e] : 0;
-      wgt[k][e] = T.ok[e] ? T.wgt[e] : 0.f;
-    }
+  for (int e = 0; e < 4; ++e) {
+    idx[e] = T.ok[e] ? T.idx[e] : 0;
+    wgt[e] = T.ok[e] ? T.wgt[e] : 0.f;
   }
-  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p0;
+  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
   const float* fr = a.fmap_ref + ((size_t)b * a.C + c0) * P;
-  float* out = cost + (((size_t)b * D + d) * a.C + c0) * P + p0;
-#pragma unroll 4
-  for (int c = 0; c < cn; ++c) {
-    const float* pl = fr + (size_t)c * P;
-    const float4 f = *reinterpret_cast<const float4*>(fm + (size_t)c * P);
-    float v[4];
+  float* out = cost + (((size_t)b * D + d) * a.C + c0) * P + p;
+  for (int cb = 0; cb < cn; cb += 8) {
+    float f[8], v[8][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float val = 0.f;
-      val += pl[idx[k][0]] * wgt[k][0];
-      val += pl[idx[k][1]] * wgt[k][1];
-      val += pl[idx[k][2]] * wgt[k][2];
-      val += pl[idx[k][3]] * wgt[k][3];
-      v[k] = val;
+    for (int c = 0; c < 8; ++c) {
+      const int cc = min(cb + c, cn - 1);
+      const float* pl = fr + (size_t)cc * P;
+      f[c] = fm[(size_t)cc * P];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] = pl[idx[e]];
     }
-    float4 o;
-    o.x = (f.x - v[0]) * (f.x - v[0]);
-    o.y = (f.y - v[1]) * (f.y - v[1]);
-    o.z = (f.z - v[2]) * (f.z - v[2]);
-    o.w = (f.w - v[3]) * (f.w - v[3]);
-    *reinterpret_cast<float4*>(out + (size_t)c * P) = o;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float val = 0.f;
+      val += v[c][0] * wgt[0];
+      val += v[c][1] * wgt[1];
+      val += v[c][2] * wgt[2];
+      val += v[c][3] * wgt[3];
+      const float df = f[c] - val;
+      // streaming volume: non-temporal stores keep it out of L2's way
+      if (cb + c < cn) __builtin_nontemporal_store(df * df, out + (size_t)(cb + c) * P);
+    }
   }
 }
 
@@ -497,14 +459,8 @@ extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref,
   WarpArgs a = make_args(fmap, fmap_ref, nullptr, DRO_DEPTH_DISP, min_disp, max_disp, K, ref_K,
                          scale, pose, pose_mode, B, 1, C, h, w, 0);
   const int P = h * w;
-  const bool quad = (w % 4) == 0 && ((uintptr_t)fmap % 16) == 0 && ((uintptr_t)cost % 16) == 0;
-  if (quad) {
-    dim3 grid((P / 4 + 255) / 256, (C + kSweepCPT - 1) / kSweepCPT, B * D);
-    hipLaunchKernelGGL(plane_sweep_quad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D,
-                       cost);
-    return launch_status("plane_sweep_quad_kernel launch failed");
-  }
-  dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B * D);
-  hipLaunchKernelGGL(plane_sweep_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D, cost);
-  return launch_status("plane_sweep_kernel launch failed");
+  dim3 grid((P + kWave - 1) / kWave, (C + 4 * kSweepCPT - 1) / (4 * kSweepCPT), B * D);
+  hipLaunchKernelGGL(plane_sweep_wide_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D,
+                     cost);
+  return launch_status("plane_sweep_wide_kernel launch failed");
 }

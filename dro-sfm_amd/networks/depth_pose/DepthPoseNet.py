@@ -14,13 +14,12 @@ Execution plan (what changes versus the reference, never the math):
     and the whole pose update block (cost, encoder, GRU, head) run once over
     N*B samples instead of N Python iterations;
   * convex upsampling is one HIP launch (hip.convex_upsample);
-  * the two context encoders (cnet_depth, cnet_pose) run on two side HIP
-    streams concurrently with the feature encoder and the initial heads: the
-    three ResNet trunks are independent and individually too small to fill
-    the GPU at B=2.  Autograd runs each op's backward on its forward stream, so
-    the encoders' backward overlaps too; a hipGraph capture records the
-    fork/join as parallel branches (set_concurrent_encoders(False) to
-    serialise, for A/B runs);
+  * optionally (set_concurrent_encoders(True)) the two context encoders
+    (cnet_depth, cnet_pose) run on two side HIP streams beside the feature
+    encoder; autograd runs their backward on the same streams and a hipGraph
+    capture records the fork/join as parallel branches.  Measured slower on
+    MI355X (24.7 vs 23.7 ms/step: the cross-stream edges cost more than the
+    overlap of three MIOpen-bound trunks gains), so serial is the default;
   * no host synchronisation anywhere: the step can be captured in a hipGraph.
 """
 import contextlib
@@ -49,12 +48,12 @@ def parse_version(version):
             "out_norm": "out" in version, "inter": "inter" in version}
 
 
-_CONCURRENT = [True]
+_CONCURRENT = [False]
 _SIDE_STREAMS = {}
 
 
 def set_concurrent_encoders(enabled):
-    """Run cnet_depth / cnet_pose on side streams beside fnet (default True)."""
+    """Run cnet_depth / cnet_pose on side streams beside fnet (default False)."""
     _CONCURRENT[0] = bool(enabled)
 
 

@@ -88,10 +88,10 @@ def test_plane_sweep(hip):
 
 @pytest.mark.parametrize("w", [80, 21])
 def test_plane_sweep_equals_per_plane_warp_cost(hip, w):
-    """D=64 sweep at the KITTI feature size (24x80: float4 quad kernel; 24x21:
-    the per-pixel kernel) against one warp_cost call per plane with that
-    plane's constant disparity map: bit-identical (same projection, same tap
-    sums; out-of-image taps weigh zero instead of being skipped)."""
+    """D=64 sweep at the KITTI feature size (24x80; and 24x21, a ragged last
+    pixel block) against one warp_cost call per plane with that plane's
+    constant disparity map: bit-identical (same projection, same tap sums;
+    out-of-image taps weigh zero instead of being skipped)."""
     g = torch.Generator().manual_seed(9)
     B, C, h, D = 2, 128, 24, 64
     fmap = torch.randn(B, C, h, w, generator=g).to(DEV)
