@@ -12,6 +12,13 @@ provides it MI355X-first:
   * a post-accumulate hook per parameter counts arrivals per bucket; a full
     bucket's all-reduce is issued immediately (async), so communication of
     late layers overlaps backward of early ones;
+  * from the second step on, parameters whose gradient autograd produces
+    (everything but the conv-engine weights written in place) start the
+    backward with .grad = None, so AccumulateGrad adopts the produced tensor
+    instead of launching an add into the zeroed flat buffer; a complete
+    bucket's adopted gradients are copied into the flat buffer with one
+    multi-tensor launch (torch._foreach_copy_) -- ~160 add launches per step
+    become a handful;
   * parameters that never receive a gradient (DepthPoseNet.cnet, dead in the
     reference forward) are discovered on the first step and left out;
   * initial parameters and buffers are broadcast from rank 0 (BatchNorm keeps
@@ -75,6 +82,8 @@ class GradBuckets:
         if cur:
             self.buckets.append(cur)
         self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b}
+        # gradients adopted from autograd (.grad = None at the start of a step)
+        self._adopt = [[p for p in b if not _direct_used(p)] for b in self.buckets]
         # gradients written in place by the hip convs (side stream, joined at the end
         # of backward) fire no hook: their buckets are reduced in finish()
         self._deferred = [any(_direct_used(p) for p in b) for b in self.buckets]
@@ -99,6 +108,8 @@ class GradBuckets:
         if b is None:
             return
         self._left[b] -= 1
+        if self._left[b] == 0:
+            self._gather(b)
         if self.flat.is_cuda:
             # the hook runs on the stream that produced this gradient (the context
             # encoders' backward runs on side streams): remember it for the bucket
@@ -112,12 +123,32 @@ class GradBuckets:
             self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
                                                  group=self.group, async_op=True))
 
+    def _gather(self, b):
+        """Copy bucket b's adopted gradients into the flat buffer (one launch)."""
+        ps = [p for p in self._adopt[b] if p.grad is not None and not self._is_view(p)]
+        if ps:
+            torch._foreach_copy_([self._view(p) for p in ps], [p.grad for p in ps])
+            for p in ps:
+                p.grad = self._view(p)
+
+    def _view(self, p):
+        off = self.offsets[p]
+        return self.flat[off:off + p.numel()].view_as(p)
+
+    def _is_view(self, p):
+        g = p.grad
+        return (g.untyped_storage().data_ptr() == self.flat.untyped_storage().data_ptr()
+                and g.storage_offset() == self.offsets[p])
+
     def zero(self):
         self.flat.zero_()
         self._pending = []
         if self.active is not None:
             self._left = list(self._need)
             self._bstreams = [set() for _ in self.buckets]
+            for ps in self._adopt:
+                for p in ps:
+                    p.grad = None
 
     def finish(self):
         """Complete every bucket's all-reduce and average over ranks."""
@@ -132,6 +163,9 @@ class GradBuckets:
                 for b in self.buckets:
                     dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM, group=self.group)
         else:
+            for b in range(len(self.buckets)):
+                if self._left[b] != 0:      # a bucket some of whose gradients never arrived
+                    self._gather(b)
             if self.world > 1:
                 for b, d in zip(self.buckets, self._deferred):
                     if d:
