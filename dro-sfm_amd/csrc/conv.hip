@@ -399,6 +399,9 @@ struct HaloShape {
 template <int BM, int KH, int KW, int MODE, int ACT, int EPI, int KS>
 __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   using S = HaloShape<BM, KH, KW>;
+  // staging prefetch distance: 2 chunks when the register budget allows
+  // (<= 8 waves per CU); 4 wave groups per block run at 128 VGPRs with 1
+  constexpr int PF = KS <= 2 ? 2 : 1;
   static_assert(KS == 1 || S::LDS >= 4 * 16 * 64, "cross-group reduction area");
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
   constexpr int CK = S::CK, NJ = S::NJ, XPER = CK / 4;
@@ -447,9 +450,17 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   constexpr bool FOLD = MODE == 1 && ACT != 0;
   const float* __restrict__ Yp = a.gy;
   const float galpha = a.galpha;
-  float xr[XPER * NJ], yr[FOLD ? XPER * NJ : 1], wv[S::WPER];
-  unsigned xmask = 0;
-  auto load = [&](int chunk) {
+  // one chunk's staging registers; with PF == 2 two sets alternate so the
+  // loads of chunk c+2 are in flight while chunk c is multiplied
+  struct Stage {
+    float xr[XPER * NJ], yr[FOLD ? XPER * NJ : 1], wv[S::WPER];
+    unsigned xmask;
+  };
+  auto load = [&](Stage& st, int chunk) {
+    float(&xr)[XPER * NJ] = st.xr;
+    float(&yr)[FOLD ? XPER * NJ : 1] = st.yr;
+    float(&wv)[S::WPER] = st.wv;
+    unsigned& xmask = st.xmask;
     const int c0 = chunk * CK;
     // weights first (no descriptor needed), then every channel's source
     // descriptor (independent scalar loads, one wait), then the input patch:
@@ -495,7 +506,11 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Stage& st, int buf) {
+    const float(&xr)[XPER * NJ] = st.xr;
+    const float(&yr)[FOLD ? XPER * NJ : 1] = st.yr;
+    const float(&wv)[S::WPER] = st.wv;
+    const unsigned xmask = st.xmask;
     float* Ws = smem + buf * STAGE;
     float* Xs = Ws + WSZ;
 #pragma unroll
@@ -539,33 +554,52 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   // group grp handles chunks cbeg + grp, cbeg + grp + KS, ...; every group
   // runs the same number of iterations (barriers are block wide)
   const int nit = (cend - cbeg + KS - 1) / KS;
-  if (cbeg + grp < cend) {
-    load(cbeg + grp);
-    store(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < nit; ++it) {
-    const int c = cbeg + it * KS + grp;
-    const int buf = it & 1;
-    const bool more = c + KS < cend;
-    if (more) load(c + KS);
-    if (KS == 1 || c < cend) {
-      const float* wa = smem + buf * STAGE + abase;
-      const float* xb = smem + buf * STAGE + WSZ + bbase;
+  auto chunk_of = [&](int it) { return cbeg + it * KS + grp; };
+  auto mma = [&](int buf) {
+    const float* wa = smem + buf * STAGE + abase;
+    const float* xb = smem + buf * STAGE + WSZ + bbase;
 #pragma unroll
-      for (int ty = 0; ty < KH; ++ty) {
+    for (int ty = 0; ty < KH; ++ty) {
 #pragma unroll
-        for (int tx = 0; tx < KW; ++tx) {
-          const int tap = ty * KW + tx;
-          const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
+      for (int tx = 0; tx < KW; ++tx) {
+        const int tap = ty * KW + tx;
+        const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
 #pragma unroll
-          for (int s = 0; s < NS; ++s)
-            acc = mfma32(wa[tap + s * ASTEP], xb[toff + 2 * s * HPAD], acc);
-        }
+        for (int s = 0; s < NS; ++s)
+          acc = mfma32(wa[tap + s * ASTEP], xb[toff + 2 * s * HPAD], acc);
       }
     }
-    if (more) store(buf ^ 1);
-    __syncthreads();
+  };
+  Stage sa, sb;
+  if (chunk_of(0) < cend) {
+    load(sa, chunk_of(0));
+    store(sa, 0);
+  }
+  if (PF == 2 && chunk_of(1) < cend) load(sb, chunk_of(1));
+  __syncthreads();
+  if (PF == 1) {
+    for (int it = 0; it < nit; ++it) {
+      const int buf = it & 1;
+      const bool more = chunk_of(it + 1) < cend;
+      if (more) load(sa, chunk_of(it + 1));
+      if (KS == 1 || chunk_of(it) < cend) mma(buf);
+      if (more) store(sa, buf ^ 1);
+      __syncthreads();
+    }
+  } else {
+    // registers: sb holds chunk it+1 (stored into LDS at the end of
+    // iteration it), sa receives chunk it+2
+    for (int it = 0; it < nit; it += 2) {
+      if (chunk_of(it + 2) < cend) load(sa, chunk_of(it + 2));
+      if (chunk_of(it) < cend) mma(0);
+      if (chunk_of(it + 1) < cend) store(sb, 1);
+      __syncthreads();
+      if (it + 1 >= nit) break;
+      if (chunk_of(it + 3) < cend) load(sb, chunk_of(it + 3));
+      if (chunk_of(it + 1) < cend) mma(1);
+      if (chunk_of(it + 2) < cend) store(sa, 0);
+      __syncthreads();
+    }
   }
   // reductions in a fixed order, every wave still resident (barriers below)
   const bool holder = WM == 2 || wk == 0;
