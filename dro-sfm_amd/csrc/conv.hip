@@ -104,6 +104,7 @@ struct IgArgs {
   // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
   // tile + halo staged once per channel chunk of CK channels
   int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
+  unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -208,6 +209,75 @@ __device__ __forceinline__ void epi_store(const IgArgs& a, int row, int eb, size
       grad_put(a.gsrc[2], a.gsrc_ctot[2], a.gsrc_coff[2], a.gsrc_acc[2], row - a.cbase[2], eb, epix, HW, acc);
     else
       grad_put(a.gsrc[3], a.gsrc_ctot[3], a.gsrc_coff[3], a.gsrc_acc[3], row - a.cbase[3], eb, epix, HW, acc);
+  }
+}
+
+// Epilogue of one 32x32 MFMA accumulator (16 rows per lane, row(r) = rbase +
+// (r & 3) + 8 (r >> 2)) at pixel (eb, epix): every operand the 16 rows need
+// (bias, z and h of the GRU epilogues, the old value of an accumulated
+// gradient) is loaded before the first is used -- one memory round trip for
+// the tile instead of one per row (measured: the per-row form spent longer
+// in the epilogue than in the whole K loop).
+template <int MODE, int ACT, int EPI>
+__device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int rbase, int eb,
+                                         size_t epix, size_t HW) {
+  const int rows = a.rows;
+  if (MODE == 0) {
+    float bv[16], zv[EPI == 1 ? 16 : 1], hv[EPI != 0 ? 16 : 1];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      const int rr = row < rows ? row : 0;
+      bv[r] = a.bias ? a.bias[rr] : 0.f;
+      if (EPI == 1) {
+        zv[r] = a.z.p[((size_t)eb * a.z.ctot + a.z.coff + rr) * HW + epix];
+        hv[r] = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + rr) * HW + epix];
+      }
+      if (EPI == 2) {
+        const int c = rr >= a.hd ? rr - a.hd : 0;
+        hv[r] = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + c) * HW + epix];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      if (row >= rows) continue;
+      float v = acc[r] + bv[r];
+      v = a.alpha * act_fwd(v, ACT);
+      if (EPI == 1) {
+        a.aux[((size_t)eb * a.rows + row) * HW + epix] = v;
+        v = (1.f - zv[r]) * hv[r] + zv[r] * v;
+      }
+      if (EPI == 2 && row >= a.hd)
+        a.aux[((size_t)eb * a.hd + (row - a.hd)) * HW + epix] = v * hv[r];
+      a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
+    }
+  } else {
+    float* dst[16];
+    bool accf[16];
+    float old[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      const int si = row >= rows ? -1 : (row >= a.cbase[1]) + (row >= a.cbase[2]) + (row >= a.cbase[3]);
+      float* base = nullptr;
+      int ctot = 0, coff = 0, cl = 0, ac = 0;
+      if (si >= 0) {
+        const int cb = si == 0 ? 0 : si == 1 ? a.cbase[1] : si == 2 ? a.cbase[2] : a.cbase[3];
+        base = si == 0 ? a.gsrc[0] : si == 1 ? a.gsrc[1] : si == 2 ? a.gsrc[2] : a.gsrc[3];
+        ctot = si == 0 ? a.gsrc_ctot[0] : si == 1 ? a.gsrc_ctot[1] : si == 2 ? a.gsrc_ctot[2] : a.gsrc_ctot[3];
+        coff = si == 0 ? a.gsrc_coff[0] : si == 1 ? a.gsrc_coff[1] : si == 2 ? a.gsrc_coff[2] : a.gsrc_coff[3];
+        ac = si == 0 ? a.gsrc_acc[0] : si == 1 ? a.gsrc_acc[1] : si == 2 ? a.gsrc_acc[2] : a.gsrc_acc[3];
+        cl = row - cb;
+      }
+      dst[r] = base ? base + ((size_t)eb * ctot + coff + cl) * HW + epix : nullptr;
+      accf[r] = base && ac;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) old[r] = accf[r] ? *dst[r] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (dst[r]) *dst[r] = accf[r] ? old[r] + acc[r] : acc[r];
   }
 }
 
@@ -346,11 +416,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   }
   const int eb = (int)(pe / (long long)HW);
   const size_t epix = (size_t)(pe - (long long)eb * HW);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < rows) epi_store<MODE, ACT, EPI>(a, row, eb, epix, HW, acc[r]);
-  }
+  epi_tile<MODE, ACT, EPI>(a, acc, row0 + wr * 32 + 4 * (lane >> 5), eb, epix, HW);
 }
 
 // ------------------------------------------------------------------ halo-tiled direct conv
@@ -555,6 +621,11 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   // runs the same number of iterations (barriers are block wide)
   const int nit = (cend - cbeg + KS - 1) / KS;
   auto chunk_of = [&](int it) { return cbeg + it * KS + grp; };
+  unsigned long long* const stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 16 : nullptr;
+  auto stamp = [&](int k) {
+    if (stp && threadIdx.x == 0 && k < 16) stp[k] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   auto mma = [&](int buf) {
     const float* wa = smem + buf * STAGE + abase;
     const float* xb = smem + buf * STAGE + WSZ + bbase;
@@ -577,6 +648,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   }
   if (PF == 2 && chunk_of(1) < cend) load(sb, chunk_of(1));
   __syncthreads();
+  stamp(1);
   if (PF == 1) {
     for (int it = 0; it < nit; ++it) {
       const int buf = it & 1;
@@ -585,6 +657,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       if (KS == 1 || chunk_of(it) < cend) mma(buf);
       if (more) store(sa, buf ^ 1);
       __syncthreads();
+      stamp(2 + it);
     }
   } else {
     // registers: sb holds chunk it+1 (stored into LDS at the end of
@@ -594,11 +667,13 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       if (chunk_of(it) < cend) mma(0);
       if (chunk_of(it + 1) < cend) store(sb, 1);
       __syncthreads();
+      stamp(2 + it);
       if (it + 1 >= nit) break;
       if (chunk_of(it + 3) < cend) load(sb, chunk_of(it + 3));
       if (chunk_of(it + 1) < cend) mma(1);
       if (chunk_of(it + 2) < cend) store(sa, 0);
       __syncthreads();
+      stamp(3 + it);
     }
   }
   // reductions in a fixed order, every wave still resident (barriers below)
@@ -630,6 +705,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       }
     }
   }
+  stamp(13);
   if (grp > 0 || !holder) return;
 
   const int oy = ty0 + qy, ox = tx0 + qx;
@@ -645,11 +721,8 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
     }
     return;
   }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < rows) epi_store<MODE, ACT, EPI>(a, row, b, epix, HW, acc[r]);
-  }
+  epi_tile<MODE, ACT, EPI>(a, acc, row0 + wr * 32 + 4 * (lane >> 5), b, epix, HW);
+  stamp(14);
 }
 
 // sum of n partials p[0], p[stride], ... in a fixed order (4 interleaved
@@ -1340,10 +1413,13 @@ Slice to_slice(const dro_slice* s) {
   return r;
 }
 
+unsigned long long* g_conv_stamps = nullptr;   // dro_debug_conv_stamps
+
 // rows / kch set by the caller; `ws` must hold plan.part_bytes
 template <int MODE, int ACT, int EPI>
 int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   const IgPlan pl = plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
+  a.stamps = g_conv_stamps;
   a.K = a.kch * a.g.KH * a.g.KW;
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
@@ -1429,6 +1505,11 @@ extern "C" int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, 
                            pl.TH, pl.TW, pl.HWd, pl.HPAD, pl.tiles_x, pl.tiles_img, pl.CK,
                            (long long)pl.lds_bytes, (long long)pl.part_bytes, pl.kin};
   for (int i = 0; i < 16; ++i) info[i] = v[i];
+  return DRO_OK;
+}
+
+extern "C" int dro_debug_conv_stamps(void* buffer) {
+  g_conv_stamps = static_cast<unsigned long long*>(buffer);
   return DRO_OK;
 }
 

@@ -54,6 +54,7 @@ def load():
     _sig(lib.dro_bilinear_upsample2x_backward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_conv2d_workspace_bytes, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_plan, I, I, I, I, I, I, I, P)
+    _sig(lib.dro_debug_conv_stamps, P)
     _sig(lib.dro_conv2d_forward, P, I, P, P, I, I, I, I, I, I, I, F, P, I, I, P, Z, S)
     _sig(lib.dro_convgru_gates_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, Z, S)
     _sig(lib.dro_convgru_blend_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, Z, S)
@@ -75,7 +76,7 @@ EXPORTED = (
     "dro_supervised_workspace_bytes", "dro_supervised_forward", "dro_supervised_backward",
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
-    "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_conv2d_forward", "dro_convgru_gates_forward",
+    "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",
     "dro_gru_backward_elem", "dro_adam_step",

@@ -210,6 +210,13 @@ size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int Cout, int KH
  * split-K partial bytes, 0. */
 int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, int W, long long* info);
 
+/* Diagnostics only: with a device buffer of >= 16 * (grid blocks) u64, every
+ * following halo-conv launch writes per-block s_memtime stamps (kernel start,
+ * after the prologue, after each K iteration, after the reductions, after
+ * the epilogue) into it; NULL turns it off.  Not thread safe; not for
+ * production launches. */
+int dro_debug_conv_stamps(void* buffer);
+
 int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
                        int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
                        float* out, int out_ctot, int out_coff, void* workspace,
