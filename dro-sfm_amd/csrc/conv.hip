@@ -676,52 +676,45 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       stamp(3 + it);
     }
   }
-  // reductions in a fixed order, every wave still resident (barriers below)
-  const bool holder = WM == 2 || wk == 0;
-  if (WM == 1) {   // sum the two channel halves (LDS reused after the final barrier)
-    float* red = smem;   // [2 pixel halves][16][64]
-    if (wk == 1) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[(wc * 16 + r) * 64 + lane] = acc[r];
-    }
-    __syncthreads();
-    if (wk == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += red[(wc * 16 + r) * 64 + lane];
-    }
-  }
-  if (KS > 1) {    // groups 1..KS-1 park their sums; group 0 adds them in group order
-    __syncthreads();
-    if (grp > 0 && holder) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) smem[(wave * 16 + r) * 64 + lane] = acc[r];
-    }
-    __syncthreads();
-    if (grp == 0 && holder) {
-      for (int g = 1; g < KS; ++g) {
-        const float* red = smem_all + g * S::LDS;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += red[(wave * 16 + r) * 64 + lane];
-      }
-    }
-  }
-  stamp(13);
-  if (grp > 0 || !holder) return;
-
-  const int oy = ty0 + qy, ox = tx0 + qx;
-  if (oy >= H || ox >= W) return;
-  const size_t epix = (size_t)oy * W + ox;
-  if (a.part) {   // split-K partial: [split][rows][P]
-    const long long P = (long long)a.g.B * HW;
-    float* dst = a.part + (size_t)blockIdx.y * rows * P + (size_t)b * HW + epix;
+  // Reduction + epilogue spread over ALL waves of the block: every wave parks
+  // its accumulator (one partial set per (group, K half)) in LDS, then each
+  // thread sums a few tile elements over the sets in a fixed order and runs
+  // the epilogue for them -- instead of one or two waves doing the whole tile
+  // (that serial tail cost as much as the K loop; profiles/r1_conv_phase_stamps.txt).
+  constexpr int NSET = (WM == 1 ? 2 : 1) * KS;
+  static_assert(NSET * BM * 64 <= KS * S::LDS, "reduction sets fit in the staging LDS");
+  {
+    const int set = grp * (WM == 1 ? 2 : 1) + (WM == 1 ? wk : 0);
+    float* red = smem_all + (size_t)set * BM * 64;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < rows) dst[(size_t)row * P] = acc[r];
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      red[rl * 64 + wc * 32 + (lane & 31)] = acc[r];
     }
-    return;
   }
-  epi_tile<MODE, ACT, EPI>(a, acc, row0 + wr * 32 + 4 * (lane >> 5), b, epix, HW);
+  __syncthreads();
+  stamp(13);
+  const long long P = (long long)a.g.B * HW;
+  for (int e = threadIdx.x; e < BM * 64; e += 256 * KS) {
+    const int rl = e >> 6, pl = e & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < KS; ++g) {
+      if (WM == 1)
+        v += smem_all[((size_t)(2 * g) * BM + rl) * 64 + pl] + smem_all[((size_t)(2 * g + 1) * BM + rl) * 64 + pl];
+      else
+        v += smem_all[((size_t)g * BM + rl) * 64 + pl];
+    }
+    const int row = row0 + rl;
+    const int py = pl / TW, px = pl - py * TW;
+    const int oy = ty0 + py, ox = tx0 + px;
+    if (row >= rows || oy >= H || ox >= W) continue;
+    const size_t epix = (size_t)oy * W + ox;
+    if (a.part)   // split-K partial: [split][rows][P]
+      a.part[(size_t)blockIdx.y * rows * P + (size_t)row * P + (size_t)b * HW + epix] = v;
+    else
+      epi_store<MODE, ACT, EPI>(a, row, b, epix, HW, v);
+  }
   stamp(14);
 }
 
