@@ -1218,7 +1218,11 @@ IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
   const long long blocks = (long long)pl.row_tiles * pl.ptiles;
   // K split inside the block first (4 or 2 wave groups per tile: no partials,
   // no finish launch), over blocks only when the grid is still very short
-  int kin = blocks < 256 ? 4 : (blocks < 512 ? 2 : 1);
+  static const long long t2 = [] {   // tuning: grids below this many tiles use 2 wave groups
+    const char* e = getenv("DRO_CONV_KIN2_BELOW");
+    return e ? atoll(e) : 512LL;
+  }();
+  int kin = blocks < 256 ? 4 : (blocks < t2 ? 2 : 1);
   static const int kin_env = [] {   // tuning override: DRO_CONV_KIN=1|2|4
     const char* e = getenv("DRO_CONV_KIN");
     const int v = e ? atoi(e) : 0;
