@@ -66,6 +66,22 @@ __device__ __forceinline__ int fdiv(int n, FastDiv f) {
   return f.one ? n : (int)__umulhi((unsigned)n, f.m);
 }
 
+// exact n / d for any 32-bit n, d >= 1: m = floor((2^32 - 1) / d) leaves the
+// mulhi estimate at most 2 low (host-computed; a few scalar ops per division)
+struct Div32 {
+  unsigned m, d;
+};
+__device__ __forceinline__ unsigned udiv(unsigned n, Div32 f) {
+  unsigned q = __umulhi(n, f.m);
+  unsigned r = n - q * f.d;
+  if (r >= f.d) {
+    ++q;
+    r -= f.d;
+  }
+  if (r >= f.d) ++q;
+  return q;
+}
+
 struct ConvGeom {
   int B, H, W, Cin, Cout, KH, KW, PH, PW;
 };
@@ -104,7 +120,14 @@ struct IgArgs {
   // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
   // tile + halo staged once per channel chunk of CK channels
   int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
+  Div32 rt_div, ti_div, tx_div;  // halo kernel: row_tiles, tiles_img, tiles_x
+  // halo forward: source s channel ch of image b starts at byte address
+  // sq0[s] + b * sqb[s] + ch * sr[s]; sm[s] = 0 for broadcast sources, else ~0
+  unsigned long long sq0[kMaxSrc], sqb[kMaxSrc];
+  unsigned sr[kMaxSrc], sm[kMaxSrc];
   unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
+  int dbg;                      // diagnostics with stamps on (env DRO_CONV_DBG): 1 skip the K
+                                // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -465,6 +488,11 @@ struct HaloShape {
 template <int BM, int KH, int KW, int MODE, int ACT, int EPI, int KS>
 __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   using S = HaloShape<BM, KH, KW>;
+  {   // diagnostics: kernel entry of wave 0 (slot 10) and of the block's last wave (slot 11)
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if (a.stamps && (threadIdx.x == 0 || threadIdx.x == blockDim.x - 64))
+      a.stamps[(size_t)blockIdx.x * 16 + (threadIdx.x == 0 ? 10 : 11)] = t0;
+  }
   // staging prefetch distance: 2 chunks when the register budget allows
   // (<= 8 waves per CU); 4 wave groups per block run at 128 VGPRs with 1
   constexpr int PF = KS <= 2 ? 2 : 1;
@@ -487,115 +515,164 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave in the group (scalar)
   float* smem = smem_all + grp * S::LDS;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int rt = tile % a.row_tiles, pt = tile / a.row_tiles;
+  const int pt = (int)udiv((unsigned)tile, a.rt_div), rt = tile - pt * a.row_tiles;
   const int row0 = rt * BM;
-  const int b = pt / a.tiles_img, trem = pt - b * a.tiles_img;
-  const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+  const int b = (int)udiv((unsigned)pt, a.ti_div), trem = pt - b * a.tiles_img;
+  const int tyi = (int)udiv((unsigned)trem, a.tx_div);
+  const int ty0 = tyi * TH, tx0 = (trem - tyi * a.tiles_x) * TW;
   const size_t HW = (size_t)H * W;
   const unsigned HWu = (unsigned)HW;
   const int nck = (kch + CK - 1) / CK;
   const int cbeg = blockIdx.y * a.chunks_per_split;
   const int cend = min(nck, cbeg + a.chunks_per_split);
 
-  // X staging: wave w stages channels w, w+4, ..; lanes run over the halo in
-  // NJ passes whose pixel offsets are chunk independent
-  int xpix[NJ];
-  unsigned xok = 0;
+  // X staging: wave w stages the XPER consecutive channels w*XPER.. of a chunk;
+  // lanes run over the halo in NJ passes whose byte offsets are chunk
+  // independent (lanes outside the image read pixel 0 and are zeroed when staged)
+  unsigned xpb[NJ];
+  bool xok[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int e = lane + 64 * j;
     const int hy = e / HWd, hx = e - hy * HWd;
     const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
-    const bool ok = e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-    xpix[j] = ok ? yy * W + xx : 0;
-    xok |= ok ? (1u << j) : 0u;
+    xok[j] = e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+    xpb[j] = xok[j] ? 4u * (unsigned)(yy * W + xx) : 0u;
   }
   const unsigned wlast = (unsigned)Cout * CinT - 1;
 
+  // Source table in SGPRs (built once): channel ch of source s starts at byte
+  // address sQ[s] + ch * sR[s] (+ 4 * pixel unless broadcast: sM[s] = 0).  Per
+  // channel the staging adds the deltas of the sources the channel has passed
+  // (masks from three compares): scalar arithmetic, no branches, so the loads
+  // share a basic block with the MFMAs
+  unsigned long long sQ[4];
+  unsigned sR[4], sM[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (MODE == 0) {
+      sQ[t] = a.sq0[t] + (unsigned long long)b * a.sqb[t];
+      sR[t] = a.sr[t];
+      sM[t] = a.sm[t];
+    } else {
+      sQ[t] = reinterpret_cast<unsigned long long>(Gp) + 4ull * (unsigned long long)b * Cout * HW;
+      sR[t] = 4u * HWu;
+      sM[t] = ~0u;
+    }
+  }
+  const unsigned long long dQ1 = sQ[1] - sQ[0], dQ2 = sQ[2] - sQ[1], dQ3 = sQ[3] - sQ[2];
+  const unsigned dR1 = sR[1] - sR[0], dR2 = sR[2] - sR[1], dR3 = sR[3] - sR[2];
+  const unsigned dM1 = sM[1] - sM[0], dM2 = sM[2] - sM[1], dM3 = sM[3] - sM[2];
+  const long long yshift = reinterpret_cast<long long>(a.gy) - reinterpret_cast<long long>(Gp);
+
   // MODE 1 with ACT != 0: the activation derivative is folded into G staging
   constexpr bool FOLD = MODE == 1 && ACT != 0;
-  const float* __restrict__ Yp = a.gy;
   const float galpha = a.galpha;
+  // weights are staged as float4 runs (a run never crosses a weight row: RUN %
+  // 4 == 0); starts need only dword alignment; per-thread offsets are chunk
+  // independent.  Tensors of < 4 weights take the flat path (plan_igemm).
+  constexpr int W4 = S::WTOT / 4, WPER4 = (W4 + 255) / 256;
+  constexpr int WREG = 4 * WPER4;
+  static_assert(S::WTOT % 4 == 0 && RUN % 4 == 0, "float4 weight runs");
+  unsigned woff[WPER4];
+  int wdst[WPER4];
+#pragma unroll
+  for (int i = 0; i < WPER4; ++i) {
+    const int e = 4 * (tid + 256 * i);
+    const int run = e / RUN, rem = e - run * RUN;
+    woff[i] = (unsigned)run * CinT + (unsigned)rem;
+    wdst[i] = (W4 % 256 == 0 || e < S::WTOT) ? run * WS + rem : -1;
+  }
   // one chunk's staging registers; with PF == 2 two sets alternate so the
   // loads of chunk c+2 are in flight while chunk c is multiplied
   struct Stage {
-    float xr[XPER * NJ], yr[FOLD ? XPER * NJ : 1], wv[S::WPER];
-    unsigned xmask;
+    float xr[XPER * NJ], yr[FOLD ? XPER * NJ : 1], wv[WREG];
+    unsigned cmask;   // scalar: bit i = channel i of this wave exists
+  };
+  // a chunk's loads: scalar set-up (weight base, one row address per channel),
+  // then NVM independent load items that the MFMA loop can interleave
+  typedef __attribute__((address_space(1))) const char* GPtr;   // global, not flat
+  typedef __attribute__((address_space(1))) const float* GFPtr;
+  struct Rows {
+    unsigned gbase;
+    GPtr rowp[XPER], yrow[XPER];
+    unsigned M[XPER];
+  };
+  constexpr int NVM = WPER4 + XPER * NJ;
+  auto prep = [&](Stage& st, int chunk, Rows& r) {
+    const int c0 = chunk * CK;
+    r.gbase = MODE == 0 ? (unsigned)row0 * CinT + (unsigned)c0 * T : (unsigned)c0 * CinT + (unsigned)row0 * T;
+    unsigned cm = 0;
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int ch = c0 + wave * XPER + i;          // scalar
+      const bool cok = ch < kch;
+      cm |= cok ? (1u << i) : 0u;
+      const int cc = cok ? ch : 0;
+      const unsigned long long k1 = MODE == 0 ? 0ull - (unsigned long long)(cc >= cb1) : 0ull;
+      const unsigned long long k2 = MODE == 0 ? 0ull - (unsigned long long)(cc >= cb2) : 0ull;
+      const unsigned long long k3 = MODE == 0 ? 0ull - (unsigned long long)(cc >= cb3) : 0ull;
+      const unsigned j1 = (unsigned)k1, j2 = (unsigned)k2, j3 = (unsigned)k3;
+      const unsigned long long Q = sQ[0] + (dQ1 & k1) + (dQ2 & k2) + (dQ3 & k3);
+      const unsigned R = sR[0] + (dR1 & j1) + (dR2 & j2) + (dR3 & j3);
+      r.M[i] = sM[0] + (dM1 & j1) + (dM2 & j2) + (dM3 & j3);
+      const unsigned long long rq = Q + (unsigned long long)(unsigned)cc * R;
+      r.rowp[i] = reinterpret_cast<GPtr>(rq);
+      r.yrow[i] = reinterpret_cast<GPtr>(rq + (unsigned long long)yshift);
+    }
+    st.cmask = cm;
+  };
+  auto item = [&](Stage& st, const Rows& r, int k) {
+    if (k < WPER4) {
+      const unsigned g = r.gbase + woff[k];
+      const float4 v = *reinterpret_cast<const float4*>(Wt + (g < wlast - 3 ? g : wlast - 3));
+      st.wv[4 * k] = v.x;
+      st.wv[4 * k + 1] = v.y;
+      st.wv[4 * k + 2] = v.z;
+      st.wv[4 * k + 3] = v.w;
+    } else {
+      const int q = k - WPER4, i = q / NJ, j = q - i * NJ;
+      const unsigned o = xpb[j] & r.M[i];
+      st.xr[q] = *reinterpret_cast<GFPtr>(r.rowp[i] + o);
+      if (FOLD) st.yr[q] = *reinterpret_cast<GFPtr>(r.yrow[i] + o);
+    }
   };
   auto load = [&](Stage& st, int chunk) {
-    float(&xr)[XPER * NJ] = st.xr;
-    float(&yr)[FOLD ? XPER * NJ : 1] = st.yr;
-    float(&wv)[S::WPER] = st.wv;
-    unsigned& xmask = st.xmask;
-    const int c0 = chunk * CK;
-    // weights first (no descriptor needed), then every channel's source
-    // descriptor (independent scalar loads, one wait), then the input patch:
-    // decoding a descriptor next to its own loads serialised the chunk on one
-    // scalar round trip per channel
-    const unsigned gbase = MODE == 0 ? (unsigned)row0 * CinT + (unsigned)c0 * T
-                                     : (unsigned)c0 * CinT + (unsigned)row0 * T;
+    Rows r;
+    prep(st, chunk, r);
 #pragma unroll
-    for (int i = 0; i < S::WPER; ++i) {
-      const int e = tid + 256 * i;
-      const int run = e / RUN, rem = e - run * RUN;
-      const unsigned g = gbase + (unsigned)run * CinT + (unsigned)rem;
-      wv[i] = Wt[g < wlast ? g : wlast];
-    }
-    const float* ps[XPER];
-    unsigned sb[XPER];
-    bool Ms[XPER], cok[XPER];
-#pragma unroll
-    for (int i = 0; i < XPER; ++i) {
-      const int ch = c0 + wave + 4 * i;          // scalar
-      cok[i] = ch < kch;
-      if (MODE == 0) {
-        const RowDesc d = row_desc(cb1, cb2, cb3, cok[i] ? ch : 0, HWu);
-        ps[i] = d.p;
-        sb[i] = (unsigned)b * d.A + d.Bc;
-        Ms[i] = d.M;
-      } else {
-        ps[i] = Gp;
-        sb[i] = ((unsigned)b * (unsigned)Cout + (unsigned)(cok[i] ? ch : 0)) * HWu;
-        Ms[i] = true;
-      }
-    }
-    xmask = 0;
-#pragma unroll
-    for (int i = 0; i < XPER; ++i) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const bool ok = cok[i] && ((xok >> j) & 1u);
-        xmask |= ok ? (1u << (i * NJ + j)) : 0u;
-        const unsigned off = ok ? sb[i] + (Ms[i] ? (unsigned)xpix[j] : 0u) : 0u;
-        xr[i * NJ + j] = ps[i][off];
-        if (FOLD) yr[i * NJ + j] = Yp[off];
-      }
-    }
+    for (int k = 0; k < NVM; ++k) item(st, r, k);
   };
   auto store = [&](const Stage& st, int buf) {
     const float(&xr)[XPER * NJ] = st.xr;
     const float(&yr)[FOLD ? XPER * NJ : 1] = st.yr;
-    const float(&wv)[S::WPER] = st.wv;
-    const unsigned xmask = st.xmask;
+    const float(&wv)[WREG] = st.wv;
     float* Ws = smem + buf * STAGE;
-    float* Xs = Ws + WSZ;
+    float* Xs = Ws + WSZ + wave * XPER * HPAD + lane;
+    auto xval = [&](int i, int j) {
+      float v = (((st.cmask >> i) & 1u) && xok[j]) ? xr[i * NJ + j] : 0.f;
+      if (MODE == 1) v *= galpha;
+      if (FOLD) v *= act_bwd(yr[i * NJ + j], ACT);
+      return v;
+    };
+    constexpr int JF = NJ * 64 <= HPAD ? NJ : NJ - 1;   // passes that fit the channel stride
 #pragma unroll
     for (int i = 0; i < XPER; ++i) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int cl = wave + 4 * i, e = lane + 64 * j;
-        float v = (xmask >> (i * NJ + j)) & 1u ? xr[i * NJ + j] : 0.f;
-        if (MODE == 1) v *= galpha;
-        if (FOLD) v *= act_bwd(yr[i * NJ + j], ACT);
-        if (e < HPAD) Xs[cl * HPAD + e] = v;
-      }
+      for (int j = 0; j < JF; ++j) Xs[i * HPAD + 64 * j] = xval(i, j);
+    }
+    if (JF < NJ && lane + 64 * (NJ - 1) < HPAD) {
+#pragma unroll
+      for (int i = 0; i < XPER; ++i) Xs[i * HPAD + 64 * (NJ - 1)] = xval(i, NJ - 1);
     }
 #pragma unroll
-    for (int i = 0; i < S::WPER; ++i) {
-      const int e = tid + 256 * i;
-      if (S::WTOT % 256 == 0 || e < S::WTOT) {
-        const int run = e / RUN, rem = e - run * RUN;
-        Ws[run * WS + rem] = wv[i];
+    for (int i = 0; i < WPER4; ++i) {
+      if (W4 % 256 == 0 || wdst[i] >= 0) {
+        float* d = Ws + wdst[i];   // odd row stride: 4 dword writes
+        d[0] = wv[4 * i];
+        d[1] = wv[4 * i + 1];
+        d[2] = wv[4 * i + 2];
+        d[3] = wv[4 * i + 3];
       }
     }
   };
@@ -622,42 +699,77 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   const int nit = (cend - cbeg + KS - 1) / KS;
   auto chunk_of = [&](int it) { return cbeg + it * KS + grp; };
   unsigned long long* const stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 16 : nullptr;
-  auto stamp = [&](int k) {
-    if (stp && threadIdx.x == 0 && k < 16) stp[k] = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int k) {   // slots: 10/11 entry, 0 set-up done, 12 first chunk staged, 1
+                                // prologue, 2.. K iterations (<= 8), 13 reductions, 14 epilogue
+    if (stp && threadIdx.x == 0 && k < 15) stp[k] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
-  auto mma = [&](int buf) {
+  // slot 15: start of the block's last wave (intra-block launch spread)
+  if (stp && threadIdx.x == blockDim.x - 64) stp[15] = __builtin_amdgcn_s_memtime();
+  // MFMAs over one staged chunk; with `st` the next chunk's load items are
+  // issued one after each MFMA (sched_barrier keeps MFMAs and global loads in
+  // this order and lets LDS reads / ALU move): issued as a burst ahead of the
+  // MFMAs, the loads of all 16 waves queued at the texture unit and held every
+  // wave's first MFMA back (profiles/r1_conv_phase_stamps.txt)
+  auto mma_ld = [&](int buf, Stage* st, const Rows* r) {
     const float* wa = smem + buf * STAGE + abase;
     const float* xb = smem + buf * STAGE + WSZ + bbase;
+    constexpr int NMF = T * NS, PD = 2;   // MFMAs per chunk; LDS operand prefetch distance
+    auto aoff = [](int k) { return (k / NS) + (k % NS) * ASTEP; };
+    auto boff = [](int k) {
+      const int tap = k / NS, s = k % NS, ty = tap / KW, tx = tap % KW;
+      return (MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx)) + 2 * s * HPAD;
+    };
+    float av[PD + 1], bv[PD + 1];
 #pragma unroll
-    for (int ty = 0; ty < KH; ++ty) {
+    for (int k = 0; k < PD && k < NMF; ++k) {
+      av[k] = wa[aoff(k)];
+      bv[k] = xb[boff(k)];
+    }
 #pragma unroll
-      for (int tx = 0; tx < KW; ++tx) {
-        const int tap = ty * KW + tx;
-        const int toff = MODE == 0 ? ty * HWd + tx : (KH - 1 - ty) * HWd + (KW - 1 - tx);
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          acc = mfma32(wa[tap + s * ASTEP], xb[toff + 2 * s * HPAD], acc);
+    for (int k = 0; k < NMF; ++k) {
+      if (k + PD < NMF) {
+        av[(k + PD) % (PD + 1)] = wa[aoff(k + PD)];
+        bv[(k + PD) % (PD + 1)] = xb[boff(k + PD)];
+      }
+      acc = mfma32(av[k % (PD + 1)], bv[k % (PD + 1)], acc);
+      if (st) {
+        if (k < NVM) item(*st, *r, k);
+        // MFMAs, LDS reads and global loads stay in this order; ALU may move
+        __builtin_amdgcn_sched_barrier(0x0006);
       }
     }
+    if (st) {
+#pragma unroll
+      for (int k = NMF; k < NVM; ++k) item(*st, *r, k);
+    }
   };
+  auto mma = [&](int buf) { mma_ld(buf, nullptr, nullptr); };
   Stage sa, sb;
   if (chunk_of(0) < cend) {
     load(sa, chunk_of(0));
     store(sa, 0);
   }
+  stamp(12);   // wave 0's first chunk landed in LDS
   if (PF == 2 && chunk_of(1) < cend) load(sb, chunk_of(1));
   __syncthreads();
   stamp(1);
+  const int dbg = a.dbg;
   if (PF == 1) {
     for (int it = 0; it < nit; ++it) {
       const int buf = it & 1;
       const bool more = chunk_of(it + 1) < cend;
-      if (more) load(sa, chunk_of(it + 1));
-      if (KS == 1 || chunk_of(it) < cend) mma(buf);
-      if (more) store(sa, buf ^ 1);
+      if (more && !(dbg & 3)) {
+        Rows r;
+        prep(sa, chunk_of(it + 1), r);
+        mma_ld(buf, &sa, &r);
+      } else {
+        if (more && !(dbg & 1)) load(sa, chunk_of(it + 1));
+        if ((KS == 1 || chunk_of(it) < cend) && !(dbg & 2)) mma(buf);
+      }
+      if (more && !(dbg & 4)) store(sa, buf ^ 1);
       __syncthreads();
-      stamp(2 + it);
+      if (it < 8) stamp(2 + it);
     }
   } else {
     // registers: sb holds chunk it+1 (stored into LDS at the end of
@@ -667,13 +779,13 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       if (chunk_of(it) < cend) mma(0);
       if (chunk_of(it + 1) < cend) store(sb, 1);
       __syncthreads();
-      stamp(2 + it);
+      if (it < 8) stamp(2 + it);
       if (it + 1 >= nit) break;
       if (chunk_of(it + 3) < cend) load(sb, chunk_of(it + 3));
       if (chunk_of(it + 1) < cend) mma(1);
       if (chunk_of(it + 2) < cend) store(sa, 0);
       __syncthreads();
-      stamp(3 + it);
+      if (it < 7) stamp(3 + it);
     }
   }
   // Reduction + epilogue spread over ALL waves of the block: every wave parks
@@ -1156,6 +1268,13 @@ using namespace dro;
 
 namespace {
 
+Div32 make_div32(int d) {
+  Div32 f;
+  f.d = (unsigned)(d > 0 ? d : 1);
+  f.m = 0xFFFFFFFFu / f.d;
+  return f;
+}
+
 FastDiv make_fdiv(int d) {
   FastDiv f;
   f.one = d == 1;
@@ -1192,7 +1311,8 @@ void halo_fill(IgPlan& pl) {
 IgPlan plan_igemm(int rows, int kch, int KH, int KW, int B, int H, int W) {
   const bool shape_ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3) ||
                         (KH == 1 && KW == 1);
-  if (!shape_ok) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
+  // the halo kernel stages weights as float4 runs: tensors of < 4 weights go flat
+  if (!shape_ok || (long long)rows * kch * KH * KW < 4) return plan_igemm_flat(rows, kch, KH, KW, B, H, W);
   IgPlan pl = {};
   const long long P = (long long)B * H * W;
   pl.halo = true;
@@ -1417,6 +1537,11 @@ template <int MODE, int ACT, int EPI>
 int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   const IgPlan pl = plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
   a.stamps = g_conv_stamps;
+  a.dbg = 0;
+  if (g_conv_stamps) {
+    const char* e = getenv("DRO_CONV_DBG");
+    a.dbg = e ? atoi(e) : 0;
+  }
   a.K = a.kch * a.g.KH * a.g.KW;
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
@@ -1430,6 +1555,22 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.tiles_x = pl.tiles_x;
     a.tiles_img = pl.tiles_img;
     a.CK = pl.CK;
+    a.rt_div = make_div32(pl.row_tiles);
+    a.ti_div = make_div32(pl.tiles_img);
+    a.tx_div = make_div32(pl.tiles_x);
+    if (MODE == 0) {
+      const unsigned long long HWl = (unsigned long long)a.g.H * a.g.W;
+      for (int t = 0; t < kMaxSrc; ++t) {
+        const Slice& sl = a.src[t];
+        const unsigned long long chs = sl.bcast ? 1ull : HWl;
+        const long long cbt = t == 0 ? 0 : a.cbase[t];
+        a.sq0[t] = reinterpret_cast<unsigned long long>(sl.p) +
+                   4ull * (unsigned long long)(((long long)sl.coff - cbt) * (long long)chs);
+        a.sqb[t] = 4ull * (unsigned long long)sl.ctot * chs;
+        a.sr[t] = 4u * (unsigned)chs;
+        a.sm[t] = sl.bcast ? 0u : ~0u;
+      }
+    }
     const int KH = a.g.KH;
     const int KW = a.g.KW;
 #define DRO_DCONV(BM_, KH_, KW_)                                                                    \

@@ -60,7 +60,15 @@ def run(name, B, hd, H, W, cins, KH, KW, gates=True, reps=5):
     print(f"== {name}: {s.shape[0]} blocks")
     start = (s[:, 0] - t0).float()
     print(f"   block start: min 0  median {start.median():.0f}  max {start.max():.0f} cycles")
-    cols = [k for k in range(1, 15) if bool((s[:, k] > 0).all())]
+    setup = (s[:, 0] - s[:, 10]).float()
+    espread = (s[:, 11] - s[:, 10]).float()
+    print(f"   wave 0 set-up {setup.median():.0f} cycles; last wave enters {espread.median():.0f}"
+          f" (max {espread.max():.0f}) after wave 0")
+    spread = (s[:, 15] - s[:, 0]).float()
+    staged = (s[:, 12] - s[:, 0]).float()
+    print(f"   last wave starts {spread.median():.0f} (max {spread.max():.0f}) cycles after wave 0;"
+          f" wave 0's first chunk staged after {staged.median():.0f}")
+    cols = [k for k in (1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 14) if bool((s[:, k] > 0).all())]
     prev = s[:, 0]
     for k in cols:
         d = (s[:, k] - prev).float()
@@ -71,7 +79,14 @@ def run(name, B, hd, H, W, cins, KH, KW, gates=True, reps=5):
     print(f"   last block done at {end.max():.0f} cycles after the first start")
 
 
-if __name__ == "__main__":
+def main():
     run("gates 1x5 (roofline shape)", 2, 64, 24, 80, (32, 63, 1), 1, 5, gates=True)
     run("relu 1x1 Cin 128 -> 64", 2, 64, 24, 80, (64,), 1, 1, gates=False)
     run("relu 3x3 Cin 128 -> 64", 2, 64, 24, 80, (64,), 3, 3, gates=False)
+
+
+if __name__ == "__main__":
+    for dbg in os.environ.get("STAMP_DBG", "0").split(","):
+        os.environ["DRO_CONV_DBG"] = dbg
+        print(f"######## DRO_CONV_DBG={dbg} (1 no loads, 2 no MFMA, 4 no LDS stores in the K loop)")
+        main()

@@ -45,6 +45,7 @@ for step in "$@"; do
     convkin) for k in 1 2 4; do run "bench_conv_kin$k" 300 env DRO_CONV_KIN=$k python tools/bench_conv.py --iters 30; done ;;
     stampkin) for k in 1 2 4; do run "conv_stamps_kin$k" 300 env DRO_CONV_KIN=$k python tools/conv_stamps.py; done ;;
     kinthr) for t in 512 1024 2048; do run "bench_kin2_below$t" 600 env DRO_CONV_KIN2_BELOW=$t python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline; done ;;
+    stampdbg) run conv_stamps_dbg 300 env STAMP_DBG=${STAMP_DBG:-0,1,2,4,3,5} python tools/conv_stamps.py ;;
     tprof) run torch_prof 600 python tools/torch_prof.py ;;
     pmcsq) run pmc_sq 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python bench.py --roofline-only ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
