@@ -389,6 +389,8 @@ def main():
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",
                     help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
+    ap.add_argument("--no-fused-bn", action="store_true",
+                    help="encoder BatchNorm+ReLU through PyTorch's kernels (A/B)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
@@ -409,6 +411,8 @@ def main():
     _update.set_conv_backend(args.conv_backend)
     from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
     _dpn.set_concurrent_encoders(args.concurrent_encoders)
+    from dro_sfm_amd.networks.optim import extractor as _extractor
+    _extractor.set_fused_batchnorm(not args.no_fused_bn)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -466,6 +470,7 @@ def main():
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_convs": args.conv_backend,
                    "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
+                   "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},
         "final_loss": round(float(loss), 6),

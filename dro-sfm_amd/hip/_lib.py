@@ -52,6 +52,9 @@ def load():
     _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, P, P, S)
     _sig(lib.dro_bilinear_upsample2x_forward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_bilinear_upsample2x_backward, P, ctypes.c_longlong, I, I, P, S)
+    _sig(lib.dro_batchnorm_workspace_bytes, I, I, I, restype=Z)
+    _sig(lib.dro_batchnorm_relu_forward, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P, P, P, Z, S)
+    _sig(lib.dro_batchnorm_relu_backward, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, Z, S)
     _sig(lib.dro_conv2d_workspace_bytes, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_plan, I, I, I, I, I, I, I, P)
     _sig(lib.dro_debug_conv_stamps, P)
@@ -76,6 +79,7 @@ EXPORTED = (
     "dro_supervised_workspace_bytes", "dro_supervised_forward", "dro_supervised_backward",
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
+    "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",

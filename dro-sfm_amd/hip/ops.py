@@ -331,3 +331,63 @@ def bilinear_upsample2x(x):
     if x.dtype != torch.float32 or x.dim() != 4:
         raise RuntimeError("bilinear_upsample2x: expects a float32 NCHW tensor")
     return _Bilinear2x.apply(x)
+
+
+class _BatchNormAct(torch.autograd.Function):
+    """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, skip, running_mean, running_var, num_batches, relu, eps,
+                momentum):
+        lib = _lib.load()
+        require_device(x, what="batchnorm_act")
+        N, C, H, W = x.shape
+        x = x.contiguous()
+        skip = skip.contiguous() if skip is not None else None
+        y = torch.empty_like(x)
+        smean = torch.empty(C, device=x.device, dtype=torch.float32)
+        sinv = torch.empty(C, device=x.device, dtype=torch.float32)
+        nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        check(lib.dro_batchnorm_relu_forward(
+            ptr(x), ptr(weight), ptr(bias), ptr(skip), int(relu), N, C, H * W, float(eps),
+            float(momentum), ptr(running_mean), ptr(running_var), ptr(num_batches), ptr(y),
+            ptr(smean), ptr(sinv), ptr(ws), nws, stream_of(x)), "dro_batchnorm_relu_forward")
+        ctx.save_for_backward(x, y, weight, smean, sinv)
+        ctx.relu, ctx.has_skip = int(relu), skip is not None
+        ctx.affine = (weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = _lib.load()
+        x, y, weight, smean, sinv = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gy = gy.contiguous()
+        gx = torch.empty_like(x)
+        gw = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[0] else None
+        gb = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[1] else None
+        gs = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
+        nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        check(lib.dro_batchnorm_relu_backward(
+            ptr(gy), ptr(x), ptr(y), ptr(weight), ptr(smean), ptr(sinv), ctx.relu, N, C, H * W,
+            ptr(gx), ptr(gw), ptr(gb), ptr(gs), ptr(ws), nws, stream_of(gy)),
+            "dro_batchnorm_relu_backward")
+        return gx, gw, gb, gs, None, None, None, None, None, None
+
+
+def batchnorm_act(x, bn, skip=None, relu=True):
+    """act(bn(x) + skip) for a training-mode nn.BatchNorm2d `bn` (float32 NCHW):
+    torch.nn.functional.batch_norm(training=True) semantics, including the
+    running-statistics update and num_batches_tracked (reference
+    networks/optim/extractor.py:7-107 via torchvision's BasicBlock)."""
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("batchnorm_act: expects a float32 NCHW tensor")
+    if bn.momentum is None:
+        raise NotImplementedError("batchnorm_act: cumulative averaging (momentum=None)")
+    track = bn.track_running_stats and bn.running_mean is not None
+    return _BatchNormAct.apply(
+        x, bn.weight, bn.bias, skip, bn.running_mean if track else None,
+        bn.running_var if track else None, bn.num_batches_tracked if track else None,
+        1 if relu else 0, bn.eps, bn.momentum)

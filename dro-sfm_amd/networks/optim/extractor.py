@@ -7,10 +7,12 @@ upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  The convolutions run on
 MIOpen (SURVEY.md §8(f) ranks a fused encoder as the next step); pretrained
 ImageNet weights are never downloaded -- load a checkpoint instead.
 
-Batch normalisation runs on PyTorch's native kernels, not MIOpen: measured on
-MI355X (tools/diag_miopen2.py), MIOpen's training-mode BN (one-pass variance)
-put 1e-2 relative error on encoder gradients against the fp64 oracle, while
-the native kernels stay at the fp32 floor (~1e-3 through the recurrent net).
+Training-mode batch normalisation runs fused with the ReLU / residual add that
+follows it (hip.batchnorm_act, csrc/batchnorm.hip: two launches each way with
+fixed-order fp64 statistics, against 6-9 PyTorch launches per site).  Not
+MIOpen's BN: measured on MI355X (tools/diag_miopen2.py), its one-pass
+variance put 1e-2 relative error on encoder gradients against the fp64
+oracle.  Eval mode and CPU tensors use PyTorch's native kernels.
 The 2x bilinear upsampling of the fusion head is a HIP kernel
 (hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.
 """
@@ -21,12 +23,29 @@ import torch.nn.functional as F
 from ... import hip
 
 
+_FUSED_BN = [True]
+
+
+def set_fused_batchnorm(enabled):
+    """hip.batchnorm_act for training-mode BN+ReLU on the GPU (default True)."""
+    _FUSED_BN[0] = bool(enabled)
+
+
 class BatchNorm2d(nn.BatchNorm2d):
     """nn.BatchNorm2d (same state_dict) computed by the native kernels."""
 
     def forward(self, x):
         with torch.backends.cudnn.flags(enabled=False):
             return super().forward(x)
+
+    def act(self, x, skip=None, relu=True):
+        """relu(bn(x) + skip): one fused op in training mode on the GPU."""
+        if _FUSED_BN[0] and self.training and x.is_cuda and self.momentum is not None:
+            return hip.batchnorm_act(x, self, skip=skip, relu=relu)
+        y = self(x)
+        if skip is not None:
+            y = y + skip
+        return F.relu(y, inplace=True) if relu else y
 
 
 class BasicBlock(nn.Module):
@@ -44,10 +63,12 @@ class BasicBlock(nn.Module):
                                             BatchNorm2d(cout))
 
     def forward(self, x):
-        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        y = self.bn2(self.conv2(y))
-        skip = x if self.downsample is None else self.downsample(x)
-        return F.relu(y + skip, inplace=True)
+        y = self.bn1.act(self.conv1(x))
+        if self.downsample is None:
+            skip = x
+        else:
+            skip = self.downsample[1].act(self.downsample[0](x), relu=False)
+        return self.bn2.act(self.conv2(y), skip=skip)
 
 
 def _stage(cin, cout, stride):
@@ -90,7 +111,7 @@ class ResNetEncoder(nn.Module):
         if isinstance(x, (list, tuple)):
             chunks = len(x)
             x = torch.cat(list(x), 0)
-        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x)), inplace=True), 3, 2, 1)
+        x = F.max_pool2d(self.bn1.act(self.conv1(x)), 3, 2, 1)
         s4 = self.layer1(x)
         s8 = self.layer2(s4)
         x = self.layer3(s8)

@@ -170,6 +170,33 @@ int dro_bilinear_upsample2x_forward(const float* x, long long planes, int h, int
 int dro_bilinear_upsample2x_backward(const float* grad_out, long long planes, int h, int w,
                                      float* grad_x, void* stream);
 
+/* Training-mode BatchNorm2d fused with the ReLU / residual add that follows it
+ * in the ResNet-18 encoders (networks/optim/extractor.py:7-107 of the reference;
+ * BasicBlock: relu(bn(conv(x)) [+ skip])).  Replaces torch.nn.functional.
+ * batch_norm(training=True, momentum) + relu: y = act((x - mean) * invstd *
+ * gamma + beta + skip) with biased batch variance; running_mean / running_var
+ * (nullable together) move by `momentum` toward the batch mean / unbiased
+ * variance; *num_batches_tracked (nullable) is incremented.  x, y, skip: NCHW
+ * [N, C, HW]; save_mean / save_invstd [C] feed the backward.  Two launches each
+ * way, fixed-order fp64 reductions (deterministic).  `workspace` holds
+ * dro_batchnorm_workspace_bytes(N, C, HW) bytes; relu is 0 or 1.
+ * Backward: grad_x = gamma * invstd * (g - mean(g) - xhat * mean(g * xhat)) with
+ * g = grad_out * [y > 0] (relu) or grad_out; grad_gamma = sum(g * xhat),
+ * grad_beta = sum(g), grad_skip = g (each nullable). */
+size_t dro_batchnorm_workspace_bytes(int N, int C, int HW);
+int dro_batchnorm_relu_forward(const float* x, const float* gamma, const float* beta,
+                               const float* skip, int relu, int N, int C, int HW, float eps,
+                               float momentum, float* running_mean, float* running_var,
+                               long long* num_batches_tracked, float* y, float* save_mean,
+                               float* save_invstd, void* workspace, size_t workspace_bytes,
+                               void* stream);
+int dro_batchnorm_relu_backward(const float* grad_out, const float* x, const float* y,
+                                const float* gamma, const float* save_mean,
+                                const float* save_invstd, int relu, int N, int C, int HW,
+                                float* grad_x, float* grad_gamma, float* grad_beta,
+                                float* grad_skip, void* workspace, size_t workspace_bytes,
+                                void* stream);
+
 /* ------------------------------------------------------------------------
  * Stride-1 'same' convolutions on f32 MFMA for the recurrent update blocks.
  * Replace the nn.Conv2d + activation + torch.cat chains of
