@@ -116,7 +116,7 @@ struct BnFwdArgs {
 // grid (blocks per plane, N * C)
 template <bool VEC>
 __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(BnFwdArgs a, BnGeom g) {
-  __shared__ float coef[2];
+  __shared__ float coef[3];
   const int plane = blockIdx.y, c = plane % g.C;
   if (threadIdx.x == 0) {
     const long long L = (long long)g.N * g.HW;
@@ -126,8 +126,11 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(BnFwdArgs a, BnGeo
     var = var > 0.0 ? var : 0.0;
     const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
     const float gm = a.gamma ? a.gamma[c] : 1.f;
-    coef[0] = gm * invstd;                                   // y = x * k + (beta - mean * k)
-    coef[1] = (a.beta ? a.beta[c] : 0.f) - (float)mean * gm * invstd;
+    // y = (x - mean) * (gamma * invstd) + beta: centre first (x * k + (beta - mean * k)
+    // cancels catastrophically when |mean| >> std)
+    coef[0] = gm * invstd;
+    coef[1] = a.beta ? a.beta[c] : 0.f;
+    coef[2] = (float)mean;
     if (plane < g.C && blockIdx.x == 0) {                    // first block of the channel (n == 0)
       a.save_mean[c] = (float)mean;
       a.save_invstd[c] = invstd;
@@ -140,10 +143,10 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(BnFwdArgs a, BnGeo
     }
   }
   __syncthreads();
-  const float k = coef[0], o = coef[1];
+  const float k = coef[0], o = coef[1], mu = coef[2];
   const long long base = (long long)plane * g.HW;
   auto f = [&](float v, float s) {
-    float r = fmaf(v, k, o) + s;
+    float r = fmaf(v - mu, k, o) + s;
     return a.relu ? fmaxf(r, 0.f) : r;
   };
   const int hw4 = g.HW & ~3;
