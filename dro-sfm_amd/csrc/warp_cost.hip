@@ -38,6 +38,7 @@ struct WarpArgs {
   int do_scale;
   int B, N, C, h, w;
   int reduce_mean;
+  int acc_fmap;      // backward: add into grad_fmap
 };
 
 __device__ __forceinline__ void cams(const WarpArgs& a, int b, float ki[9], float kr[9]) {
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
     float* out = gfmap + ((size_t)b * a.C + c0) * P + p;
 #pragma unroll
     for (int c = 0; c < kCPT; ++c)
-      if (c < cn) out[(size_t)c * P] = gf[c];
+      if (c < cn) out[(size_t)c * P] = a.acc_fmap ? out[(size_t)c * P] + gf[c] : gf[c];
   }
 }
 
@@ -343,6 +344,7 @@ static WarpArgs make_args(const float* fmap, const float* fmap_ref, const float*
                           const float* ref_K, float scale, const float* pose, int pose_mode, int B,
                           int N, int C, int h, int w, int reduce_mean) {
   WarpArgs a;
+  a.acc_fmap = 0;
   a.fmap = fmap;
   a.fmap_ref = fmap_ref;
   a.depth = depth;
@@ -403,7 +405,8 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
                                       const float* pose, int pose_mode, int B, int N, int C,
                                       int h, int w, int reduce_mean, const float* grad_cost,
                                       float* grad_fmap, float* grad_fmap_ref, float* grad_depth,
-                                      float* grad_pose, void* workspace, void* stream) {
+                                      float* grad_pose, int accumulate, void* workspace,
+                                      void* stream) {
   int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, N, C, h, w);
   if (st) return st;
   if (!depth || !grad_cost) {
@@ -418,11 +421,18 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
   hipStream_t s = (hipStream_t)stream;
   WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
                          pose, pose_mode, B, N, C, h, w, reduce_mean);
+  if (accumulate < 0 || accumulate > 3) {
+    set_error("warp_cost_backward: accumulate must be 0..3");
+    return DRO_E_MODE;
+  }
+  a.acc_fmap = accumulate & 1;
   const int P = h * w;
   float* gxy = geo ? (float*)workspace : nullptr;
   const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
   float* partial = (geo && grad_pose) ? gxy + (size_t)N * B * P * 2 : nullptr;
-  if (grad_fmap_ref && (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s))) return st;
+  if (grad_fmap_ref && !(accumulate & 2) &&
+      (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s)))
+    return st;
   if (gxy && (st = launch_zero(gxy, (size_t)N * B * P * 2, s))) return st;
   if (grad_fmap || grad_fmap_ref || gxy) {
     dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);

@@ -38,7 +38,7 @@ def load():
     _sig(lib.dro_warp_cost_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, P, S)
     _sig(lib.dro_warp_cost_workspace_bytes, I, I, I, I, restype=Z)
     _sig(lib.dro_warp_cost_backward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I,
-         P, P, P, P, P, P, S)
+         P, P, P, P, P, I, P, S)
     _sig(lib.dro_plane_sweep_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, P, S)
     _sig(lib.dro_photometric_workspace_bytes, I, I, I, I, I, restype=Z)
     _sig(lib.dro_photometric_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I,

@@ -37,6 +37,7 @@ import torch
 
 from . import _lib
 from ._lib import check, ptr, require_device, stream_of
+from .ops import _sink_of
 
 ACT = {None: 0, "none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
 
@@ -433,6 +434,7 @@ class _SepGRUHalf(torch.autograd.Function):
                                             ptr(q), ptr(hn), hd, 0, ptr(wsq), nwsq, st),
               "dro_convgru_blend_forward")
         ctx.save_for_backward(h, rh, wzr, wq, zr, q, *xs)
+        ctx.sinks = [_sink_of(x) for x in xs]
         ctx.scope = scope
         ctx.direct = direct
         ctx.keys = (key, ("q", wq.data_ptr()))
@@ -456,13 +458,19 @@ class _SepGRUHalf(torch.autograd.Function):
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(1)")
         # candidate conv over [r*h, x]: d(r*h), dx (overwrite), dWq, dbq
         drh = torch.empty_like(h)
-        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[9 + i] else None
-               for i, x in enumerate(xs)]
+        # sources with a gradient sink (hip.grad_sink) are accumulated in place and
+        # get None from autograd; the others get fresh buffers
+        sinks = [s if need[9 + i] else None for i, s in enumerate(ctx.sinks)]
+        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[9 + i] and sinks[i] is None
+               else None for i, x in enumerate(xs)]
+        tg = [s if s is not None else d for s, d in zip(sinks, dxs)]
+        qacc0 = [0] + [1 if s is not None else 0 for s in sinks]
         if ctx.direct is not None:
-            return _SepGRUHalf._backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs)
+            return _SepGRUHalf._backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs,
+                                                tg, qacc0)
         gwq, gbq, qacc, qfirst = _grad_buffers(ctx.scope, ctx.keys[1], wq, hd, h.device)
-        ptrs, ctot, coff = _grad_targets([drh, *dxs])
-        acc = (ctypes.c_int * n)()
+        ptrs, ctot, coff = _grad_targets([drh, *tg])
+        acc = (ctypes.c_int * n)(*qacc0)
         ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq.contiguous()), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
@@ -472,7 +480,7 @@ class _SepGRUHalf(torch.autograd.Function):
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
         # gate conv over [h, x]: dh, dx accumulate; dWz|dWr, dbz|dbr
         gwzr, gbzr, zacc, zfirst = _grad_buffers(ctx.scope, ctx.keys[0], wzr, 2 * hd, h.device)
-        ptrs, ctot, coff = _grad_targets([dh, *dxs])
+        ptrs, ctot, coff = _grad_targets([dh, *tg])
         acc = (ctypes.c_int * n)(*([1] * n))
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
@@ -483,7 +491,7 @@ class _SepGRUHalf(torch.autograd.Function):
         return (dh if need[0] else None, *gz, *gq, None, None, *dxs)
 
     @staticmethod
-    def _backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs):
+    def _backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs, tg, qacc0):
         """Data-gradient chain on the current stream; dWq/dbq and dWz|r/dbz|r
         accumulate into the flat .grad views on the side stream."""
         B, hd, H, W = h.shape
@@ -494,8 +502,8 @@ class _SepGRUHalf(torch.autograd.Function):
         (_, _), (gwzr, gbzr), (gwq, gbq) = ctx.direct
         main = torch.cuda.current_stream()
         drh = torch.empty_like(h)
-        ptrs, ctot, coff = _grad_targets([drh, *dxs])
-        acc = (ctypes.c_int * n)()
+        ptrs, ctot, coff = _grad_targets([drh, *tg])
+        acc = (ctypes.c_int * n)(*qacc0)
         ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
@@ -512,7 +520,7 @@ class _SepGRUHalf(torch.autograd.Function):
                       "dro_conv2d_backward(q weight)")
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
-        ptrs, ctot, coff = _grad_targets([dh, *dxs])
+        ptrs, ctot, coff = _grad_targets([dh, *tg])
         acc = (ctypes.c_int * n)(*([1] * n))
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,

@@ -37,6 +37,51 @@ def _disp_range(min_depth, max_depth):
 
 
 # ------------------------------------------------------------------------- warp + feature cost
+class _GradSink(torch.autograd.Function):
+    """Identity whose gradient is a buffer that consumers add into in place.
+
+    A tensor read by many ops of one step (the feature maps of every cost call,
+    the context features of every GRU step) otherwise gets one gradient per
+    use and autograd sums them with one add launch each.  Ops that know the
+    sink (hip.warp_cost, hip.sepconvgru_half) accumulate straight into it and
+    return None; autograd runs this node only after all of them, so the buffer
+    is complete when it is handed on (plus any gradient other ops returned)."""
+
+    @staticmethod
+    def forward(ctx, x, buf):
+        ctx.buf = buf
+        ctx.set_materialize_grads(False)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (ctx.buf if g is None else ctx.buf + g), None
+
+
+_SINKS = [True]
+
+
+def set_grad_sinks(enabled):
+    """grad_sink on (default) / off (identity; autograd sums per use) for A/B runs."""
+    _SINKS[0] = bool(enabled)
+
+
+def grad_sink(x):
+    """x (aliased) with an in-place gradient sink; x itself when no gradient flows.
+    One backward per forward: the buffer is zeroed here, in the forward."""
+    if not (_SINKS[0] and torch.is_grad_enabled() and x.requires_grad and x.is_cuda
+            and x.is_contiguous()):
+        return x
+    buf = torch.zeros_like(x, memory_format=torch.contiguous_format)
+    y = _GradSink.apply(x, buf)
+    y._dro_gsink = buf
+    return y
+
+
+def _sink_of(t):
+    return getattr(t, "_dro_gsink", None)
+
+
 class _WarpCost(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale,
@@ -50,6 +95,7 @@ class _WarpCost(torch.autograd.Function):
                                "depth [B,1,h,w], K [B,3,3])")
         pose_flat, pose_mode, restore = _pose_layout(pose, (N, B))
         require_device(pose_flat, what="warp_cost")
+        sinks = (_sink_of(fmap), _sink_of(fmap_ref))
         fmap, fmap_ref, depth = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous()
         K, ref_K = K.contiguous(), ref_K.contiguous()
         out_shape = (B, C, h, w) if reduce_mean else (N, B, C, h, w)
@@ -59,6 +105,7 @@ class _WarpCost(torch.autograd.Function):
                                         ptr(pose_flat), pose_mode, B, N, C, h, w, int(reduce_mean),
                                         ptr(cost), stream_of(fmap)), "dro_warp_cost_forward")
         ctx.save_for_backward(fmap, fmap_ref, depth, pose_flat, K, ref_K)
+        ctx.sinks = sinks
         ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode, int(reduce_mean))
         ctx.restore = restore
         return cost
@@ -72,8 +119,11 @@ class _WarpCost(torch.autograd.Function):
         N = fmap_ref.shape[0]
         need = ctx.needs_input_grad
         gcost = gcost.contiguous()
-        g_f = torch.empty_like(fmap) if need[0] else None
-        g_r = torch.empty_like(fmap_ref) if need[1] else None
+        # feature maps shared by all cost calls of a step: summed in their sinks
+        sf, sr = ctx.sinks
+        g_f = (sf if sf is not None else torch.empty_like(fmap)) if need[0] else None
+        g_r = (sr if sr is not None else torch.empty_like(fmap_ref)) if need[1] else None
+        accumulate = (1 if sf is not None else 0) | (2 if sr is not None else 0)
         g_d = torch.empty_like(depth) if need[2] else None
         g_p = torch.empty_like(pose_flat) if need[3] else None
         ws = None
@@ -84,9 +134,13 @@ class _WarpCost(torch.autograd.Function):
                                          min_disp, max_disp, ptr(K), ptr(ref_K), scale,
                                          ptr(pose_flat), pose_mode, B, N, C, h, w, reduce_mean,
                                          ptr(gcost), ptr(g_f), ptr(g_r), ptr(g_d), ptr(g_p),
-                                         ptr(ws), stream_of(fmap)), "dro_warp_cost_backward")
+                                         accumulate, ptr(ws), stream_of(fmap)), "dro_warp_cost_backward")
         if g_p is not None:
             g_p = ctx.restore(g_p)
+        if sf is not None:
+            g_f = None
+        if sr is not None:
+            g_r = None
         return g_f, g_r, g_d, g_p, None, None, None, None, None, None, None
 
 

@@ -20,6 +20,9 @@ Execution plan (what changes versus the reference, never the math):
     capture records the fork/join as parallel branches.  Measured slower on
     MI355X (24.7 vs 23.7 ms/step: the cross-stream edges cost more than the
     overlap of three MIOpen-bound trunks gains), so serial is the default;
+  * tensors read by every iteration (feature maps, context features) carry a
+    gradient sink (hip.grad_sink): the cost and GRU backward kernels add into
+    it in place instead of autograd summing one gradient per use;
   * no host synchronisation anywhere: the step can be captured in a hipGraph.
 """
 import contextlib
@@ -147,6 +150,9 @@ class DepthPoseNet(nn.Module):
         h, w = fmaps.shape[2:]
         fmap1 = fmaps[:B]
         frefs = fmaps[B:].view(N, B, C, h, w)           # free view: all refs, one tensor
+        # every cost call reads the same feature maps: their gradients are summed
+        # in place by the warp-cost backward (no per-call add launches)
+        fmap1, frefs = hip.grad_sink(fmap1), hip.grad_sink(frefs)
 
         # initial poses of all refs in one pass: cat([fmap1, fmap_ref_j]) per ref j
         pair = torch.cat([fmap1.unsqueeze(0).expand(N, B, C, h, w), frefs], 2).view(N * B, 2 * C, h, w)
@@ -164,6 +170,9 @@ class DepthPoseNet(nn.Module):
             for t in (h_d, x_d, h_p, x_p):
                 t.record_stream(main)
 
+        if self.iters > 0:
+            # the context features feed every GRU step: gradients summed in place
+            x_d, x_p = hip.grad_sink(x_d), hip.grad_sink(x_p)
         for _ in range(self.iters):
             disp = disp.detach()
             poses = poses.detach()

@@ -75,14 +75,18 @@ size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w);
 /* Gradients of sum(cost * grad_cost).  Any grad_* may be NULL (not computed).
  * grad_depth is w.r.t. the depth input in its depth_mode encoding; grad_pose
  * is w.r.t. the pose input in its pose_mode encoding.  `workspace` must hold
- * dro_warp_cost_workspace_bytes() bytes when grad_depth or grad_pose is set. */
+ * dro_warp_cost_workspace_bytes() bytes when grad_depth or grad_pose is set.
+ * accumulate: bit 0 adds into grad_fmap, bit 1 into grad_fmap_ref (otherwise
+ * they are overwritten) -- the feature maps are shared by every cost call of a
+ * step, so their gradients can be summed in place (hip.grad_sink). */
 int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float* depth,
                            int depth_mode, float min_disp, float max_disp,
                            const float* K, const float* ref_K, float scale,
                            const float* pose, int pose_mode,
                            int B, int N, int C, int h, int w, int reduce_mean,
                            const float* grad_cost, float* grad_fmap, float* grad_fmap_ref,
-                           float* grad_depth, float* grad_pose, void* workspace, void* stream);
+                           float* grad_depth, float* grad_pose, int accumulate, void* workspace,
+                           void* stream);
 
 /* D fronto-parallel hypothesis planes (SURVEY.md §8(d) measurement extension):
  * for each plane d, depth = inv2depth(disp_to_depth(disp[d])) everywhere and

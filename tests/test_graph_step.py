@@ -107,3 +107,34 @@ def test_direct_weight_grads_match_autograd_path():
     assert O.rel_err(l1.cpu(), l0.cpu()) < 1e-6 and O.rel_err(l2.cpu(), l0.cpu()) < 1e-6
     assert float((g1 - g0).norm() / g0.norm()) < 1e-4
     assert float((g2 - g0).norm() / g0.norm()) < 1e-4
+
+
+@pytest.mark.gpu
+def test_grad_sinks_match_per_use_gradients():
+    """hip.grad_sink (feature maps and context features summed in place by the
+    warp-cost and GRU backward kernels) against autograd's per-use sums: same
+    loss, parameter gradients within fp32 reassociation (1e-4 relative)."""
+    from dro_sfm_amd.hip import ops as hops
+    from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
+    res = []
+    for enabled in (True, False):
+        hops.set_grad_sinks(enabled)
+        try:
+            torch.manual_seed(0)
+            net = DepthPoseNet(version="it4-seq2-inter-out", min_depth=0.5, max_depth=80).cuda().train()
+            g = torch.Generator().manual_seed(3)
+            img = torch.rand(1, 3, 96, 160, generator=g).cuda()
+            refs = [torch.rand(1, 3, 96, 160, generator=g).cuda() for _ in range(2)]
+            K = torch.tensor([[[120.0, 0, 80], [0, 120, 48], [0, 0, 1]]]).cuda()
+            invs, poses = net(img, refs, K)
+            loss = sum(i.mean() for i in invs) + poses.square().mean()
+            loss.backward()
+            res.append((float(loss), {k: p.grad.clone() for k, p in net.named_parameters()
+                                      if p.grad is not None}))
+        finally:
+            hops.set_grad_sinks(True)
+    (l1, g1), (l2, g2) = res
+    assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l2))
+    assert g1.keys() == g2.keys()
+    for k in g1:
+        torch.testing.assert_close(g1[k], g2[k], rtol=1e-4, atol=1e-6, msg=k)
