@@ -1530,6 +1530,200 @@ Slice to_slice(const dro_slice* s) {
   return r;
 }
 
+// ---------------------------------------------------------------- thin 7x7
+// The 7x7 state convolutions of the projection encoders (update.py:77-124:
+// convd1 1 -> hidden, convp1 6 -> hidden, the latter over a broadcast pose
+// map) have <= 8 input channels: as an MFMA GEMM 26-97 % of every tile is
+// padding, so they run on plain FMAs over an 8x8 pixel tile staged with its
+// halo in LDS.  Forward: a block is 64 pixels x 16 output channels (thread =
+// 1 pixel x 4 channels, float4 weight reads).  Data gradient: a block is 64
+// pixels x all input channels, the output channels split over 4 thread
+// groups and summed through LDS in a fixed order (deterministic).
+constexpr int kThinK = 7, kThinT = 49, kThinHalo = 14 * 14;
+
+template <int ACT>
+__global__ __launch_bounds__(256) void thin_fwd_kernel(IgArgs a, int tiles_x) {
+  __shared__ float Xs[8 * kThinHalo];
+  __shared__ float4 Wv[8 * kThinT * 4];          // [ci][tap][co/4], 16 co per block
+  const int H = a.g.H, W = a.g.W, Cin = a.g.Cin, Cout = a.g.Cout;
+  const size_t HW = (size_t)H * W;
+  const int b = blockIdx.z, co0 = blockIdx.y * 16;
+  const int ty0 = (blockIdx.x / tiles_x) * 8, tx0 = (blockIdx.x % tiles_x) * 8;
+  const Slice sl = a.src[0];
+  for (int e = threadIdx.x; e < Cin * kThinHalo; e += 256) {
+    const int ci = e / kThinHalo, r = e - ci * kThinHalo, hy = r / 14, hx = r - hy * 14;
+    const int yy = ty0 - 3 + hy, xx = tx0 - 3 + hx;
+    float v = 0.f;
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+      const size_t ch = (size_t)b * sl.ctot + sl.coff + ci;
+      v = sl.bcast ? sl.p[ch] : sl.p[ch * HW + (size_t)yy * W + xx];
+    }
+    Xs[e] = v;
+  }
+  float* Wf = reinterpret_cast<float*>(Wv);
+  for (int e = threadIdx.x; e < Cin * kThinT * 16; e += 256) {
+    const int col = e & 15, q = e >> 4, tap = q % kThinT, ci = q / kThinT;
+    const int co = co0 + col;
+    Wf[e] = co < Cout ? a.weight[((size_t)co * Cin + ci) * kThinT + tap] : 0.f;
+  }
+  __syncthreads();
+  const int px = threadIdx.x & 63, cg = threadIdx.x >> 6;   // 4 channels per thread
+  const int py = px >> 3, pxx = px & 7;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int ci = 0; ci < Cin; ++ci) {
+    const float* xb = Xs + ci * kThinHalo + py * 14 + pxx;
+    const float4* wb = Wv + ci * kThinT * 4 + cg;
+#pragma unroll
+    for (int ky = 0; ky < kThinK; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < kThinK; ++kx) {
+        const float v = xb[ky * 14 + kx];
+        const float4 w = wb[(ky * kThinK + kx) * 4];
+        acc.x = fmaf(v, w.x, acc.x);
+        acc.y = fmaf(v, w.y, acc.y);
+        acc.z = fmaf(v, w.z, acc.z);
+        acc.w = fmaf(v, w.w, acc.w);
+      }
+  }
+  const int oy = ty0 + py, ox = tx0 + pxx;
+  if (oy >= H || ox >= W) return;
+  const float r[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = co0 + cg * 4 + j;
+    if (co >= Cout) continue;
+    const float v = a.alpha * act_fwd(r[j] + (a.bias ? a.bias[co] : 0.f), ACT);
+    a.out[((size_t)b * a.out_ctot + a.out_coff + co) * HW + (size_t)oy * W + ox] = v;
+  }
+}
+
+// data gradient w.r.t. a single source of <= 8 channels; G folded as in dconv.
+// blockIdx.y takes a span of output channels (partials [split][Cin][P] summed by
+// igemm_finish_kernel in a fixed order when there is more than one span)
+template <int ACT, int CINP>
+__global__ __launch_bounds__(256) void thin_dgrad_kernel(IgArgs a, int tiles_x, int cps) {
+  constexpr int CC = 16;                          // output channels staged per pass
+  __shared__ float Gs[CC * kThinHalo];
+  __shared__ float Ws[CC * kThinT * CINP];        // [co][tap][ci]
+  __shared__ float red[4 * 64 * CINP];
+  const int H = a.g.H, W = a.g.W, Cin = a.rows, Cout = a.g.Cout;
+  const size_t HW = (size_t)H * W;
+  const int b = blockIdx.z;
+  const int ty0 = (blockIdx.x / tiles_x) * 8, tx0 = (blockIdx.x % tiles_x) * 8;
+  const int px = threadIdx.x & 63, cg = threadIdx.x >> 6;   // group cg takes 4 co per pass
+  const int py = px >> 3, pxx = px & 7;
+  const int co_lo = blockIdx.y * cps, co_hi = min(Cout, co_lo + cps);
+  float acc[CINP];
+#pragma unroll
+  for (int i = 0; i < CINP; ++i) acc[i] = 0.f;
+  for (int c0 = co_lo; c0 < co_hi; c0 += CC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < CC * kThinHalo; e += 256) {
+      const int cl = e / kThinHalo, r = e - cl * kThinHalo, hy = r / 14, hx = r - hy * 14;
+      const int yy = ty0 - 3 + hy, xx = tx0 - 3 + hx, co = c0 + cl;
+      float v = 0.f;
+      if (co < co_hi && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+        const size_t o = ((size_t)b * Cout + co) * HW + (size_t)yy * W + xx;
+        v = a.galpha * a.G[o];
+        if (ACT != 0) v *= act_bwd(a.gy[o], ACT);
+      }
+      Gs[e] = v;
+    }
+    for (int e = threadIdx.x; e < CC * kThinT * CINP; e += 256) {
+      const int ci = e % CINP, q = e / CINP, tap = q % kThinT, cl = q / kThinT, co = c0 + cl;
+      Ws[e] = (co < co_hi && ci < Cin) ? a.weight[((size_t)co * Cin + ci) * kThinT + tap] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int j = 0; j < CC / 4; ++j) {
+      const int cl = cg * (CC / 4) + j;
+      const float* gb = Gs + cl * kThinHalo + py * 14 + pxx;
+      const float* wb = Ws + cl * kThinT * CINP;
+#pragma unroll
+      for (int ky = 0; ky < kThinK; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < kThinK; ++kx) {
+          // input pixel (y, x) receives G at (y - ky + 3, x - kx + 3)
+          const float g = gb[(6 - ky) * 14 + (6 - kx)];
+          const int tap = ky * kThinK + kx;
+          if (CINP == 8) {
+            const float4 w0 = reinterpret_cast<const float4*>(wb)[tap * 2];
+            const float4 w1 = reinterpret_cast<const float4*>(wb)[tap * 2 + 1];
+            acc[0] = fmaf(g, w0.x, acc[0]);
+            acc[1 % CINP] = fmaf(g, w0.y, acc[1 % CINP]);
+            acc[2 % CINP] = fmaf(g, w0.z, acc[2 % CINP]);
+            acc[3 % CINP] = fmaf(g, w0.w, acc[3 % CINP]);
+            acc[4 % CINP] = fmaf(g, w1.x, acc[4 % CINP]);
+            acc[5 % CINP] = fmaf(g, w1.y, acc[5 % CINP]);
+            acc[6 % CINP] = fmaf(g, w1.z, acc[6 % CINP]);
+            acc[7 % CINP] = fmaf(g, w1.w, acc[7 % CINP]);
+          } else {
+#pragma unroll
+            for (int ci = 0; ci < CINP; ++ci) acc[ci] = fmaf(g, wb[tap * CINP + ci], acc[ci]);
+          }
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < CINP; ++i) red[(cg * 64 + px) * CINP + i] = acc[i];
+  __syncthreads();
+  const long long P = (long long)a.g.B * HW;
+  for (int e = threadIdx.x; e < 64 * CINP; e += 256) {
+    const int p = e / CINP, ci = e % CINP;
+    if (ci >= Cin) continue;
+    const float v = (red[(0 * 64 + p) * CINP + ci] + red[(1 * 64 + p) * CINP + ci]) +
+                    (red[(2 * 64 + p) * CINP + ci] + red[(3 * 64 + p) * CINP + ci]);
+    const int oy = ty0 + (p / 8), ox = tx0 + (p % 8);
+    if (oy >= H || ox >= W) continue;
+    const size_t epix = (size_t)oy * W + ox;
+    if (a.part)
+      a.part[(size_t)blockIdx.y * Cin * P + (size_t)ci * P + (size_t)b * HW + epix] = v;
+    else
+      grad_put(a.gsrc[0], a.gsrc_ctot[0], a.gsrc_coff[0], a.gsrc_acc[0], ci, b, epix, HW, v);
+  }
+}
+
+// thin path eligibility: 7x7, a single source of <= 8 channels, plain epilogue
+template <int MODE, int EPI>
+bool thin_ok(const IgArgs& a) {
+  if (EPI != 0 || a.g.KH != kThinK || a.g.KW != kThinK || a.g.B > 65535) return false;
+  const int cin = MODE == 0 ? a.g.Cin : a.rows;
+  if (cin > 8 || a.cbase[1] < cin) return false;
+  if (MODE == 1 && a.gsrc[0] == nullptr) return false;
+  return true;
+}
+
+template <int MODE, int ACT>
+int launch_thin(IgArgs& a, int max_splits, hipStream_t s) {
+  const int tiles_x = (a.g.W + 7) / 8, tiles = tiles_x * ((a.g.H + 7) / 8);
+  if (MODE == 0) {
+    hipLaunchKernelGGL((thin_fwd_kernel<ACT>), dim3(tiles, (a.g.Cout + 15) / 16, a.g.B), dim3(256), 0,
+                       s, a, tiles_x);
+    return launch_status("thin_fwd_kernel launch failed");
+  }
+  // output channels in spans of 16 over up to 4 blocks (partials in the
+  // workspace the caller sized for the flat plan's split-K)
+  const int splits = max_splits >= 4 ? 4 : (max_splits >= 2 ? 2 : 1);
+  const int cps = (a.g.Cout + splits - 1) / splits;
+  if (splits == 1) a.part = nullptr;
+  const dim3 grid(tiles, splits, a.g.B);
+  if (a.rows == 1)
+    hipLaunchKernelGGL((thin_dgrad_kernel<ACT, 1>), grid, dim3(256), 0, s, a, tiles_x, cps);
+  else if (a.rows == 2)
+    hipLaunchKernelGGL((thin_dgrad_kernel<ACT, 2>), grid, dim3(256), 0, s, a, tiles_x, cps);
+  else if (a.rows <= 4)
+    hipLaunchKernelGGL((thin_dgrad_kernel<ACT, 4>), grid, dim3(256), 0, s, a, tiles_x, cps);
+  else
+    hipLaunchKernelGGL((thin_dgrad_kernel<ACT, 8>), grid, dim3(256), 0, s, a, tiles_x, cps);
+  int st = launch_status("thin_dgrad_kernel launch failed");
+  if (st || splits == 1) return st;
+  const long long P = (long long)a.g.B * a.g.H * a.g.W;
+  const long long total = (long long)a.rows * P;
+  hipLaunchKernelGGL((igemm_finish_kernel<1, 0, 0>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     s, a, splits);
+  return launch_status("igemm_finish_kernel launch failed");
+}
+
 unsigned long long* g_conv_stamps = nullptr;   // dro_debug_conv_stamps
 
 // rows / kch set by the caller; `ws` must hold plan.part_bytes
@@ -1543,6 +1737,11 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.dbg = e ? atoi(e) : 0;
   }
   a.K = a.kch * a.g.KH * a.g.KW;
+  static const bool thin_off = getenv("DRO_CONV_NO_THIN") != nullptr;   // A/B switch
+  if (!thin_off && thin_ok<MODE, EPI>(a)) {
+    a.part = reinterpret_cast<float*>(ws);
+    return launch_thin<MODE, ACT>(a, pl.ksplit, s);
+  }
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;

@@ -57,6 +57,9 @@ CASES = [
     ([("dense", 128)], 1, (3, 3), "tanh", 1.0, 2, 24, 80),
     ([("dense", 128)], 6, (3, 3), None, 1.0, 4, 24, 80),
     ([("dense", 37), ("slice", 11)], 45, (5, 3), "sigmoid", 1.0, 3, 7, 13),
+    # thin 7x7 path (<= 8 input channels): ragged tiles, Cout not a multiple of 16
+    ([("dense", 3)], 20, (7, 7), "tanh", 1.0, 3, 13, 21),
+    ([("slice", 8)], 64, (7, 7), None, 0.5, 2, 9, 11),
 ]
 
 

@@ -129,7 +129,7 @@ def test_grad_sinks_match_per_use_gradients():
             invs, poses = net(img, refs, K)
             loss = sum(i.mean() for i in invs) + poses.square().mean()
             loss.backward()
-            res.append((float(loss), {k: p.grad.clone() for k, p in net.named_parameters()
+            res.append((float(loss.detach()), {k: p.grad.clone() for k, p in net.named_parameters()
                                       if p.grad is not None}))
         finally:
             hops.set_grad_sinks(True)
@@ -137,4 +137,11 @@ def test_grad_sinks_match_per_use_gradients():
     assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l2))
     assert g1.keys() == g2.keys()
     for k in g1:
-        torch.testing.assert_close(g1[k], g2[k], rtol=1e-4, atol=1e-6, msg=k)
+        # the encoders run on MIOpen, whose convolutions are not run-to-run
+        # deterministic (its weight gradients vary run to run
+        # too): their gradients are compared by relative L2 norm
+        if k.split(".")[0] in ("fnet", "cnet", "cnet_depth", "cnet_pose"):
+            err = float((g1[k] - g2[k]).norm() / g2[k].norm().clamp_min(1e-12))
+            assert err < 1e-2, (k, err)
+        else:
+            torch.testing.assert_close(g1[k], g2[k], rtol=1e-4, atol=1e-6, msg=lambda m, k=k: f"{k}: {m}")
