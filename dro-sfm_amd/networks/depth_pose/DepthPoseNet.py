@@ -138,18 +138,20 @@ class DepthPoseNet(nn.Module):
                         t.record_stream(st)
             with torch.cuda.stream(side[0]) if side else _null():
                 ctx_d = self.cnet_depth(target_image)
-                h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
+                h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
+                h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
             with torch.cuda.stream(side[1]) if side else _null():
                 pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
                                    torch.stack(list(ref_imgs))], 2).flatten(0, 1)
                 ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
-                h_p, x_p = torch.tanh(ctx_p[:, :hd]), torch.relu(ctx_p[:, hd:hd + cd])
+                h_p, x_p = torch.split(ctx_p, [hd, cd], 1)
+                h_p, x_p = torch.tanh(h_p), torch.relu(x_p)
 
         fmaps = self.fnet(torch.cat([target_image] + list(ref_imgs), 0))
         assert target_image.shape[2] // fmaps.shape[2] == self.feat_ratio
         h, w = fmaps.shape[2:]
-        fmap1 = fmaps[:B]
-        frefs = fmaps[B:].view(N, B, C, h, w)           # free view: all refs, one tensor
+        fmap1, frefs = torch.split(fmaps, [B, N * B], 0)
+        frefs = frefs.view(N, B, C, h, w)               # free view: all refs, one tensor
         # every cost call reads the same feature maps: their gradients are summed
         # in place by the warp-cost backward (no per-call add launches)
         fmap1, frefs = hip.grad_sink(fmap1), hip.grad_sink(frefs)
