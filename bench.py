@@ -389,8 +389,8 @@ def main():
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",
                     help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
-    ap.add_argument("--no-grad-sinks", action="store_true",
-                    help="per-use gradients summed by autograd instead of in-place sinks (A/B)")
+    ap.add_argument("--grad-sinks", action="store_true",
+                    help="in-place gradient sinks for shared tensors (A/B; default off)")
     ap.add_argument("--no-fused-bn", action="store_true",
                     help="encoder BatchNorm+ReLU through PyTorch's kernels (A/B)")
     ap.add_argument("--roofline-only", action="store_true",
@@ -416,7 +416,7 @@ def main():
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     from dro_sfm_amd.hip import ops as _hops
-    _hops.set_grad_sinks(not args.no_grad_sinks)
+    _hops.set_grad_sinks(args.grad_sinks)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)

@@ -313,6 +313,7 @@ class _Conv2d(torch.autograd.Function):
                                      act, ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(ws), nws,
                                      stream_of(out)), "dro_conv2d_forward")
         ctx.save_for_backward(weight, out if act else None, *srcs)
+        ctx.sinks = [_sink_of(x) for x in srcs]
         ctx.meta = (act, alpha, bias is not None)
         ctx.scope = scope
         ctx.direct = direct
@@ -328,15 +329,20 @@ class _Conv2d(torch.autograd.Function):
         B, _, H, W = srcs[0].shape
         need = ctx.needs_input_grad
         gout = gout.contiguous()
-        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[7 + i] else None
-                for i, s in enumerate(srcs)]
+        # sources with a gradient sink are written in place (and get None)
+        sinks = [s if need[7 + i] else None for i, s in enumerate(ctx.sinks)]
+        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[7 + i] and sinks[i] is None
+                else None for i, s in enumerate(srcs)]
+        sk = [s.target() if s is not None else (None, 0) for s in sinks]
+        tgt = [t if s is not None else g for (t, _), s, g in zip(sk, sinks, gsrc)]
+        dacc = [a for _, a in sk]
         ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
         if ctx.direct is not None:
             # data gradients here, weight gradients on the side stream into .grad
             gw, gb = ctx.direct[2], ctx.direct[3]
-            ptrs, ctot, coff = _grad_targets(gsrc)
-            acc = (ctypes.c_int * len(srcs))()
-            if any(g is not None for g in gsrc):
+            ptrs, ctot, coff = _grad_targets(tgt)
+            acc = (ctypes.c_int * len(srcs))(*dacc)
+            if any(g is not None for g in tgt):
                 ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
                 check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                               act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
@@ -360,8 +366,8 @@ class _Conv2d(torch.autograd.Function):
                                                 weight, Cout if has_bias else 0, gout.device)
         else:
             gw, gb, wacc, first = None, None, 0, False
-        ptrs, ctot, coff = _grad_targets(gsrc)
-        acc = (ctypes.c_int * len(srcs))()
+        ptrs, ctot, coff = _grad_targets(tgt)
+        acc = (ctypes.c_int * len(srcs))(*dacc)
         ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
         check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
@@ -463,8 +469,9 @@ class _SepGRUHalf(torch.autograd.Function):
         sinks = [s if need[9 + i] else None for i, s in enumerate(ctx.sinks)]
         dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[9 + i] and sinks[i] is None
                else None for i, x in enumerate(xs)]
-        tg = [s if s is not None else d for s, d in zip(sinks, dxs)]
-        qacc0 = [0] + [1 if s is not None else 0 for s in sinks]
+        sk = [s.target() if s is not None else (None, 0) for s in sinks]
+        tg = [t if s is not None else d for (t, _), s, d in zip(sk, sinks, dxs)]
+        qacc0 = [0] + [a for _, a in sk]
         if ctx.direct is not None:
             return _SepGRUHalf._backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs,
                                                 tg, qacc0)

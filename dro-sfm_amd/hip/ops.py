@@ -37,44 +37,71 @@ def _disp_range(min_depth, max_depth):
 
 
 # ------------------------------------------------------------------------- warp + feature cost
-class _GradSink(torch.autograd.Function):
-    """Identity whose gradient is a buffer that consumers add into in place.
+class GradSinkState:
+    """A sink's dense gradient buffer and whether a consumer has written it yet
+    (the first consumer to run overwrites, the later ones add: no zero-fill)."""
+    __slots__ = ("buf", "written")
 
-    A tensor read by many ops of one step (the feature maps of every cost call,
-    the context features of every GRU step) otherwise gets one gradient per
+    def __init__(self, like):
+        self.buf = torch.empty(like.shape, device=like.device, dtype=like.dtype)
+        self.written = False
+
+    def target(self):
+        """(buffer, accumulate flag) for the calling consumer's backward."""
+        acc = 1 if self.written else 0
+        self.written = True
+        return self.buf, acc
+
+
+class _GradSink(torch.autograd.Function):
+    """Identity whose gradient is a buffer that consumers write into in place.
+
+    A tensor read by several ops of one step (the feature maps of every cost
+    call, the context features of every GRU step, the state and projection
+    features every GRU half and 7x7 conv read) otherwise gets one gradient per
     use and autograd sums them with one add launch each.  Ops that know the
-    sink (hip.warp_cost, hip.sepconvgru_half) accumulate straight into it and
-    return None; autograd runs this node only after all of them, so the buffer
-    is complete when it is handed on (plus any gradient other ops returned)."""
+    sink (hip.warp_cost, hip.sepconvgru_half, hip.conv2d) write straight into
+    it and return None; autograd runs this node only after all of them, so the
+    buffer is complete when it is handed on (plus any gradient other ops
+    returned)."""
 
     @staticmethod
-    def forward(ctx, x, buf):
-        ctx.buf = buf
+    def forward(ctx, x, state):
+        ctx.state = state
         ctx.set_materialize_grads(False)
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
-        return (ctx.buf if g is None else ctx.buf + g), None
+        st = ctx.state
+        if not st.written:
+            return g, None
+        st.written = False
+        return (st.buf if g is None else st.buf + g), None
 
 
-_SINKS = [True]
+_SINKS = [False]
 
 
 def set_grad_sinks(enabled):
-    """grad_sink on (default) / off (identity; autograd sums per use) for A/B runs."""
+    """grad_sink on / off (default: identity, autograd sums per use).  Measured on
+    one MI355X box: sinks on the feature maps and context features 21.58 vs
+    21.55 ms/step, extended to the per-step state / projection features / pose
+    map 21.79 vs 21.24 ms/step (the accumulating epilogues' extra reads cost more
+    than the add launches they remove), so the default is off."""
     _SINKS[0] = bool(enabled)
 
 
 def grad_sink(x):
     """x (aliased) with an in-place gradient sink; x itself when no gradient flows.
-    One backward per forward: the buffer is zeroed here, in the forward."""
+    One backward per forward.  x may be a broadcast view (an expanded pose map):
+    the sink buffer is dense, the view's own backward reduces it once."""
     if not (_SINKS[0] and torch.is_grad_enabled() and x.requires_grad and x.is_cuda
-            and x.is_contiguous()):
+            and x.dim() == 4):
         return x
-    buf = torch.zeros_like(x, memory_format=torch.contiguous_format)
-    y = _GradSink.apply(x, buf)
-    y._dro_gsink = buf
+    st = GradSinkState(x)
+    y = _GradSink.apply(x, st)
+    y._dro_gsink = st
     return y
 
 
@@ -121,9 +148,19 @@ class _WarpCost(torch.autograd.Function):
         gcost = gcost.contiguous()
         # feature maps shared by all cost calls of a step: summed in their sinks
         sf, sr = ctx.sinks
-        g_f = (sf if sf is not None else torch.empty_like(fmap)) if need[0] else None
-        g_r = (sr if sr is not None else torch.empty_like(fmap_ref)) if need[1] else None
-        accumulate = (1 if sf is not None else 0) | (2 if sr is not None else 0)
+        sf = sf if need[0] else None
+        sr = sr if need[1] else None
+        accumulate = 0
+        if sf is not None:
+            g_f, af = sf.target()
+            accumulate |= af
+        else:
+            g_f = torch.empty_like(fmap) if need[0] else None
+        if sr is not None:
+            g_r, ar = sr.target()
+            accumulate |= 2 * ar
+        else:
+            g_r = torch.empty_like(fmap_ref) if need[1] else None
         g_d = torch.empty_like(depth) if need[2] else None
         g_p = torch.empty_like(pose_flat) if need[3] else None
         ws = None

@@ -20,9 +20,10 @@ Execution plan (what changes versus the reference, never the math):
     capture records the fork/join as parallel branches.  Measured slower on
     MI355X (24.7 vs 23.7 ms/step: the cross-stream edges cost more than the
     overlap of three MIOpen-bound trunks gains), so serial is the default;
-  * tensors read by every iteration (feature maps, context features) carry a
-    gradient sink (hip.grad_sink): the cost and GRU backward kernels add into
-    it in place instead of autograd summing one gradient per use;
+  * tensors read by every iteration (feature maps, context features) can carry
+    a gradient sink (hip.grad_sink, off by default -- measured neutral): the
+    cost and GRU backward kernels then add into it in place instead of autograd
+    summing one gradient per use;
   * no host synchronisation anywhere: the step can be captured in a hipGraph.
 """
 import contextlib

@@ -167,7 +167,8 @@ class _Projection(nn.Module):
         s1, s2, f = (getattr(self, f"conv{t}{i}") for i in ("1", "2", ""))
         cor = conv(conv(cost, c1.weight, c1.bias, "relu"), c2.weight, c2.bias, "relu")
         sfm = conv(conv(state_map, s1.weight, s1.bias, "relu"), s2.weight, s2.bias, "relu")
-        return [conv([cor, sfm], f.weight, f.bias, "relu"), state_map]
+        # both GRU halves read the fused features: their gradients meet in a sink
+        return [hip.grad_sink(conv([cor, sfm], f.weight, f.bias, "relu")), state_map]
 
 
 class ProjectionInputDepth(_Projection):
@@ -187,7 +188,9 @@ class ProjectionInputPose(_Projection):
         return pose.reshape(bs, 6, 1, 1).expand(bs, 6, h, w)
 
     def sources(self, pose, cost):
-        return super().sources(self.pose_map(pose, cost), cost)
+        # the broadcast pose map feeds the 7x7 conv and both GRU halves: one dense
+        # gradient buffer, reduced once by the expand's backward
+        return super().sources(hip.grad_sink(self.pose_map(pose, cost)), cost)
 
     def forward(self, pose, cost):
         return torch.cat(self.sources(pose, cost), 1)
@@ -228,6 +231,8 @@ class BasicUpdateBlockDepth(nn.Module):
         scale_func = scale_func or (lambda x: (x, None))
         invs, masks = [], []
         for _ in range(seq_len):
+            # the state feeds the cost, the 7x7 conv, both GRU halves and the update
+            inv_depth = hip.grad_sink(inv_depth)
             feat = self.encoder.sources(inv_depth, cost_func(scale_func(inv_depth)[0]))
             net = self.depth_gru(net, [context, *feat])
             delta, mask = self.heads(net)

@@ -43,7 +43,7 @@ for step in "$@"; do
     w:*) wl=${step#w:}; run "bench_$wl" 900 python bench.py --workload "$wl" --steps 10 --warmup 3 ;;
     benchnowrw) run bench_nowrwnhwc 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     benchnoig) run bench_noigemm 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
-    benchnosink) run bench_nosink 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-grad-sinks ;;
+    benchsink) run bench_sink 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --grad-sinks ;;
     benchab) run bench_a 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     benchnobn) run bench_nofusedbn 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-fused-bn ;;
     benchconc) run bench_conc 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --concurrent-encoders ;;
