@@ -7,6 +7,10 @@
 //   g += wd * p;  m += (1-b1) (g - m);  v = b2 v + (1-b2) g^2
 //   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 // HBM-bound: 16 B read + 12 B written per parameter (p, g, m, v / p, m, v).
+// Every hyper-parameter is read from DEVICE memory (hyper = {lr, beta1, beta2,
+// eps, weight_decay}), like the step counter: a replayed hipGraph picks up a
+// learning-rate schedule (torch.optim.lr_scheduler.StepLR in the reference,
+// model_wrapper.py:192-193) written between replays.
 #include <hip/hip_runtime.h>
 
 #include "dro_common.hpp"
@@ -24,9 +28,10 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, flo
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   long long n, const float* __restrict__ step, float lr,
-                                                   float b1, float b2, float eps, float wd) {
+                                                   long long n, const float* __restrict__ step,
+                                                   const float* __restrict__ hyper) {
   const float t = *step;
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
   const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
   const long long n4 = n / 4;
@@ -53,9 +58,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 }  // namespace dro
 
 extern "C" int dro_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                             long long n, const float* step, float lr, float beta1, float beta2,
-                             float eps, float weight_decay, void* stream) {
-  if (!param || !grad || !exp_avg || !exp_avg_sq || !step) {
+                             long long n, const float* step, const float* hyper, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !step || !hyper) {
     dro::set_error("adam_step: NULL pointer");
     return DRO_E_NULL;
   }
@@ -68,6 +72,6 @@ extern "C" int dro_adam_step(float* param, const float* grad, float* exp_avg, fl
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(dro::adam_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
-                     exp_avg, exp_avg_sq, n, step, lr, beta1, beta2, eps, weight_decay);
+                     exp_avg, exp_avg_sq, n, step, hyper);
   return dro::launch_status("adam_kernel launch failed");
 }

@@ -64,7 +64,7 @@ def load():
     _sig(lib.dro_conv2d_backward, P, I, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, I, P, Z, S)
     _sig(lib.dro_conv2d_weight_grad_multi_workspace_bytes, I, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_weight_grad_multi, P, I, I, I, I, I, I, I, I, I, F, P, P, I, P, Z, S)
-    _sig(lib.dro_adam_step, P, P, P, P, ctypes.c_longlong, P, F, F, F, F, F, S)
+    _sig(lib.dro_adam_step, P, P, P, P, ctypes.c_longlong, P, P, S)
     _sig(lib.dro_gru_backward_elem, I, I, I, I, I, P, P, P, P, P, P, P, P, S)
     _lib = lib
     return lib

@@ -94,10 +94,14 @@ def set_grad_sinks(enabled):
 
 def grad_sink(x):
     """x (aliased) with an in-place gradient sink; x itself when no gradient flows.
-    One backward per forward.  x may be a broadcast view (an expanded pose map):
-    the sink buffer is dense, the view's own backward reduces it once."""
-    if not (_SINKS[0] and torch.is_grad_enabled() and x.requires_grad and x.is_cuda
-            and x.dim() == 4):
+    One backward per forward.  x may be a dense tensor of any rank or a 4-D
+    broadcast view (an expanded pose map): the sink buffer is dense, the view's
+    own backward reduces it once."""
+    if not (_SINKS[0] and torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
+        return x
+    if not x.is_contiguous() and x.dim() != 4:
+        # broadcast (expanded) views: only the 4-D pose maps the convs read; dense
+        # tensors of any rank (the [N,B,C,h,w] reference feature maps) qualify
         return x
     st = GradSinkState(x)
     y = _GradSink.apply(x, st)

@@ -10,8 +10,11 @@ provides it MI355X-first:
     it), cut into ~bucket_mb buckets in reverse registration order -- the order
     backward produces them;
   * a post-accumulate hook per parameter counts arrivals per bucket; a full
-    bucket's all-reduce is issued immediately (async), so communication of
-    late layers overlaps backward of early ones;
+    bucket's all-reduce is issued (async) as soon as every bucket before it in
+    one rank-independent order has been issued, so communication of late
+    layers overlaps backward of early ones and every rank issues the same
+    sequence of collectives even when its buckets complete in another order
+    or a gradient does not arrive on some step;
   * from the second step on, parameters whose gradient autograd produces
     (everything but the conv-engine weights written in place) start the
     backward with .grad = None, so AccumulateGrad adopts the produced tensor
@@ -88,6 +91,14 @@ class GradBuckets:
         # of backward) fire no hook: their buckets are reduced in finish()
         self._deferred = [any(_direct_used(p) for p in b) for b in self.buckets]
         self._need = [sum(not _direct_used(p) for p in b) for b in self.buckets]
+        # ONE all-reduce order, identical on every rank (the build is decided from
+        # all-reduced flags): hook-completed buckets in backward order, then the
+        # deferred ones.  A bucket is issued only after every bucket before it in
+        # this order, so ranks whose buckets complete in different orders -- or
+        # not at all on some step (a gradient that never arrives) -- still pair
+        # their collectives one for one (as DDP's in-order bucket launch does).
+        self._order = ([b for b in range(len(self.buckets)) if not self._deferred[b]] +
+                       [b for b in range(len(self.buckets)) if self._deferred[b]])
 
     def _slice(self, bucket):
         """One contiguous flat slice covering a bucket (slots of inactive params
@@ -107,28 +118,46 @@ class GradBuckets:
         b = self._bucket_of.get(p)
         if b is None:
             return
-        self._left[b] -= 1
-        if self._left[b] == 0:
-            self._gather(b)
         if self.flat.is_cuda:
             # the hook runs on the stream that produced this gradient (the context
             # encoders' backward runs on side streams): remember it for the bucket
             self._bstreams[b].add(torch.cuda.current_stream())
-        if self._left[b] == 0 and self.world > 1 and not self._deferred[b]:
-            if self.flat.is_cuda:
-                cur = torch.cuda.current_stream()
-                for st in self._bstreams[b]:
-                    if st != cur:
-                        cur.wait_stream(st)
-            self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
-                                                 group=self.group, async_op=True))
+        self._left[b] -= 1
+        if self._left[b] == 0:
+            self._complete(b)
+            self._issue_ready()
+
+    def _complete(self, b):
+        """Bucket b's gradients are final: order the current stream after every
+        stream that produced one of them, then gather them into the flat buffer."""
+        if self.flat.is_cuda:
+            cur = torch.cuda.current_stream()
+            for st in self._bstreams[b]:
+                if st != cur:
+                    cur.wait_stream(st)
+        self._gather(b)
+        self._ready[b] = True
+
+    def _issue_ready(self):
+        """Issue the all-reduce of every ready bucket at the head of the order."""
+        while self._next < len(self._order) and self._ready[self._order[self._next]]:
+            b = self._order[self._next]
+            self._next += 1
+            if self.world > 1:
+                self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
+                                                     group=self.group, async_op=True))
 
     def _gather(self, b):
-        """Copy bucket b's adopted gradients into the flat buffer (one launch)."""
+        """Copy bucket b's adopted gradients into the flat buffer (one launch).
+        A gradient that never arrived this step keeps its zeroed slot, which
+        becomes its .grad (the all-reduced average may still be non-zero)."""
         ps = [p for p in self._adopt[b] if p.grad is not None and not self._is_view(p)]
         if ps:
             torch._foreach_copy_([self._view(p) for p in ps], [p.grad for p in ps])
             for p in ps:
+                p.grad = self._view(p)
+        for p in self._adopt[b]:
+            if p.grad is None:
                 p.grad = self._view(p)
 
     def _view(self, p):
@@ -145,6 +174,8 @@ class GradBuckets:
         self._pending = []
         if self.active is not None:
             self._left = list(self._need)
+            self._ready = [False] * len(self.buckets)
+            self._next = 0
             self._bstreams = [set() for _ in self.buckets]
             for ps in self._adopt:
                 for p in ps:
@@ -163,14 +194,13 @@ class GradBuckets:
                 for b in self.buckets:
                     dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM, group=self.group)
         else:
+            # deferred buckets, and buckets some of whose gradients never arrived
+            # this step (their missing slots are the zeros of zero()): complete
+            # them, then issue everything not issued yet, in the common order
             for b in range(len(self.buckets)):
-                if self._left[b] != 0:      # a bucket some of whose gradients never arrived
-                    self._gather(b)
-            if self.world > 1:
-                for b, d in zip(self.buckets, self._deferred):
-                    if d:
-                        self._pending.append(dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM,
-                                                             group=self.group, async_op=True))
+                if not self._ready[b]:
+                    self._complete(b)
+            self._issue_ready()
             for work in self._pending:
                 work.wait()
             self._pending = []
@@ -224,48 +254,125 @@ def broadcast_module(module, src=0, group=None):
             dist.broadcast(t.data, src=src, group=group)
 
 
-class FlatAdam:
+class FlatAdam(torch.optim.Optimizer):
     """torch.optim.Adam (amsgrad off) over ONE flat parameter buffer: a single
     fused HIP launch per step (csrc/optim.hip) instead of per-tensor kernels.
-    The step counter lives on the device (capturable); lr/betas/eps are baked
-    into a captured graph, as with torch's capturable Adam."""
+
+    A torch.optim.Optimizer, so torch.optim.lr_scheduler wraps it (the
+    reference builds StepLR, model_wrapper.py:192-193).  The step counter AND
+    the hyper-parameters {lr, beta1, beta2, eps, weight_decay} live in device
+    memory and the kernel reads them at run time: a captured hipGraph follows
+    a schedule.  Eager step() syncs param_groups into the device copy;
+    GraphedTrainStep.step() calls sync_hyper() before each replay.
+
+    state_dict() / load_state_dict() use torch.optim.Adam's per-parameter
+    layout ({'state': {i: {'step', 'exp_avg', 'exp_avg_sq'}}, 'param_groups':
+    [{..., 'params': [0..n-1]}]}), indexed in the order of `params` -- the
+    reference saves its Adam state that way under 'optimizer'
+    (model_checkpoint.py:76), so checkpoints interchange in both directions."""
 
     def __init__(self, params, flat_param, flat_grad, lr=2e-4, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0):
+                 weight_decay=0.0, offsets=None):
         from ..hip import _lib
         self._lib = _lib
         _lib.load()
+        params = list(params)
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                        amsgrad=False, maximize=False, foreach=None, capturable=True,
+                        differentiable=False, fused=None)
+        super().__init__(params if params else [flat_param], defaults)
         self.params, self.flat_param, self.flat_grad = params, flat_param, flat_grad
+        if offsets is None:
+            offsets, off = {}, 0
+            for p in params:
+                offsets[p] = off
+                off += p.numel()
+        self.offsets = offsets
+        self.active = None               # params that ever receive a gradient (None: all)
         self.exp_avg = torch.zeros_like(flat_param)
         self.exp_avg_sq = torch.zeros_like(flat_param)
         self.step_t = torch.zeros((), device=flat_param.device, dtype=torch.float32)
-        self.state = {"flat": {"step": self.step_t, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}}
-        self.param_groups = [{"params": params, "lr": lr, "betas": betas, "eps": eps,
-                              "weight_decay": weight_decay}]
+        self.hyper_t = torch.zeros(5, device=flat_param.device, dtype=torch.float32)
+        self._hyper_host = None
+        self.sync_hyper()
 
-    def step(self):
+    def _hyper(self):
         g = self.param_groups[0]
+        return (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]),
+                float(g["weight_decay"]))
+
+    def sync_hyper(self):
+        """Write param_groups' hyper-parameters to the device copy the kernel
+        reads (only when they changed; never during graph capture -- the write
+        would be baked into the graph)."""
+        h = self._hyper()
+        if h == self._hyper_host:
+            return
+        if self.hyper_t.is_cuda and torch.cuda.is_current_stream_capturing():
+            return
+        self.hyper_t.copy_(torch.tensor(h, dtype=torch.float32), non_blocking=False)
+        self._hyper_host = h
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if closure is not None:
+            raise RuntimeError("FlatAdam.step: closures are not supported")
+        self.sync_hyper()
         self.step_t += 1
         lib = self._lib
         lib.check(lib.load().dro_adam_step(lib.ptr(self.flat_param), lib.ptr(self.flat_grad),
                                            lib.ptr(self.exp_avg), lib.ptr(self.exp_avg_sq),
-                                           self.flat_param.numel(), lib.ptr(self.step_t), g["lr"],
-                                           g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"],
-                                           lib.stream_of(self.flat_param)), "dro_adam_step")
+                                           self.flat_param.numel(), lib.ptr(self.step_t),
+                                           lib.ptr(self.hyper_t), lib.stream_of(self.flat_param)),
+                  "dro_adam_step")
 
     def zero_grad(self, set_to_none=False):
         self.flat_grad.zero_()
 
+    def _slot(self, buf, p):
+        off = self.offsets[p]
+        return buf[off:off + p.numel()].view_as(p)
+
     def state_dict(self):
-        return {"state": {k: v.clone() for k, v in self.state["flat"].items()},
-                "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}]}
+        g = {k: v for k, v in self.param_groups[0].items() if k != "params"}
+        g["params"] = list(range(len(self.params)))
+        state = {}
+        if float(self.step_t) > 0:               # torch.optim.Adam has no state before its first step
+            for i, p in enumerate(self.params):
+                if self.active is not None and p not in self.active:
+                    continue                 # torch.optim.Adam keeps no state without a grad
+                # a CPU step tensor, as torch.optim.Adam(capturable=False) saves it
+                state[i] = {"step": torch.tensor(float(self.step_t), dtype=torch.float32),
+                            "exp_avg": self._slot(self.exp_avg, p).detach().clone(),
+                            "exp_avg_sq": self._slot(self.exp_avg_sq, p).detach().clone()}
+        return {"state": state, "param_groups": [g]}
 
     def load_state_dict(self, sd):
-        """In place (a captured graph holds these buffers' addresses)."""
+        """In place (a captured graph holds these buffers' addresses).  Accepts
+        torch.optim.Adam state dicts over the same parameter list."""
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self.params):
+            raise ValueError("FlatAdam.load_state_dict: expected one group over "
+                             f"{len(self.params)} parameters")
         with torch.no_grad():
-            for k, v in sd["state"].items():
-                self.state["flat"][k].copy_(v)
-        self.param_groups[0].update(sd["param_groups"][0])
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            steps = set()
+            for slot, i in enumerate(groups[0]["params"]):
+                st = sd["state"].get(i)
+                if st is None:
+                    continue
+                p = self.params[slot]
+                self._slot(self.exp_avg, p).copy_(st["exp_avg"])
+                self._slot(self.exp_avg_sq, p).copy_(st["exp_avg_sq"])
+                steps.add(float(st["step"]))
+            if len(steps) > 1:
+                raise ValueError(f"FlatAdam.load_state_dict: per-parameter steps differ {sorted(steps)}")
+            self.step_t.fill_(steps.pop() if steps else 0.0)
+        for k, v in groups[0].items():
+            if k != "params":
+                self.param_groups[0][k] = tuple(v) if k == "betas" else v
+        self.sync_hyper()
 
 
 def flatten_parameters(params, offsets, total, device):
@@ -299,8 +406,11 @@ class DataParallelTrainer:
             # fused Adam over flat buffers (the product path on the GPU)
             self.flat_params = flatten_parameters(self.grads.params, self.grads.offsets,
                                                   self.grads.flat.numel(), dev)
-            self.optimizer = FlatAdam(self.grads.params, self.flat_params, self.grads.flat, lr=lr,
-                                      betas=betas, eps=eps)
+            # indexed in registration order, like the reference's Adam over
+            # depth_net.parameters() (model_wrapper.py:168-187)
+            order = [p for p in model.parameters() if p.requires_grad]
+            self.optimizer = FlatAdam(order, self.flat_params, self.grads.flat, lr=lr,
+                                      betas=betas, eps=eps, offsets=self.grads.offsets)
         else:
             # CPU (gloo tests of the data-parallel host logic): PyTorch's Adam
             self.optimizer = torch.optim.Adam(self.grads.params, lr=lr, betas=betas, eps=eps,
@@ -312,6 +422,9 @@ class DataParallelTrainer:
         loss = out["loss"]
         loss.sum().backward()
         self.grads.finish()
+        if isinstance(self.optimizer, FlatAdam) and self.optimizer.active is None \
+                and self.grads.active is not None:
+            self.optimizer.active = set(self.grads.active)
         self.optimizer.step()
         return loss.detach(), out.get("metrics", {})
 
@@ -388,6 +501,9 @@ class GraphedTrainStep:
         return self.tr._step_inner(self.static, flip=flip)
 
     def step(self, batch, flip=None):
+        sync = getattr(self.tr.optimizer, "sync_hyper", None)
+        if sync is not None:
+            sync()                       # a scheduler's lr reaches the captured Adam
         _copy_batch(self.static, {k: v for k, v in batch.items() if k != "intrinsics"})
         self.static["intrinsics_ref"].copy_(batch["intrinsics"], non_blocking=True)
         if flip is None:

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);
+int dro_abi_version(void);   /* 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* ------------------------------------------------------------------------
  * Inverse warp + feature cost.
@@ -322,13 +322,14 @@ int dro_gru_backward_elem(int stage, int B, int hd, int H, int W, const float* d
 /* ------------------------------------------------------------------------
  * Fused Adam over flat fp32 buffers (the data-parallel trainer's parameters,
  * gradients and moments; torch.optim.Adam semantics, amsgrad off).  `step` is
- * the device-side step counter AFTER the increment for this update.  All four
+ * the device-side step counter AFTER the increment for this update; `hyper`
+ * points to 5 device floats {lr, beta1, beta2, eps, weight_decay}, read at
+ * run time so a captured graph follows a learning-rate schedule.  All four
  * buffers 16-byte aligned.  Replaces the optimizer step of the reference's
  * training loop (trainers/horovod_trainer.py:113-116, torch.optim.Adam).
  * ---------------------------------------------------------------------- */
 int dro_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
-                  const float* step, float lr, float beta1, float beta2, float eps,
-                  float weight_decay, void* stream);
+                  const float* step, const float* hyper, void* stream);
 
 #ifdef __cplusplus
 }

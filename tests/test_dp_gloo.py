@@ -30,6 +30,27 @@ class Toy(nn.Module):
         return {"loss": ((y - batch["y"]) ** 2).mean().reshape(1)}
 
 
+class ToySkip(Toy):
+    """Toy plus a head `d` that some ranks skip on some steps: its gradient
+    never arrives there, so its bucket completes on one rank and not on the
+    other (the collective order must still pair up)."""
+
+    def __init__(self):
+        super().__init__()
+        self.d = nn.Linear(8, 4)
+
+    def forward(self, batch):
+        f = torch.relu(self.b(torch.relu(self.a(batch["x"])))).mean((2, 3))
+        y = self.c(f)
+        if batch["use_d"]:
+            y = y + self.d(f)
+        return {"loss": ((y - batch["y"]) ** 2).mean().reshape(1)}
+
+
+# (step, rank) pairs on which ToySkip leaves `d` out
+SKIP = {(1, 1), (2, 0), (4, 0), (4, 1)}
+
+
 def data(rank, step, n=4):
     g = torch.Generator().manual_seed(100 * step + rank)
     return {"x": torch.randn(n, 3, 8, 8, generator=g), "y": torch.randn(n, 4, generator=g)}
@@ -43,17 +64,20 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, steps, out):
+def _worker(rank, world, port, steps, out, skip=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, init_distributed
     init_distributed("gloo")
     torch.manual_seed(rank)            # different init per rank: broadcast must fix it
-    model = Toy()
+    model = ToySkip() if skip else Toy()
     dead0 = model.dead.weight.detach().clone()
-    tr = DataParallelTrainer(model, lr=1e-2, bucket_mb=0.0005)
+    tr = DataParallelTrainer(model, lr=1e-2, bucket_mb=1e-7 if skip else 0.0005)
     for s in range(steps):
-        tr.step(data(rank, s))
+        batch = data(rank, s)
+        if skip:
+            batch["use_d"] = (s, rank) not in SKIP
+        tr.step(batch)
     flat = torch.cat([p.detach().flatten() for p in model.parameters()])
     out[rank] = (flat, len(tr.grads.buckets), torch.equal(model.dead.weight, dead0) or rank)
     dist.barrier()
@@ -80,5 +104,39 @@ def test_two_rank_gloo_matches_single_process():
     for s in range(steps):
         a, b = data(0, s), data(1, s)
         tr.step({k: torch.cat([a[k], b[k]]) for k in a})
+    ref = torch.cat([p.detach().flatten() for p in model.parameters()])
+    assert torch.allclose(p0, ref, rtol=1e-5, atol=1e-6), float((p0 - ref).abs().max())
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_missing_gradient_on_one_rank():
+    """A parameter whose gradient arrives on one rank only (or on neither) on
+    some steps: every bucket is still all-reduced exactly once per step on
+    every rank, in the same order -- ranks stay identical and equal to one
+    process minimising the mean of the two per-rank losses."""
+    steps = 6
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_worker, args=(2, port, steps, out, True), nprocs=2, join=True)
+        res = dict(out)
+    (p0, nb0, _), (p1, _, _) = res[0], res[1]
+    assert nb0 > 4, "expected one bucket per parameter"
+    assert torch.equal(p0, p1), "ranks diverged"
+    torch.manual_seed(0)
+    model = ToySkip()
+    opt = torch.optim.Adam([p for p in model.parameters()], lr=1e-2)
+    for s in range(steps):
+        opt.zero_grad(set_to_none=True)
+        loss = 0.0
+        for r in range(2):
+            b = data(r, s)
+            b["use_d"] = (s, r) not in SKIP
+            loss = loss + 0.5 * model(b)["loss"].sum()
+        loss.backward()
+        for p in model.parameters():
+            if p.grad is None and p is not model.dead.weight and p is not model.dead.bias:
+                p.grad = torch.zeros_like(p)       # the DP path steps it with a zero gradient
+        opt.step()
     ref = torch.cat([p.detach().flatten() for p in model.parameters()])
     assert torch.allclose(p0, ref, rtol=1e-5, atol=1e-6), float((p0 - ref).abs().max())
