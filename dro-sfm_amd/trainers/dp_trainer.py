@@ -292,6 +292,9 @@ class FlatAdam(torch.optim.Optimizer):
         self.exp_avg = torch.zeros_like(flat_param)
         self.exp_avg_sq = torch.zeros_like(flat_param)
         self.step_t = torch.zeros((), device=flat_param.device, dtype=torch.float32)
+        # the flat moments + step are this optimizer's whole state (restored in
+        # place by callers that snapshot optimizer.state, e.g. test_graph_step)
+        self.state["flat"] = {"step": self.step_t, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
         self.hyper_t = torch.zeros(5, device=flat_param.device, dtype=torch.float32)
         self._hyper_host = None
         self.sync_hyper()
