@@ -40,269 +40,11 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "conv_common.hpp"
 #include "dro_common.hpp"
 
 namespace dro {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int kBN = 64;   // pixels per tile (forward / data gradient)
-constexpr int kBK = 32;   // reduction chunk (forward / data gradient)
-constexpr int kWP = 64;   // pixels per weight-gradient chunk
-constexpr int kMaxSrc = 4;
-
-struct Slice {            // channels [coff, coff+C) of a [B, ctot, H, W] tensor
-  const float* p;
-  int C, ctot, coff;
-  int bcast;              // 1: a [B, ctot, 1, 1] tensor broadcast over H x W
-};
-
-// exact n / d for 0 <= n < 2^16, 1 <= d < 2^12: umulhi(n, ceil(2^32/d)), d = 1 apart
-struct FastDiv {
-  unsigned m;
-  int one;
-};
-__device__ __forceinline__ int fdiv(int n, FastDiv f) {
-  return f.one ? n : (int)__umulhi((unsigned)n, f.m);
-}
-
-// exact n / d for any 32-bit n, d >= 1: m = floor((2^32 - 1) / d) leaves the
-// mulhi estimate at most 2 low (host-computed; a few scalar ops per division)
-struct Div32 {
-  unsigned m, d;
-};
-__device__ __forceinline__ unsigned udiv(unsigned n, Div32 f) {
-  unsigned q = __umulhi(n, f.m);
-  unsigned r = n - q * f.d;
-  if (r >= f.d) {
-    ++q;
-    r -= f.d;
-  }
-  if (r >= f.d) ++q;
-  return q;
-}
-
-struct ConvGeom {
-  int B, H, W, Cin, Cout, KH, KW, PH, PW;
-};
-
-struct IgArgs {
-  ConvGeom g;
-  Slice src[kMaxSrc];     // forward inputs (virtual concat); read by index from the kernarg segment
-  int cbase[kMaxSrc];     // first virtual channel of each source (Cin for unused)
-  const float* weight;    // [Cout][Cin][KH][KW]
-  const float* bias;      // [Cout] or nullptr
-  float alpha;            // output scale (act none only)
-  float* out;             // forward output slice base
-  int out_ctot, out_coff;
-  Slice z, h;             // EPI 1: out = (1-z) h + z q, q = tanh(acc + b); EPI 2: h for r*h
-  float* aux;             // EPI 1: q (saved for the backward); EPI 2: r*h  (dense, [B, hd, H, W])
-  int hd;                 // EPI 2: rows >= hd are the r gate
-  const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation (or w.r.t. the
-                          // output when folded: then G_pre = galpha * G * act'(gy))
-  const float* gy;        // folded activation: saved output y, dense [B, Cout, H, W]
-  float galpha;           // folded output scale
-  float* gsrc[kMaxSrc];   // data-gradient targets per source (nullable)
-  int gsrc_ctot[kMaxSrc], gsrc_coff[kMaxSrc], gsrc_acc[kMaxSrc];
-  float* gweight;         // [Cout][Cin][KH][KW]
-  float* gbias;           // [Cout]
-  int wacc;               // 1: add into gweight / gbias instead of overwriting
-  int rows;               // GEMM rows: Cout (forward) / Cin (data gradient)
-  int kch;                // channels reduced per tap: Cin (forward) / Cout (data gradient)
-  int K;                  // kch * KH * KW
-  FastDiv kdiv, kwdiv, cindiv;
-  int row_tiles;          // tile = pixel_tile * row_tiles + row_tile
-  int chunks_per_split;   // split-K (gridDim.y > 1): partials to `part`
-  float* part;            // [ksplit][rows][P] (igemm) / [splits][Cout][NK+1] (wgrad)
-  float* bpart;           // [splits][Cout] bias partials (halo weight gradient)
-  int otiles;             // weight gradient: output-channel tiles
-  long long pchunk;       // weight gradient: pixels per split
-  // halo-tiled direct convolution (KH*KW > 1): TH x TW pixel tiles, the input
-  // tile + halo staged once per channel chunk of CK channels
-  int TH, TW, HWd, HPAD, tiles_x, tiles_img, CK;
-  Div32 rt_div, ti_div, tx_div;  // halo kernel: row_tiles, tiles_img, tiles_x
-  // halo forward: source s channel ch of image b starts at byte address
-  // sq0[s] + b * sqb[s] + ch * sr[s]; sm[s] = 0 for broadcast sources, else ~0
-  unsigned long long sq0[kMaxSrc], sqb[kMaxSrc];
-  unsigned sr[kMaxSrc], sm[kMaxSrc];
-  unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
-  int dbg;                      // diagnostics with stamps on (env DRO_CONV_DBG): 1 skip the K
-                                // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)
-};
-
-__device__ __forceinline__ float act_fwd(float v, int act) {
-  switch (act) {
-    case 1: return fmaxf(v, 0.f);
-    case 2: return 1.f / (1.f + expf(-v));
-    case 3: return tanhf(v);
-    default: return v;
-  }
-}
-
-// d act / d pre, expressed through the saved activation output y
-__device__ __forceinline__ float act_bwd(float y, int act) {
-  switch (act) {
-    case 1: return y > 0.f ? 1.f : 0.f;
-    case 2: return y * (1.f - y);
-    case 3: return 1.f - y * y;
-    default: return 1.f;
-  }
-}
-
-__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-// Blocks that share a pixel tile get consecutive logical ids on one XCD
-// (hardware dispatch is round-robin over the 8 XCDs by block id).
-__device__ __forceinline__ int xcd_remap(int id, int total) {
-  const int xcd = id & 7, local = id >> 3, per = total >> 3, rem = total & 7;
-  return (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + local;
-}
-
-// The source descriptors are read straight from the kernel-argument segment
-// with a computed index (s_load for a wave-uniform channel).  Selecting among
-// struct fields instead gets rewritten by the compiler into a dynamically
-// indexed copy of the arguments in scratch.
-typedef __attribute__((address_space(4))) const Slice* KSlice;
-
-__device__ __forceinline__ KSlice kernarg_srcs() {
-  return (KSlice)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                  offsetof(IgArgs, src));
-}
-
-// Element offset of virtual channel ch in its source is b * A + Bc + (M ? pixel : 0)
-// (broadcast sources: A = ctot, M = 0).  32-bit element offsets (checked on the host).
-struct RowDesc {
-  const float* p;
-  unsigned A, Bc;
-  bool M;
-};
-
-__device__ __forceinline__ RowDesc row_desc_at(KSlice base, int cb1, int cb2, int cb3, int ch,
-                                               unsigned HW) {
-  const int si = (ch >= cb1) + (ch >= cb2) + (ch >= cb3);
-  const KSlice ks = base + si;
-  const int cl = ch - (si == 0 ? 0 : si == 1 ? cb1 : si == 2 ? cb2 : cb3);
-  const int ctot = ks->ctot, coff = ks->coff, bc = ks->bcast;
-  RowDesc d;
-  d.p = ks->p;
-  d.A = bc ? (unsigned)ctot : (unsigned)ctot * HW;
-  d.Bc = bc ? (unsigned)(coff + cl) : (unsigned)(coff + cl) * HW;
-  d.M = !bc;
-  return d;
-}
-
-__device__ __forceinline__ RowDesc row_desc(int cb1, int cb2, int cb3, int ch, unsigned HW) {
-  return row_desc_at(kernarg_srcs(), cb1, cb2, cb3, ch, HW);
-}
-
-__device__ __forceinline__ void grad_put(float* dst, int ctot, int coff, int accf, int cl, int eb,
-                                         size_t epix, size_t HW, float v) {
-  if (!dst) return;
-  float* q = dst + ((size_t)eb * ctot + coff + cl) * HW + epix;
-  *q = accf ? (*q + v) : v;
-}
-
-// final value of GEMM element (row, pixel) -> destination
-template <int MODE, int ACT, int EPI>
-__device__ __forceinline__ void epi_store(const IgArgs& a, int row, int eb, size_t epix, size_t HW,
-                                          float acc) {
-  if (MODE == 0) {
-    float v = acc + (a.bias ? a.bias[row] : 0.f);
-    v = a.alpha * act_fwd(v, ACT);
-    if (EPI == 1) {
-      const float z = a.z.p[((size_t)eb * a.z.ctot + a.z.coff + row) * HW + epix];
-      const float hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + row) * HW + epix];
-      a.aux[((size_t)eb * a.rows + row) * HW + epix] = v;
-      v = (1.f - z) * hv + z * v;
-    }
-    if (EPI == 2 && row >= a.hd) {
-      const int c = row - a.hd;
-      const float hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + c) * HW + epix];
-      a.aux[((size_t)eb * a.hd + c) * HW + epix] = v * hv;
-    }
-    a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
-  } else {
-    if (row < a.cbase[1])
-      grad_put(a.gsrc[0], a.gsrc_ctot[0], a.gsrc_coff[0], a.gsrc_acc[0], row, eb, epix, HW, acc);
-    else if (row < a.cbase[2])
-      grad_put(a.gsrc[1], a.gsrc_ctot[1], a.gsrc_coff[1], a.gsrc_acc[1], row - a.cbase[1], eb, epix, HW, acc);
-    else if (row < a.cbase[3])
-      grad_put(a.gsrc[2], a.gsrc_ctot[2], a.gsrc_coff[2], a.gsrc_acc[2], row - a.cbase[2], eb, epix, HW, acc);
-    else
-      grad_put(a.gsrc[3], a.gsrc_ctot[3], a.gsrc_coff[3], a.gsrc_acc[3], row - a.cbase[3], eb, epix, HW, acc);
-  }
-}
-
-// Epilogue of one 32x32 MFMA accumulator (16 rows per lane, row(r) = rbase +
-// (r & 3) + 8 (r >> 2)) at pixel (eb, epix): every operand the 16 rows need
-// (bias, z and h of the GRU epilogues, the old value of an accumulated
-// gradient) is loaded before the first is used -- one memory round trip for
-// the tile instead of one per row (measured: the per-row form spent longer
-// in the epilogue than in the whole K loop).
-template <int MODE, int ACT, int EPI>
-__device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int rbase, int eb,
-                                         size_t epix, size_t HW) {
-  const int rows = a.rows;
-  if (MODE == 0) {
-    float bv[16], zv[EPI == 1 ? 16 : 1], hv[EPI != 0 ? 16 : 1];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = rbase + (r & 3) + 8 * (r >> 2);
-      const int rr = row < rows ? row : 0;
-      bv[r] = a.bias ? a.bias[rr] : 0.f;
-      if (EPI == 1) {
-        zv[r] = a.z.p[((size_t)eb * a.z.ctot + a.z.coff + rr) * HW + epix];
-        hv[r] = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + rr) * HW + epix];
-      }
-      if (EPI == 2) {
-        const int c = rr >= a.hd ? rr - a.hd : 0;
-        hv[r] = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + c) * HW + epix];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = rbase + (r & 3) + 8 * (r >> 2);
-      if (row >= rows) continue;
-      float v = acc[r] + bv[r];
-      v = a.alpha * act_fwd(v, ACT);
-      if (EPI == 1) {
-        a.aux[((size_t)eb * a.rows + row) * HW + epix] = v;
-        v = (1.f - zv[r]) * hv[r] + zv[r] * v;
-      }
-      if (EPI == 2 && row >= a.hd)
-        a.aux[((size_t)eb * a.hd + (row - a.hd)) * HW + epix] = v * hv[r];
-      a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
-    }
-  } else {
-    float* dst[16];
-    bool accf[16];
-    float old[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = rbase + (r & 3) + 8 * (r >> 2);
-      const int si = row >= rows ? -1 : (row >= a.cbase[1]) + (row >= a.cbase[2]) + (row >= a.cbase[3]);
-      float* base = nullptr;
-      int ctot = 0, coff = 0, cl = 0, ac = 0;
-      if (si >= 0) {
-        const int cb = si == 0 ? 0 : si == 1 ? a.cbase[1] : si == 2 ? a.cbase[2] : a.cbase[3];
-        base = si == 0 ? a.gsrc[0] : si == 1 ? a.gsrc[1] : si == 2 ? a.gsrc[2] : a.gsrc[3];
-        ctot = si == 0 ? a.gsrc_ctot[0] : si == 1 ? a.gsrc_ctot[1] : si == 2 ? a.gsrc_ctot[2] : a.gsrc_ctot[3];
-        coff = si == 0 ? a.gsrc_coff[0] : si == 1 ? a.gsrc_coff[1] : si == 2 ? a.gsrc_coff[2] : a.gsrc_coff[3];
-        ac = si == 0 ? a.gsrc_acc[0] : si == 1 ? a.gsrc_acc[1] : si == 2 ? a.gsrc_acc[2] : a.gsrc_acc[3];
-        cl = row - cb;
-      }
-      dst[r] = base ? base + ((size_t)eb * ctot + coff + cl) * HW + epix : nullptr;
-      accf[r] = base && ac;
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) old[r] = accf[r] ? *dst[r] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (dst[r]) *dst[r] = accf[r] ? old[r] + acc[r] : acc[r];
-  }
-}
 
 // ------------------------------------------------------------------ forward / data gradient
 // MODE 0: out[o, p]  = sum_{tap, c} W[o, c, tap] * X[c, p + d(tap)]   (+ epilogue)
@@ -830,37 +572,6 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   stamp(14);
 }
 
-// sum of n partials p[0], p[stride], ... in a fixed order (4 interleaved
-// chains, combined at the end): the loads are independent and issue together
-__device__ __forceinline__ float split_sum(const float* __restrict__ p, size_t stride, int n) {
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int i = 0;
-  for (; i + 4 <= n; i += 4) {
-    s0 += p[(size_t)i * stride];
-    s1 += p[(size_t)(i + 1) * stride];
-    s2 += p[(size_t)(i + 2) * stride];
-    s3 += p[(size_t)(i + 3) * stride];
-  }
-  for (; i < n; ++i) s0 += p[(size_t)i * stride];
-  return (s0 + s1) + (s2 + s3);
-}
-
-// split-K finish: sum the partials in split order, then the epilogue
-template <int MODE, int ACT, int EPI>
-__global__ __launch_bounds__(256) void igemm_finish_kernel(IgArgs a, int ksplit) {
-  const size_t HW = (size_t)a.g.H * a.g.W;
-  const long long P = (long long)a.g.B * HW;
-  const long long total = (long long)a.rows * P;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    float v = 0.f;
-    v = split_sum(a.part + i, (size_t)total, ksplit);
-    const int row = (int)(i / P);
-    const long long p = i - (long long)row * P;
-    const int eb = (int)(p / (long long)HW);
-    epi_store<MODE, ACT, EPI>(a, row, eb, (size_t)(p - (long long)eb * HW), HW, v);
-  }
-}
 
 // ------------------------------------------------------------------ weight (+ bias) gradient
 // dW[o, n] = sum_p G[o, p] * X[c(n), p + d(tap(n))] with n = tap*Cin + c, and
@@ -1268,21 +979,12 @@ using namespace dro;
 
 namespace {
 
-Div32 make_div32(int d) {
-  Div32 f;
-  f.d = (unsigned)(d > 0 ? d : 1);
-  f.m = 0xFFFFFFFFu / f.d;
-  return f;
-}
-
 FastDiv make_fdiv(int d) {
   FastDiv f;
   f.one = d == 1;
   f.m = d == 1 ? 0u : (unsigned)(((1ULL << 32) + (unsigned long long)d - 1) / (unsigned long long)d);
   return f;
 }
-
-size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 // ---- launch plans (shared by the workspace query and the launches)
 struct IgPlan {
@@ -1444,14 +1146,16 @@ WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
 }
 
 size_t fwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
-  return plan_igemm(Cout, Cin, KH, KW, B, H, W).part_bytes;
+  return std::max(plan_igemm(Cout, Cin, KH, KW, B, H, W).part_bytes,
+                  xconv_part_bytes(Cout, Cin, KH, KW, B, H, W));
 }
 
 size_t bwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   const long long P = (long long)B * H * W;
   const int T = KH * KW;
   return align256((size_t)Cout * P * sizeof(float)) +              // pre-activation gradient
-         plan_igemm(Cin, Cout, KH, KW, B, H, W).part_bytes +        // data-gradient split-K
+         std::max(plan_igemm(Cin, Cout, KH, KW, B, H, W).part_bytes,  // data-gradient split-K
+                  xconv_part_bytes(Cin, Cout, KH, KW, B, H, W)) +
          std::max(plan_wgrad(Cin, Cout, T, P).part_bytes,           // weight-gradient partials
                   plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).part_bytes);
 }
@@ -1742,6 +1446,8 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     a.part = reinterpret_cast<float*>(ws);
     return launch_thin<MODE, ACT>(a, pl.ksplit, s);
   }
+  // split-bf16 MFMA engine (xconv.hip) when the caller passed split weights
+  if (a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
@@ -1859,9 +1565,10 @@ extern "C" size_t dro_conv2d_workspace_bytes(int B, int H, int W, int Cin, int C
 
 extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
                                   int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
-                                  float* out, int out_ctot, int out_coff, void* workspace,
-                                  size_t workspace_bytes, void* stream) {
+                                  float* out, int out_ctot, int out_coff, const void* wsplit,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
   IgArgs a = {};
+  a.wsplit = static_cast<const char*>(wsplit);
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
   if (!weight || !out || out_coff < 0 || out_coff + Cout > out_ctot || too_big(B, out_ctot, (long long)H * W)) {
@@ -1892,9 +1599,10 @@ extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* 
 
 extern "C" int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const float* weight,
                                          const float* bias, int B, int H, int W, int hd, int KH, int KW,
-                                         float* zr, float* rh, void* workspace, size_t workspace_bytes,
-                                         void* stream) {
+                                         float* zr, float* rh, const void* wsplit, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
   IgArgs a = {};
+  a.wsplit = static_cast<const char*>(wsplit);
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, 2 * hd, KH, KW);
   if (st) return st;
   if (!weight || !zr || !rh) {
@@ -1925,9 +1633,10 @@ extern "C" int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const 
 extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const float* weight,
                                          const float* bias, int B, int H, int W, int Cout, int KH, int KW,
                                          const dro_slice* z, const dro_slice* h, float* q_out, float* out,
-                                         int out_ctot, int out_coff, void* workspace,
+                                         int out_ctot, int out_coff, const void* wsplit, void* workspace,
                                          size_t workspace_bytes, void* stream) {
   IgArgs a = {};
+  a.wsplit = static_cast<const char*>(wsplit);
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
   if (!weight || !out || !q_out || !z || !h || !z->data || !h->data) {
@@ -1957,9 +1666,10 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
                                    const dro_slice* y, const float* dout, float* const* grad_srcs,
                                    const int* grad_ctot, const int* grad_coff,
                                    const int* grad_accumulate, float* grad_weight, float* grad_bias,
-                                   int grad_weight_accumulate, void* workspace, size_t workspace_bytes,
-                                   void* stream) {
+                                   int grad_weight_accumulate, const void* wsplit, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
   IgArgs a = {};
+  a.wsplit = static_cast<const char*>(wsplit);   // transposed layout: the data gradient
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
   if (st) return st;
   const bool pre = act != 0 || alpha != 1.f;
@@ -1999,7 +1709,8 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   char* ws = static_cast<char*>(workspace);
   char* ws_pre = ws;
   char* ws_ig = ws_pre + align256((size_t)Cout * P * sizeof(float));
-  char* ws_wg = ws_ig + plan_igemm(a.g.Cin, Cout, KH, KW, B, H, W).part_bytes;
+  char* ws_wg = ws_ig + std::max(plan_igemm(a.g.Cin, Cout, KH, KW, B, H, W).part_bytes,
+                                 xconv_part_bytes(a.g.Cin, Cout, KH, KW, B, H, W));
   // fold the activation derivative into the halo kernels' G staging when both
   // gradients run there (dense y); otherwise form G first
   const WhPlan wh = plan_wgrad_halo(a.g.Cin, Cout, KH, KW, B, H, W);

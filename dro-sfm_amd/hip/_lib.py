@@ -58,10 +58,12 @@ def load():
     _sig(lib.dro_conv2d_workspace_bytes, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_plan, I, I, I, I, I, I, I, P)
     _sig(lib.dro_debug_conv_stamps, P)
-    _sig(lib.dro_conv2d_forward, P, I, P, P, I, I, I, I, I, I, I, F, P, I, I, P, Z, S)
-    _sig(lib.dro_convgru_gates_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, Z, S)
-    _sig(lib.dro_convgru_blend_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, Z, S)
-    _sig(lib.dro_conv2d_backward, P, I, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, I, P, Z, S)
+    _sig(lib.dro_weight_split_bytes, I, I, I, I, I, restype=Z)
+    _sig(lib.dro_weight_split, P, I, I, I, I, P, P, S)
+    _sig(lib.dro_conv2d_forward, P, I, P, P, I, I, I, I, I, I, I, F, P, I, I, P, P, Z, S)
+    _sig(lib.dro_convgru_gates_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, P, Z, S)
+    _sig(lib.dro_convgru_blend_forward, P, I, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, Z, S)
+    _sig(lib.dro_conv2d_backward, P, I, P, I, I, I, I, I, I, I, F, P, P, P, P, P, P, P, P, I, P, P, Z, S)
     _sig(lib.dro_conv2d_weight_grad_multi_workspace_bytes, I, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_weight_grad_multi, P, I, I, I, I, I, I, I, I, I, F, P, P, I, P, Z, S)
     _sig(lib.dro_adam_step, P, P, P, P, ctypes.c_longlong, P, P, S)
@@ -80,6 +82,7 @@ EXPORTED = (
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
+    "dro_weight_split_bytes", "dro_weight_split",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",

@@ -29,6 +29,13 @@ launch + one split reduction per use, each use is queued (sources, output
 gradient, saved output kept alive) and all uses of a weight are reduced by ONE
 dro_conv2d_weight_grad_multi launch at the end of backward (engine final
 callback, before the trainer's gradient all-reduce).  set_batched_weight_grads.
+
+Split-bf16 engine (set_split_engine, default off): the 1x5 / 5x1 / 3x3 / 1x1
+forward and data-gradient GEMMs run on bf16 MFMA over operands split into three
+bf16 terms (csrc/xconv.hip, f32 accuracy at 2.67x the f32 MFMA rate).  Each
+weight is split (both GEMM layouts) at its first use in a forward pass of the
+network (one split per weight_grad_scope; every call outside a scope splits
+afresh) and the split buffers are saved for the backward.
 """
 import contextlib
 import ctypes
@@ -82,16 +89,56 @@ class WeightGradScope:
 
 
 _SCOPE = [None]
+_GEN = [0, 0]      # [weight generation, open scopes]: splits are reused within one generation
 
 
 @contextlib.contextmanager
 def weight_grad_scope():
     prev = _SCOPE[0]
     _SCOPE[0] = WeightGradScope() if torch.is_grad_enabled() else None
+    if _GEN[1] == 0:
+        _GEN[0] += 1       # a new forward pass: weights may have changed since the last one
+    _GEN[1] += 1
     try:
         yield _SCOPE[0]
     finally:
         _SCOPE[0] = prev
+        _GEN[1] -= 1
+
+
+_XCONV = [False]   # measured: not faster than the f32 engine at the step's shapes
+_XSHAPES = {(1, 5), (5, 1), (3, 3), (1, 1)}
+_SPLITS = {}       # (data_ptr, shape, device) -> [generation, fwd split, bwd split]
+
+
+def set_split_engine(enabled):
+    """Split-bf16 MFMA engine for the halo convs (True) or the f32-MFMA engine
+    (False, default: the faster of the two at the update-block shapes)."""
+    _XCONV[0] = bool(enabled)
+
+
+def _wsplit(weight):
+    """(fwd, bwd) split-bf16 copies of a contiguous weight for the xconv engine,
+    or (None, None) when the f32 engine runs this conv."""
+    if not _XCONV[0] or tuple(weight.shape[2:]) not in _XSHAPES:
+        return None, None
+    lib = _lib.load()
+    Cout, Cin, KH, KW = weight.shape
+    key = (weight.data_ptr(), tuple(weight.shape), weight.device)
+    ent = _SPLITS.get(key)
+    if ent is None:
+        if len(_SPLITS) > 512:   # drop splits of weights unused for two forward passes
+            for k in [k for k, v in _SPLITS.items() if v[0] < _GEN[0] - 1]:
+                del _SPLITS[k]
+        nf = int(lib.dro_weight_split_bytes(Cout, Cin, KH, KW, 0))
+        nb = int(lib.dro_weight_split_bytes(Cout, Cin, KH, KW, 1))
+        ent = _SPLITS[key] = [-1, torch.empty(nf // 2, dtype=torch.int16, device=weight.device),
+                              torch.empty(nb // 2, dtype=torch.int16, device=weight.device)]
+    if ent[0] != _GEN[0] or _GEN[1] == 0:
+        check(lib.dro_weight_split(ptr(weight), Cout, Cin, KH, KW, ptr(ent[1]), ptr(ent[2]),
+                                   stream_of(weight)), "dro_weight_split")
+        ent[0] = _GEN[0]
+    return ent[1], ent[2]
 
 
 def current_scope():
@@ -309,9 +356,11 @@ class _Conv2d(torch.autograd.Function):
         weight = weight.contiguous()
         out = _dense_out(srcs, Cout)
         ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, out.device)
+        wf, wb = _wsplit(weight)
         check(lib.dro_conv2d_forward(_slices(srcs), len(srcs), ptr(weight), ptr(bias), B, H, W, Cout, KH, KW,
-                                     act, ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(ws), nws,
+                                     act, ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(wf), ptr(ws), nws,
                                      stream_of(out)), "dro_conv2d_forward")
+        ctx.wsplit = wb
         ctx.save_for_backward(weight, out if act else None, *srcs)
         ctx.sinks = [_sink_of(x) for x in srcs]
         ctx.meta = (act, alpha, bias is not None)
@@ -346,8 +395,8 @@ class _Conv2d(torch.autograd.Function):
                 ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
                 check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                               act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                              ptr(gout), ptrs, ctot, coff, acc, None, None, 0, ptr(ws), nws,
-                                              stream_of(gout)), "dro_conv2d_backward(data)")
+                                              ptr(gout), ptrs, ctot, coff, acc, None, None, 0, ptr(ctx.wsplit),
+                                              ptr(ws), nws, stream_of(gout)), "dro_conv2d_backward(data)")
             if _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None):
                 return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
             side = _fork_side()
@@ -357,7 +406,7 @@ class _Conv2d(torch.autograd.Function):
                 check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                               act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
                                               ptr(gout), None, None, None, None, ptr(gw),
-                                              ptr(gb) if has_bias else None, 1, ptr(ws), nws,
+                                              ptr(gb) if has_bias else None, 1, None, ptr(ws), nws,
                                               stream_of(gout)), "dro_conv2d_backward(weight)")
             return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
         want_w = need[0] or (has_bias and need[1])
@@ -371,8 +420,8 @@ class _Conv2d(torch.autograd.Function):
         ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
         check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
                                       act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), wacc, ptr(ws), nws,
-                                      stream_of(gout)), "dro_conv2d_backward")
+                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), wacc, ptr(ctx.wsplit),
+                                      ptr(ws), nws, stream_of(gout)), "dro_conv2d_backward")
         rw = gw if (first and need[0]) else None
         rb = gb if (first and has_bias and need[1]) else None
         return (rw, rb, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
@@ -427,18 +476,22 @@ class _SepGRUHalf(torch.autograd.Function):
         zr = torch.empty(B, 2 * hd, H, W, device=h.device)
         rh = torch.empty_like(h)
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
+        wq = wq.contiguous()
+        zf, zb = _wsplit(wzr)
+        qf, qb = _wsplit(wq)
         check(lib.dro_convgru_gates_forward(_slices([h, *xs]), 1 + len(xs), ptr(wzr), ptr(bzr), B, H, W, hd,
-                                            KH, KW, ptr(zr), ptr(rh), ptr(ws), nws, st),
+                                            KH, KW, ptr(zr), ptr(rh), ptr(zf), ptr(ws), nws, st),
               "dro_convgru_gates_forward")
         q = torch.empty_like(h)
         hn = torch.empty_like(h)
         z_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, 0, 0)
         h_sl = DroSlice(h.data_ptr(), hd, hd, 0, 0)
         wsq, nwsq = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-        check(lib.dro_convgru_blend_forward(_slices([rh, *xs]), 1 + len(xs), ptr(wq.contiguous()), ptr(bq),
+        check(lib.dro_convgru_blend_forward(_slices([rh, *xs]), 1 + len(xs), ptr(wq), ptr(bq),
                                             B, H, W, hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl),
-                                            ptr(q), ptr(hn), hd, 0, ptr(wsq), nwsq, st),
+                                            ptr(q), ptr(hn), hd, 0, ptr(qf), ptr(wsq), nwsq, st),
               "dro_convgru_blend_forward")
+        ctx.wsplit = (zb, qb)
         ctx.save_for_backward(h, rh, wzr, wq, zr, q, *xs)
         ctx.sinks = [_sink_of(x) for x in xs]
         ctx.scope = scope
@@ -481,7 +534,8 @@ class _SepGRUHalf(torch.autograd.Function):
         ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq.contiguous()), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
-                                      ptr(gwq), ptr(gbq), qacc, ptr(ws), nws, st), "dro_conv2d_backward(q)")
+                                      ptr(gwq), ptr(gbq), qacc, ptr(ctx.wsplit[1]), ptr(ws), nws, st),
+              "dro_conv2d_backward(q)")
         # stage 2: pre-activation grad of r, dh += d(r*h) r
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
@@ -492,7 +546,8 @@ class _SepGRUHalf(torch.autograd.Function):
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
-                                      ptr(gwzr), ptr(gbzr), zacc, ptr(ws), nws, st), "dro_conv2d_backward(zr)")
+                                      ptr(gwzr), ptr(gbzr), zacc, ptr(ctx.wsplit[0]), ptr(ws), nws, st),
+              "dro_conv2d_backward(zr)")
         gz = (gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:]) if zfirst else (None,) * 4
         gq = (gwq, gbq) if qfirst else (None, None)
         return (dh if need[0] else None, *gz, *gq, None, None, *dxs)
@@ -514,7 +569,8 @@ class _SepGRUHalf(torch.autograd.Function):
         ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
-                                      None, None, 0, ptr(ws), nws, st), "dro_conv2d_backward(q data)")
+                                      None, None, 0, ptr(ctx.wsplit[1]), ptr(ws), nws, st),
+              "dro_conv2d_backward(q data)")
         batched = _queue_weight_grad([rh, *xs], wq.shape, 0, 1.0, dq, None, gwq, gbq)
         side = main if batched else _fork_side()  # dq and r*h are final here
         _on_side(side, [] if batched else [dq, rh, wq, *xs])
@@ -523,7 +579,7 @@ class _SepGRUHalf(torch.autograd.Function):
                 wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
                 check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
                                               0, ctypes.c_float(1.0), None, ptr(dq), None, None, None,
-                                              None, ptr(gwq), ptr(gbq), 1, ptr(wsw), nwsw, stream_of(h)),
+                                              None, ptr(gwq), ptr(gbq), 1, None, ptr(wsw), nwsw, stream_of(h)),
                       "dro_conv2d_backward(q weight)")
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
@@ -532,7 +588,8 @@ class _SepGRUHalf(torch.autograd.Function):
         ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
         check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
                                       0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
-                                      None, None, 0, ptr(ws), nws, st), "dro_conv2d_backward(zr data)")
+                                      None, None, 0, ptr(ctx.wsplit[0]), ptr(ws), nws, st),
+              "dro_conv2d_backward(zr data)")
         if _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
             need = ctx.needs_input_grad
             return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
@@ -543,7 +600,7 @@ class _SepGRUHalf(torch.autograd.Function):
             wsw, nwsw = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
             check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
                                           0, ctypes.c_float(1.0), None, ptr(dzr), None, None, None, None,
-                                          ptr(gwzr), ptr(gbzr), 1, ptr(wsw), nwsw, stream_of(h)),
+                                          ptr(gwzr), ptr(gbzr), 1, None, ptr(wsw), nwsw, stream_of(h)),
                   "dro_conv2d_backward(zr weight)")
         need = ctx.needs_input_grad
         return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* ------------------------------------------------------------------------
  * Inverse warp + feature cost.
@@ -229,6 +229,22 @@ typedef struct dro_slice {
 #define DRO_ACT_SIGMOID 2
 #define DRO_ACT_TANH 3
 
+/* Split-bf16 operands (the xconv engine).  dro_weight_split writes a weight
+ * [Cout][Cin][KH][KW] as three bf16 planes w = w0 + w1 + w2 (24 significant
+ * bits): the forward layout `fwd` ([3][Cout][ceil(Cin/32)*KH*KW*32]) and/or the
+ * transposed, tap-flipped data-gradient layout `bwd` ([3][Cin][ceil(Cout/32)*
+ * KH*KW*32]); sizes from dro_weight_split_bytes(..., transposed 0 / 1).  A conv
+ * call given `wsplit` (the layout of its GEMM: fwd for the forward calls, bwd
+ * for the data gradient of dro_conv2d_backward) runs its 1x5 / 5x1 / 3x3 / 1x1
+ * GEMM on bf16 MFMA as six split products per term (a0b0 + a0b1 + a1b0 + a0b2 +
+ * a1b1 + a2b0, f32 accumulation): f32 accuracy (dropped terms < 2^-24 |ab|) at
+ * 2.67x the f32 MFMA rate.  wsplit = NULL: the f32-MFMA engine.  The split
+ * must be redone whenever the weight changes (the Python layer re-splits once
+ * per forward pass).  Replaces the weight side of the same nn.Conv2d calls. */
+size_t dro_weight_split_bytes(int Cout, int Cin, int KH, int KW, int transposed);
+int dro_weight_split(const float* weight, int Cout, int Cin, int KH, int KW, void* fwd, void* bwd,
+                     void* stream);
+
 /* Scratch needed by any conv call below for this shape (split-K partials,
  * weight-gradient partials, the pre-activation gradient); pass a device buffer
  * of at least this size as `workspace`.  No call keeps state in it. */
@@ -250,8 +266,8 @@ int dro_debug_conv_stamps(void* buffer);
 
 int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
                        int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
-                       float* out, int out_ctot, int out_coff, void* workspace,
-                       size_t workspace_bytes, void* stream);
+                       float* out, int out_ctot, int out_coff, const void* wsplit,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* SepConvGRU z|r gates (update.py:64-65 / :71-72) with r*h fused:
  * zr = sigmoid(conv([h; x]) + b) into a dense [B, 2hd, H, W] (z first) and
@@ -259,8 +275,8 @@ int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, con
  * state h (hd channels); weight = cat(convz.weight, convr.weight). */
 int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const float* weight,
                               const float* bias, int B, int H, int W, int hd, int KH, int KW,
-                              float* zr, float* rh, void* workspace, size_t workspace_bytes,
-                              void* stream);
+                              float* zr, float* rh, const void* wsplit, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 /* SepConvGRU candidate with the blend fused (update.py:66-67 / :73-74):
  * q = tanh(conv([r*h; x]) + b) saved to q_out (dense [B, Cout, H, W]) and
@@ -268,8 +284,8 @@ int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const float* weig
 int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const float* weight,
                               const float* bias, int B, int H, int W, int Cout, int KH, int KW,
                               const dro_slice* z, const dro_slice* h, float* q_out, float* out,
-                              int out_ctot, int out_coff, void* workspace, size_t workspace_bytes,
-                              void* stream);
+                              int out_ctot, int out_coff, const void* wsplit, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 /* Gradients of dro_conv2d_forward given dout [B,Cout,H,W] (dense) and, for
  * act != 0, the saved activation output y (the pre-activation gradient
@@ -284,8 +300,8 @@ int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, in
                         int Cout, int KH, int KW, int act, float alpha, const dro_slice* y,
                         const float* dout, float* const* grad_srcs, const int* grad_ctot,
                         const int* grad_coff, const int* grad_accumulate, float* grad_weight,
-                        float* grad_bias, int grad_weight_accumulate, void* workspace,
-                        size_t workspace_bytes, void* stream);
+                        float* grad_bias, int grad_weight_accumulate, const void* wsplit,
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* Weight (+ bias) gradient of ONE weight over several convolutions that use it
  * (the recurrent update blocks apply each weight once per iteration): one

@@ -6,7 +6,8 @@ Shapes are the update-block convolutions of networks/optim/update.py
 SepConvGRU 1x5 / 5x1 gates over [h, context, projection, depth|pose-map]
 virtual concatenations, projection-encoder 7x7/3x3/1x1 convs, heads, the
 0.25-scaled mask conv.  Tolerance 1e-4 relative (max|a-b| / max|b|), the
-north_star bound; f32 MFMA accumulates in exact fp32.
+north_star bound; f32 MFMA accumulates in exact fp32, the split-bf16 engine
+sums six bf16 products per term (dropped terms < 2^-24 |ab|) in fp32.
 """
 import pytest
 import torch
@@ -23,6 +24,17 @@ def hip():
     from dro_sfm_amd.hip import _lib
     _lib.load()
     return H
+
+
+@pytest.fixture(params=["split", "f32"])
+def engine(request, hip):
+    """Both engines: split-bf16 MFMA (csrc/xconv.hip, 1x5/5x1/3x3/1x1) and f32 MFMA
+    (csrc/conv.hip, the default); the same f32-level tolerance for both."""
+    from dro_sfm_amd.hip import conv as C
+    C.set_split_engine(request.param == "split")
+    prev = C._XCONV[0]
+    yield request.param
+    C.set_split_engine(prev)
 
 
 def rel(a, b):
@@ -64,7 +76,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_conv2d_fwd_bwd(hip, case):
+def test_conv2d_fwd_bwd(hip, engine, case):
     srcs_spec, Cout, (KH, KW), act, alpha, B, H, W = CASES[case]
     g = torch.Generator().manual_seed(100 + case)
     bases, views = zip(*[make_src(k, B, C, H, W, g) for k, C in srcs_spec])
@@ -106,7 +118,7 @@ def _gru_ref(h, xs, wz, bz, wr, br, wq, bq, pad):
 
 @pytest.mark.parametrize("kernel", [(1, 5), (5, 1)])
 @pytest.mark.parametrize("pose", [False, True])
-def test_sepconvgru_half(hip, kernel, pose):
+def test_sepconvgru_half(hip, engine, kernel, pose):
     """One SepConvGRU direction (update.py:59-70) fused: 2 launches forward."""
     B, hd, H, W = 2, 64, 24, 40
     g = torch.Generator().manual_seed(7 + pose)
@@ -272,3 +284,38 @@ def test_weight_grad_multi_rejects(hip):
     assert lib.dro_conv2d_weight_grad_multi(two, 2, 2, *args) == -2           # no workspace
     assert lib.dro_conv2d_weight_grad_multi(arr, 1, 1, B, H, W, 4, 3, 3, 1, ctypes.c_float(1.0),
                                             gw.data_ptr(), None, 1, None, 0, None) == -1   # relu, no y
+
+
+def test_weight_split_exact(hip):
+    """dro_weight_split: the three bf16 planes sum back to the f32 weight (within
+    2^-24 relative per element, the f32 rounding unit) in both layouts; padded
+    channels are zero; the data-gradient layout is the transposed, tap-flipped
+    weight."""
+    import ctypes  # noqa: F401
+    from dro_sfm_amd.hip import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(5)
+    Cout, Cin, KH, KW = 45, 37, 3, 3
+    T = KH * KW
+    w = torch.randn(Cout, Cin, KH, KW, generator=g) * torch.logspace(-6, 3, Cout).view(-1, 1, 1, 1)
+    wd = w.to(DEV)
+    nf = lib.dro_weight_split_bytes(Cout, Cin, KH, KW, 0)
+    nb = lib.dro_weight_split_bytes(Cout, Cin, KH, KW, 1)
+    fw = torch.empty(nf // 2, dtype=torch.int16, device=DEV)
+    bw = torch.empty(nb // 2, dtype=torch.int16, device=DEV)
+    assert lib.dro_weight_split(_lib.ptr(wd), Cout, Cin, KH, KW, _lib.ptr(fw), _lib.ptr(bw), None) == 0
+    torch.cuda.synchronize()
+
+    def planes(buf, rows, kc):
+        nch = (kc + 31) // 32
+        p = buf.cpu().view(torch.bfloat16).float().view(3, rows, nch, T, 32)
+        return (p[0].double() + p[1].double() + p[2].double()), p
+    s, p = planes(fw, Cout, Cin)
+    ref = w.permute(0, 1, 2, 3).reshape(Cout, Cin, T).double()
+    got = s.permute(0, 1, 3, 2).reshape(Cout, -1, T)[:, :Cin]        # [Cout][c][tap]
+    assert ((got - ref).abs() <= ref.abs() * 2.0 ** -24).all()
+    assert (s.permute(0, 1, 3, 2).reshape(Cout, -1, T)[:, Cin:] == 0).all()
+    s, _ = planes(bw, Cin, Cout)
+    refb = w.reshape(Cout, Cin, T).flip(2).permute(1, 0, 2).double()  # [Cin][o][flipped tap]
+    gotb = s.permute(0, 1, 3, 2).reshape(Cin, -1, T)[:, :Cout]
+    assert ((gotb - refb).abs() <= refb.abs() * 2.0 ** -24).all()

@@ -14,7 +14,10 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from dro_sfm_amd.hip import _lib  # noqa: E402
+from dro_sfm_amd.hip import conv as hconv  # noqa: E402
 from dro_sfm_amd.hip.conv import _slices, _workspace  # noqa: E402
+
+SPLIT = [True]   # STAMP_ENGINE=f32 for the f32-MFMA engine
 
 
 def run(name, B, hd, H, W, cins, KH, KW, gates=True, reps=5):
@@ -33,16 +36,18 @@ def run(name, B, hd, H, W, cins, KH, KW, gates=True, reps=5):
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     stamps = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
     sl = _slices(srcs)
+    wf = hconv._wsplit(w)[0] if SPLIT[0] else None
 
     def launch():
         if gates:
             _lib.check(lib.dro_convgru_gates_forward(sl, len(srcs), _lib.ptr(w), _lib.ptr(bias), B, H, W, hd,
-                                                     KH, KW, _lib.ptr(out), _lib.ptr(rh), _lib.ptr(ws), nws, st),
+                                                     KH, KW, _lib.ptr(out), _lib.ptr(rh), _lib.ptr(wf), _lib.ptr(ws), nws,
+                                                     st),
                        "gates")
         else:
             _lib.check(lib.dro_conv2d_forward(sl, len(srcs), _lib.ptr(w), _lib.ptr(bias), B, H, W, cout, KH, KW,
-                                              1, ctypes.c_float(1.0), _lib.ptr(out), cout, 0, _lib.ptr(ws), nws,
-                                              st), "conv")
+                                              1, ctypes.c_float(1.0), _lib.ptr(out), cout, 0, _lib.ptr(wf), _lib.ptr(ws),
+                                              nws, st), "conv")
     for _ in range(3):
         launch()
     torch.cuda.synchronize()
@@ -86,7 +91,10 @@ def main():
 
 
 if __name__ == "__main__":
+    SPLIT[0] = os.environ.get("STAMP_ENGINE", "split") == "split"
+    hconv.set_split_engine(SPLIT[0])
     for dbg in os.environ.get("STAMP_DBG", "0").split(","):
         os.environ["DRO_CONV_DBG"] = dbg
-        print(f"######## DRO_CONV_DBG={dbg} (1 no loads, 2 no MFMA, 4 no LDS stores in the K loop)")
+        print(f"######## engine {'split-bf16' if SPLIT[0] else 'f32'}, DRO_CONV_DBG={dbg} "
+              "(1 no loads, 2 no MFMA, 4 no LDS stores in the K loop)")
         main()
