@@ -389,10 +389,15 @@ def main():
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",
                     help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
-    ap.add_argument("--grad-sinks", action="store_true",
-                    help="in-place gradient sinks for shared tensors (A/B; default off)")
+    ap.add_argument("--concurrent-blocks", action="store_true",
+                    help="pose update block on a side stream beside the depth block (A/B)")
+    ap.add_argument("--no-grad-sinks", action="store_true",
+                    help="autograd's per-use gradient sums instead of in-place gradient sinks (A/B)")
     ap.add_argument("--no-fused-bn", action="store_true",
                     help="encoder BatchNorm+ReLU through PyTorch's kernels (A/B)")
+    ap.add_argument("--miopen-find", choices=("on", "off"), default="off",
+                    help="torch.backends.cudnn.benchmark (MIOpen Find for the library convs; the "
+                         "reference sets it, horovod_trainer.py:34)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
@@ -401,6 +406,7 @@ def main():
     if args.batch is None:
         args.batch = WL["batch"]
     torch.backends.cudnn.enabled = not args.no_miopen
+    torch.backends.cudnn.benchmark = args.miopen_find == "on"
     if args.roofline_only:
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         torch.cuda.set_device(dev)
@@ -413,10 +419,11 @@ def main():
     _update.set_conv_backend(args.conv_backend)
     from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
     _dpn.set_concurrent_encoders(args.concurrent_encoders)
+    _dpn.set_concurrent_blocks(args.concurrent_blocks)
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     from dro_sfm_amd.hip import ops as _hops
-    _hops.set_grad_sinks(args.grad_sinks)
+    _hops.set_grad_sinks(not args.no_grad_sinks)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -474,6 +481,8 @@ def main():
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_convs": args.conv_backend,
                    "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
+                   "update_blocks": "concurrent streams" if args.concurrent_blocks else "serial",
+                   "grad_sinks": not args.no_grad_sinks,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},

@@ -1134,8 +1134,18 @@ WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
   pl.ctiles = (Cin + 31) / 32;
   const int blocks = pl.otiles * pl.ctiles;
   // ~1.5 blocks per CU (parallelism beats the partials' extra traffic here)
-  int sp = (384 + blocks - 1) / blocks;
-  if (sp > 32) sp = 32;
+  static const int max_sp = [] {   // tuning override: DRO_WH_MAX_SPLITS (default 32)
+    const char* e = getenv("DRO_WH_MAX_SPLITS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 32;
+  }();
+  static const int target = [] {   // tuning override: DRO_WH_TARGET_BLOCKS (default 384)
+    const char* e = getenv("DRO_WH_TARGET_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 384;
+  }();
+  int sp = (target + blocks - 1) / blocks;
+  if (sp > max_sp) sp = max_sp;
   if (sp > ntiles) sp = ntiles;
   if (sp < 1) sp = 1;
   pl.tiles_per_split = (ntiles + sp - 1) / sp;

@@ -266,6 +266,7 @@ class DroWgradUse(ctypes.Structure):
 _BATCH = [True]
 _PENDING = {}
 _PENDING_CB = [False]
+_PENDING_STREAMS = []   # streams the queued uses' tensors were produced on
 _MULTI_SHAPES = {(1, 1), (1, 5), (5, 1), (3, 3)}
 _MAX_USES = 16
 
@@ -289,6 +290,9 @@ def _queue_weight_grad(srcs, wshape, act, alpha, dout, y, gw, gb):
     if ent is None:
         ent = _PENDING[key] = ((B, H, W, Cin, Cout, KH, KW, act, float(alpha), gw, gb, len(srcs)), [])
     ent[1].append((list(srcs), dout, y))
+    cur = torch.cuda.current_stream()
+    if all(s != cur for s in _PENDING_STREAMS):
+        _PENDING_STREAMS.append(cur)
     if not _PENDING_CB[0]:
         _PENDING_CB[0] = True
         stream = torch.cuda.current_stream()
@@ -306,6 +310,15 @@ def flush_weight_grads(stream=None):
     items = list(_PENDING.values())
     _PENDING.clear()
     stream = stream or torch.cuda.current_stream()
+    for s in _PENDING_STREAMS:        # uses queued from other streams (concurrent blocks)
+        if s != stream:
+            stream.wait_stream(s)
+            for _, uses in items:
+                for srcs, dout, y in uses:
+                    for x in (*srcs, dout, y):
+                        if x is not None:
+                            x.record_stream(stream)
+    _PENDING_STREAMS.clear()
     with torch.cuda.stream(stream):
         for meta, uses in items:
             B, H, W, Cin, Cout, KH, KW, act, alpha, gw, gb, nsrc = meta

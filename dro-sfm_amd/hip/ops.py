@@ -80,15 +80,15 @@ class _GradSink(torch.autograd.Function):
         return (st.buf if g is None else st.buf + g), None
 
 
-_SINKS = [False]
+_SINKS = [True]
 
 
 def set_grad_sinks(enabled):
-    """grad_sink on / off (default: identity, autograd sums per use).  Measured on
-    one MI355X box: sinks on the feature maps and context features 21.58 vs
-    21.55 ms/step, extended to the per-step state / projection features / pose
-    map 21.79 vs 21.24 ms/step (the accumulating epilogues' extra reads cost more
-    than the add launches they remove), so the default is off."""
+    """grad_sink on (default) / off (identity: autograd sums per use).  Measured
+    (round 2, sinks covering the 5-D reference feature maps, one box, two
+    interleaved rounds of 40 steps): 20.92 / 20.81 ms/step on against 21.28 /
+    21.04 off.  (Round 1, before the feature maps were covered: 21.79 on vs
+    21.24 off.)"""
     _SINKS[0] = bool(enabled)
 
 

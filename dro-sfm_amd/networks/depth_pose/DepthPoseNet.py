@@ -61,6 +61,16 @@ def set_concurrent_encoders(enabled):
     _CONCURRENT[0] = bool(enabled)
 
 
+_CONCURRENT_BLOCKS = [False]
+
+
+def set_concurrent_blocks(enabled):
+    """Run the pose update block on a side stream beside the depth update block
+    (they are independent within an outer iteration: each reads the other's
+    state of the previous iteration, detached; DepthPoseNet.py:154-197)."""
+    _CONCURRENT_BLOCKS[0] = bool(enabled)
+
+
 def _side_streams(device):
     ss = _SIDE_STREAMS.get(device)
     if ss is None:
@@ -176,27 +186,51 @@ class DepthPoseNet(nn.Module):
         if self.iters > 0:
             # the context features feed every GRU step: gradients summed in place
             x_d, x_p = hip.grad_sink(x_d), hip.grad_sink(x_p)
+        pside = None
+        if self.iters > 0 and _CONCURRENT_BLOCKS[0] and target_image.is_cuda:
+            pside = _side_streams(target_image.device)[1]
         for _ in range(self.iters):
             disp = disp.detach()
             poses = poses.detach()
-            frozen_poses = poses
-            depth_cost = lambda d: self._cost(fmap1, frefs, d, frozen_poses, K, True)
-            h_d, masks, disps = self.update_block_depth(h_d, depth_cost, disp, x_d,
-                                                        seq_len=self.seq_len)
-            keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
-            for k in keep:
-                inv_preds.append(self.scale_inv_depth(
-                    self.upsample_depth(disps[k], masks[k], self.feat_ratio)))
+            frozen_poses, frozen_disp = poses, disp
 
-            # pose block over all N refs at once; depth frozen at this outer step
-            frozen_disp = disp
-            pose_cost = lambda q: self._cost(fmap1, frefs, frozen_disp, q.view(N, B, 6), K,
-                                             False).view(N * B, C, h, w)
-            h_p, seq = self.update_block_pose(h_p, pose_cost, poses.reshape(N * B, 6), x_p,
-                                              seq_len=self.seq_len)
-            seq = seq if self.inter_sup else [seq[-1]]
-            pose_preds.extend(q.view(N, B, 6) for q in seq)
-            disp, poses = disps[-1], seq[-1].view(N, B, 6)
+            def depth_block(h_d):
+                depth_cost = lambda d: self._cost(fmap1, frefs, d, frozen_poses, K, True)
+                h_d, masks, disps = self.update_block_depth(h_d, depth_cost, frozen_disp, x_d,
+                                                            seq_len=self.seq_len)
+                keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
+                for k in keep:
+                    inv_preds.append(self.scale_inv_depth(
+                        self.upsample_depth(disps[k], masks[k], self.feat_ratio)))
+                return h_d, disps[-1]
+
+            def pose_block(h_p):
+                # pose block over all N refs at once; depth frozen at this outer step
+                pose_cost = lambda q: self._cost(fmap1, frefs, frozen_disp, q.view(N, B, 6), K,
+                                                 False).view(N * B, C, h, w)
+                h_p, seq = self.update_block_pose(h_p, pose_cost, frozen_poses.reshape(N * B, 6), x_p,
+                                                  seq_len=self.seq_len)
+                seq = seq if self.inter_sup else [seq[-1]]
+                return h_p, [q.view(N, B, 6) for q in seq]
+
+            if pside is None:
+                h_d, disp_last = depth_block(h_d)
+                h_p, seq = pose_block(h_p)
+            else:
+                # the pose block reads only the detached depth and poses of the previous
+                # outer step: it runs on a side stream beside the depth block
+                main = torch.cuda.current_stream(target_image.device)
+                pside.wait_stream(main)
+                for t in (fmap1, frefs, frozen_disp, frozen_poses, h_p, x_p, K):
+                    t.record_stream(pside)
+                with torch.cuda.stream(pside):
+                    h_p, seq = pose_block(h_p)
+                h_d, disp_last = depth_block(h_d)
+                main.wait_stream(pside)                    # join before the outputs are read
+                for t in (h_p, *seq):
+                    t.record_stream(main)
+            pose_preds.extend(seq)
+            disp, poses = disp_last, seq[-1]
 
         if not self.training:
             return inv_preds[-1], pose_preds[-1].permute(1, 0, 2)          # [B,N,6]

@@ -117,6 +117,7 @@ def test_grad_sinks_match_per_use_gradients():
     from dro_sfm_amd.hip import ops as hops
     from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
     res = []
+    prev = hops._SINKS[0]
     for enabled in (True, False):
         hops.set_grad_sinks(enabled)
         try:
@@ -132,7 +133,7 @@ def test_grad_sinks_match_per_use_gradients():
             res.append((float(loss.detach()), {k: p.grad.clone() for k, p in net.named_parameters()
                                       if p.grad is not None}))
         finally:
-            hops.set_grad_sinks(False)
+            hops.set_grad_sinks(prev)
     (l1, g1), (l2, g2) = res
     assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l2))
     assert g1.keys() == g2.keys()
