@@ -56,4 +56,4 @@ int launch_zero(float* p, size_t n, hipStream_t s) {
 
 extern "C" const char* dro_last_error(void) { return dro::g_last_error; }
 
-extern "C" int dro_abi_version(void) { return 3; }
+extern "C" int dro_abi_version(void) { return 4; }

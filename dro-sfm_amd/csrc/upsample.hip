@@ -18,9 +18,11 @@ namespace dro {
 
 constexpr int kMaxR = 8;
 
+// out = add + mul * upsample (the disp_to_depth scaling of DepthPoseNet.scale_inv_depth,
+// DepthPoseNet.py:128/181, fused: a multiply then an add, as the reference)
 __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restrict__ inv,
                                                             const float* __restrict__ mask, int B,
-                                                            int h, int w, int r,
+                                                            int h, int w, int r, float add, float mul,
                                                             float* __restrict__ out) {
   const int hw = h * w;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -51,13 +53,13 @@ __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restr
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc += (m[k] / s) * d[k];
-    ob[c] = acc;
+    ob[c] = __fadd_rn(add, __fmul_rn(mul, acc));
   }
 }
 
 __global__ __launch_bounds__(256) void convex_up_bwd_kernel(
     const float* __restrict__ inv, const float* __restrict__ mask, const float* __restrict__ gout,
-    int B, int h, int w, int r, float* __restrict__ ginv, float* __restrict__ gmask) {
+    int B, int h, int w, int r, float mul, float* __restrict__ ginv, float* __restrict__ gmask) {
   const int hw = h * w;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= B * r * hw) return;
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(256) void convex_up_bwd_kernel(
   float* gmb = gmask + (size_t)b * 9 * r * r * hw + pix;
   const float* gb = gout + ((size_t)b * h * r + (size_t)y * r + a) * (w * r) + (size_t)x * r;
   for (int c = 0; c < r; ++c) {
-    const float G = gb[c];
+    const float G = __fmul_rn(gb[c], mul);
     float m[9], mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -200,7 +202,7 @@ static int up_check(const float* inv, const float* mask, int B, int h, int w, in
 }
 
 extern "C" int dro_convex_upsample_forward(const float* inv, const float* mask, int B, int h, int w,
-                                           int ratio, float* out, void* stream) {
+                                           int ratio, float add, float mul, float* out, void* stream) {
   int st = up_check(inv, mask, B, h, w, ratio);
   if (st) return st;
   if (!out) {
@@ -209,13 +211,13 @@ extern "C" int dro_convex_upsample_forward(const float* inv, const float* mask, 
   }
   const int total = B * ratio * h * w;
   hipLaunchKernelGGL(convex_up_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, inv, mask, B, h, w, ratio, out);
+                     (hipStream_t)stream, inv, mask, B, h, w, ratio, add, mul, out);
   return launch_status("convex_up_fwd_kernel launch failed");
 }
 
 extern "C" int dro_convex_upsample_backward(const float* inv, const float* mask,
                                             const float* grad_out, int B, int h, int w, int ratio,
-                                            float* grad_inv, float* grad_mask, void* stream) {
+                                            float mul, float* grad_inv, float* grad_mask, void* stream) {
   int st = up_check(inv, mask, B, h, w, ratio);
   if (st) return st;
   if (!grad_out || !grad_mask) {
@@ -226,7 +228,7 @@ extern "C" int dro_convex_upsample_backward(const float* inv, const float* mask,
   if (grad_inv && (st = launch_zero(grad_inv, (size_t)B * h * w, s))) return st;
   const int total = B * ratio * h * w;
   hipLaunchKernelGGL(convex_up_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, inv, mask,
-                     grad_out, B, h, w, ratio, grad_inv, grad_mask);
+                     grad_out, B, h, w, ratio, mul, grad_inv, grad_mask);
   return launch_status("convex_up_bwd_kernel launch failed");
 }
 

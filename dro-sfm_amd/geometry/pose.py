@@ -130,3 +130,41 @@ class Pose:
         if isinstance(other, torch.Tensor) and other.dim() in (3, 4) and other.shape[1] == 3:
             return self.transform_points(other)
         raise ValueError(f"Unknown operand for Pose @: {type(other)}")
+
+
+class PoseGrid(list):
+    """The reference's N x n_pred list of Pose objects (SfmModelMF.py:174-181),
+    remembering the [B,N,n_pred,6] tensor they were sliced from: the fused
+    losses read it as one [N,n_pred,B,6] tensor (one permuted copy forward and
+    backward) instead of re-stacking N*n_pred slices (whose backward is a
+    zero-fill + copy + add per slice)."""
+
+    def __init__(self, rows, vec, mode):
+        super().__init__(rows)
+        self.vec, self.mode = vec, mode
+
+    def kernel_poses(self):
+        """[N, n_pred, B, 6] euler vectors, or None when the grid no longer mirrors
+        the source tensor (entries replaced, or a non-euler mode)."""
+        if self.mode != "euler" or self.vec is None:
+            return None
+        N, n = self.vec.shape[1], self.vec.shape[2]
+        if len(self) != N or any(len(row) != n for row in self):
+            return None
+        return self.vec.permute(1, 2, 0, 3).contiguous()
+
+
+def kernel_pose_tensor(poses, n):
+    """[N, n, B, 6|3x4] kernel poses of an N x n list of Pose objects."""
+    fast = poses.kernel_poses() if isinstance(poses, PoseGrid) else None
+    if fast is not None and fast.shape[1] == n:
+        # every entry must still be the untouched slice [:, j, i] of the source tensor
+        src = poses.vec
+        ok = all(isinstance(poses[j][i], Pose) and poses[j][i]._mat is None and poses[j][i].vec is not None
+                 and poses[j][i].vec.data_ptr() == src[:, j, i].data_ptr()
+                 and poses[j][i].vec.stride() == src[:, j, i].stride()
+                 for j in range(len(poses)) for i in range(n))
+        if ok:
+            return fast
+    return torch.stack([torch.stack([poses[j][i].kernel_pose() for i in range(n)], 0)
+                        for j in range(len(poses))], 0)

@@ -48,8 +48,8 @@ def load():
     _sig(lib.dro_supervised_workspace_bytes, I, I, I, I, I, restype=Z)
     _sig(lib.dro_supervised_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, S)
     _sig(lib.dro_supervised_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, P, P, S)
-    _sig(lib.dro_convex_upsample_forward, P, P, I, I, I, I, P, S)
-    _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, P, P, S)
+    _sig(lib.dro_convex_upsample_forward, P, P, I, I, I, I, F, F, P, S)
+    _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, F, P, P, S)
     _sig(lib.dro_bilinear_upsample2x_forward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_bilinear_upsample2x_backward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_batchnorm_workspace_bytes, I, I, I, restype=Z)

@@ -4,6 +4,8 @@ Each Function checks dtype/device/shape up front (RuntimeError, as the
 reference's ATen ops would raise), allocates outputs through the caching
 allocator, and launches on the current stream.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -363,7 +365,7 @@ def supervised_loss(gt_inv, inv_depths, pose, gt_pose, K, ref_K=None, *, min_dep
 # ------------------------------------------------------------------------- convex upsample
 class _ConvexUpsample(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, inv, mask, ratio):
+    def forward(ctx, inv, mask, ratio, add, mul):
         lib = _lib.load()
         require_device(inv, mask, what="convex_upsample")
         B, _, h, w = inv.shape
@@ -371,10 +373,11 @@ class _ConvexUpsample(torch.autograd.Function):
             raise RuntimeError("convex_upsample: mask must be [B, 9*r*r, h, w]")
         inv, mask = inv.contiguous(), mask.contiguous()
         out = torch.empty(B, 1, h * ratio, w * ratio, device=inv.device, dtype=torch.float32)
-        check(lib.dro_convex_upsample_forward(ptr(inv), ptr(mask), B, h, w, ratio, ptr(out),
-                                              stream_of(inv)), "dro_convex_upsample_forward")
+        check(lib.dro_convex_upsample_forward(ptr(inv), ptr(mask), B, h, w, ratio, ctypes.c_float(add),
+                                              ctypes.c_float(mul), ptr(out), stream_of(inv)),
+              "dro_convex_upsample_forward")
         ctx.save_for_backward(inv, mask)
-        ctx.ratio = ratio
+        ctx.ratio, ctx.mul = ratio, mul
         return out
 
     @staticmethod
@@ -385,14 +388,16 @@ class _ConvexUpsample(torch.autograd.Function):
         g_inv = torch.empty_like(inv) if ctx.needs_input_grad[0] else None
         g_mask = torch.empty_like(mask)
         check(lib.dro_convex_upsample_backward(ptr(inv), ptr(mask), ptr(gout.contiguous()), B, h, w,
-                                               ctx.ratio, ptr(g_inv), ptr(g_mask), stream_of(inv)),
-              "dro_convex_upsample_backward")
-        return g_inv, g_mask if ctx.needs_input_grad[1] else None, None
+                                               ctx.ratio, ctypes.c_float(ctx.mul), ptr(g_inv), ptr(g_mask),
+                                               stream_of(inv)), "dro_convex_upsample_backward")
+        return g_inv, g_mask if ctx.needs_input_grad[1] else None, None, None, None
 
 
-def convex_upsample(inv, mask, ratio=8):
-    """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74): [B,1,h,w] -> [B,1,rh,rw]."""
-    return _ConvexUpsample.apply(inv, mask, int(ratio))
+def convex_upsample(inv, mask, ratio=8, affine=None):
+    """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74): [B,1,h,w] -> [B,1,rh,rw];
+    affine=(add, mul) folds `add + mul * out` (scale_inv_depth) into the kernel."""
+    add, mul = affine if affine is not None else (0.0, 1.0)
+    return _ConvexUpsample.apply(inv, mask, int(ratio), float(add), float(mul))
 
 
 # ------------------------------------------------------------------ bilinear 2x upsample

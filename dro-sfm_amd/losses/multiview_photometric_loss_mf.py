@@ -13,6 +13,7 @@ Anything else raises NotImplementedError rather than running a slow path.
 import torch
 
 from ..hip import photometric_loss
+from ..geometry.pose import kernel_pose_tensor
 from .loss_base import LossBase, ProgressiveScaling
 
 
@@ -60,8 +61,7 @@ class MultiViewPhotometricDecayLoss(LossBase):
         n, N = self.n, len(context)
         ctx = torch.stack(list(context), 0)                                   # [N,B,3,H,W]
         invs = torch.stack(list(inv_depths), 0)                               # [n,B,1,H,W]
-        kp = [[poses[j][i].kernel_pose() for i in range(n)] for j in range(N)]
-        pose_t = torch.stack([torch.stack(row, 0) for row in kp], 0)          # [N,n,B,6|3x4]
+        pose_t = kernel_pose_tensor(poses, n)                                 # [N,n,B,6|3x4]
         loss, metrics, sel = photometric_loss(
             image, ctx, invs, pose_t, K.float(), ref_K.float(), ssim_w=self.ssim_loss_weight,
             C1=self.C1, C2=self.C2, smooth_w=self.smooth_loss_weight, automask=self.automask_loss,

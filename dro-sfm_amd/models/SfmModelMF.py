@@ -4,7 +4,7 @@ import random
 import torch
 import torch.nn as nn
 
-from ..geometry.pose import Pose
+from ..geometry.pose import Pose, PoseGrid
 
 
 def flip_lr(image):
@@ -76,6 +76,8 @@ class SfmModelMF(nn.Module):
         elif pose_vec.shape[-2:] == (4, 4):
             poses = [Pose(pose_vec[:, j]) for j in range(pose_vec.shape[1])]
         else:                                                   # train: [B,N,n_pred,6]
-            poses = [[Pose.from_vec(pose_vec[:, j, i], self.rotation_mode)
-                      for i in range(pose_vec.shape[2])] for j in range(pose_vec.shape[1])]
+            poses = PoseGrid([[Pose.from_vec(pose_vec[:, j, i], self.rotation_mode)
+                               for i in range(pose_vec.shape[2])] for j in range(pose_vec.shape[1])],
+                             pose_vec, self.rotation_mode)
         return {"inv_depths": inv_depths, "poses": poses}
+

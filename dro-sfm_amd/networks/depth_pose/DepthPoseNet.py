@@ -120,6 +120,14 @@ class DepthPoseNet(nn.Module):
         """Convex upsampling (DepthPoseNet.py:63-74), one HIP launch."""
         return hip.convex_upsample(depth, mask, ratio)
 
+    def upsample_scaled(self, depth, mask, ratio=8):
+        """scale_inv_depth(upsample_depth(...)) in one launch (DepthPoseNet.py:126-128,
+        :180-181): the disp_to_depth affine is the upsample kernel's epilogue."""
+        if not self.out_normalize:
+            return hip.convex_upsample(depth, mask, ratio)
+        lo, hi = 1.0 / self.max_depth, 1.0 / self.min_depth
+        return hip.convex_upsample(depth, mask, ratio, affine=(lo, hi - lo))
+
     def _cost(self, fmap1, frefs, disp, poses, K, reduce_mean):
         return hip.warp_cost(fmap1, frefs, disp, poses, K, depth_mode=self.depth_mode,
                              min_depth=self.min_depth, max_depth=self.max_depth,
@@ -172,8 +180,7 @@ class DepthPoseNet(nn.Module):
         poses = self.pose_head(pair).view(N, B, 6)
 
         disp = self.depth_head(fmap1, act_fn=torch.sigmoid)
-        inv_preds = [self.scale_inv_depth(self.upsample_depth(disp, self.upmask_net(fmap1),
-                                                              self.feat_ratio))]
+        inv_preds = [self.upsample_scaled(disp, self.upmask_net(fmap1), self.feat_ratio)]
         pose_preds = [poses]
 
         if side:                                          # join: the update blocks read h/x
@@ -200,8 +207,7 @@ class DepthPoseNet(nn.Module):
                                                             seq_len=self.seq_len)
                 keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
                 for k in keep:
-                    inv_preds.append(self.scale_inv_depth(
-                        self.upsample_depth(disps[k], masks[k], self.feat_ratio)))
+                    inv_preds.append(self.upsample_scaled(disps[k], masks[k], self.feat_ratio))
                 return h_d, disps[-1]
 
             def pose_block(h_p):

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* ------------------------------------------------------------------------
  * Inverse warp + feature cost.
@@ -157,13 +157,17 @@ int dro_supervised_backward(const float* gt_inv, const float* inv_depths, const 
                             void* stream);
 
 /* ------------------------------------------------------------------------
- * Convex 8x upsampling: DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74).
+ * Convex 8x upsampling: DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74),
+ * followed by out = add + mul * up (DepthPoseNet.scale_inv_depth, the
+ * disp_to_depth scaling of every prediction, DepthPoseNet.py:128/181; add = 0,
+ * mul = 1 for the plain upsample), computed as a multiply then an add.
  *   inv [B,1,h,w]; mask [B,9*r*r,h,w] -> out [B,1,h*r,w*r]
+ * The backward takes the same `mul` (d out / d up).
  * ---------------------------------------------------------------------- */
 int dro_convex_upsample_forward(const float* inv, const float* mask, int B, int h, int w,
-                                int ratio, float* out, void* stream);
+                                int ratio, float add, float mul, float* out, void* stream);
 int dro_convex_upsample_backward(const float* inv, const float* mask, const float* grad_out,
-                                 int B, int h, int w, int ratio,
+                                 int B, int h, int w, int ratio, float mul,
                                  float* grad_inv, float* grad_mask, void* stream);
 
 /* Bilinear 2x upsampling, align_corners=False (F.interpolate(scale_factor=2,

@@ -34,7 +34,7 @@ def test_header_matches_exports(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dro_abi_version() == 3
+    assert lib.dro_abi_version() == 4
 
 
 def test_null_arguments_rejected(lib):
@@ -46,7 +46,7 @@ def test_null_arguments_rejected(lib):
     st = lib.dro_photometric_forward(NULL, NULL, NULL, NULL, NULL, NULL, 0, 1, 1, 1, 8, 8, 0.85,
                                      1e-4, 9e-4, 1e-3, 1, 1, NULL, NULL, NULL)
     assert st == -1
-    st = lib.dro_convex_upsample_forward(NULL, NULL, 1, 2, 2, 8, NULL, NULL)
+    st = lib.dro_convex_upsample_forward(NULL, NULL, 1, 2, 2, 8, 0.0, 1.0, NULL, NULL)
     assert st == -1
 
 
@@ -62,7 +62,7 @@ def test_bad_sizes_and_modes_rejected(lib):
     # automask needs the min reduction
     assert lib.dro_photometric_forward(p, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.85, 1e-4, 9e-4, 1e-3,
                                        1, 0, p, p, None) == -3
-    assert lib.dro_convex_upsample_forward(p, p, 1, 2, 2, 9, p, None) == -2
+    assert lib.dro_convex_upsample_forward(p, p, 1, 2, 2, 9, 0.0, 1.0, p, None) == -2
 
 
 def test_workspace_sizes(lib):

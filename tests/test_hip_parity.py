@@ -266,6 +266,26 @@ def test_convex_upsample_kitti_size(hip):
     assert rel(up, ref) < TOL and rel(ig.grad, ic.grad) < TOL and rel(mg.grad, mc.grad) < TOL
 
 
+def test_convex_upsample_fused_scale(hip):
+    """affine=(lo, hi - lo): the disp_to_depth scaling of DepthPoseNet.scale_inv_depth
+    (networks/layers/resnet/layers.py:11-20) in the upsample epilogue equals the
+    upsample followed by PyTorch's multiply and add to f32 rounding (1e-6
+    relative), forward and backward."""
+    g = torch.Generator().manual_seed(4)
+    inv, mask = torch.rand(2, 1, 24, 80, generator=g), torch.randn(2, 576, 24, 80, generator=g)
+    lo, hi = 1.0 / 80.0, 1.0 / 0.5
+    G = torch.randn(2, 1, 192, 640, generator=g).to(DEV)
+    a, am = inv.to(DEV).requires_grad_(True), mask.to(DEV).requires_grad_(True)
+    ref = lo + (hi - lo) * hip.convex_upsample(a, am, 8)
+    (ref * G).sum().backward()
+    b, bm = inv.to(DEV).requires_grad_(True), mask.to(DEV).requires_grad_(True)
+    out = hip.convex_upsample(b, bm, 8, affine=(lo, hi - lo))
+    (out * G).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-6
+    assert rel(b.grad, a.grad) < 1e-6 and rel(bm.grad, am.grad) < 1e-6
+
+
 # ------------------------------------------------------------------ network level
 def _load_net(tag, version, mind, maxd):
     from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
