@@ -398,6 +398,8 @@ def main():
     ap.add_argument("--miopen-find", choices=("on", "off"), default="off",
                     help="torch.backends.cudnn.benchmark (MIOpen Find for the library convs; the "
                          "reference sets it, horovod_trainer.py:34)")
+    ap.add_argument("--split-engine", choices=("off", "all", "3x3fwd"), default="off",
+                    help="split-bf16 MFMA conv engine (csrc/xconv.hip) for the halo convs (A/B)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
@@ -415,6 +417,7 @@ def main():
     import dro_sfm_amd.hip.conv as _hconv
     _hconv.set_direct_weight_grads(not args.no_direct_wgrad)
     _hconv.set_weight_grad_stream(args.wgrad_side_stream)
+    _hconv.set_split_engine(args.split_engine != "off", args.split_engine)
     from dro_sfm_amd.networks.optim import update as _update
     _update.set_conv_backend(args.conv_backend)
     from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
@@ -483,6 +486,7 @@ def main():
                    "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
                    "update_blocks": "concurrent streams" if args.concurrent_blocks else "serial",
                    "grad_sinks": not args.no_grad_sinks,
+                   "split_engine": args.split_engine,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},

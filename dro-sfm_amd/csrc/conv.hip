@@ -1796,8 +1796,18 @@ static WhPlan plan_wgrad_multi(int Cin, int Cout, int KH, int KW, int nuse, int 
   if (!pl.ok) return pl;
   const int ntiles = nuse * B * pl.tiles_img;
   const int blocks = pl.otiles * pl.ctiles;
-  int sp = (512 + blocks - 1) / blocks;
-  if (sp > 64) sp = 64;
+  static const int target = [] {   // tuning override: DRO_WHM_TARGET_BLOCKS (default 512)
+    const char* e = getenv("DRO_WHM_TARGET_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  static const int max_sp = [] {   // tuning override: DRO_WHM_MAX_SPLITS (default 64)
+    const char* e = getenv("DRO_WHM_MAX_SPLITS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 64;
+  }();
+  int sp = (target + blocks - 1) / blocks;
+  if (sp > max_sp) sp = max_sp;
   if (sp > ntiles / 4) sp = ntiles / 4;
   if (sp < 1) sp = 1;
   pl.tiles_per_split = (ntiles + sp - 1) / sp;

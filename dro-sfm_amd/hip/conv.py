@@ -108,19 +108,24 @@ def weight_grad_scope():
 
 _XCONV = [False]   # measured: not faster than the f32 engine at the step's shapes
 _XSHAPES = {(1, 5), (5, 1), (3, 3), (1, 1)}
+_XPOLICY = ["all"]  # "all": every xconv shape, fwd + data grad; "3x3fwd": 3x3 forwards only
 _SPLITS = {}       # (data_ptr, shape, device) -> [generation, fwd split, bwd split]
 
 
-def set_split_engine(enabled):
+def set_split_engine(enabled, policy="all"):
     """Split-bf16 MFMA engine for the halo convs (True) or the f32-MFMA engine
-    (False, default: the faster of the two at the update-block shapes)."""
+    (False, default: the faster of the two at the update-block shapes).
+    policy "3x3fwd" limits it to the forward of the 3x3 convs."""
     _XCONV[0] = bool(enabled)
+    _XPOLICY[0] = policy
 
 
 def _wsplit(weight):
     """(fwd, bwd) split-bf16 copies of a contiguous weight for the xconv engine,
     or (None, None) when the f32 engine runs this conv."""
     if not _XCONV[0] or tuple(weight.shape[2:]) not in _XSHAPES:
+        return None, None
+    if _XPOLICY[0] == "3x3fwd" and tuple(weight.shape[2:]) != (3, 3):
         return None, None
     lib = _lib.load()
     Cout, Cin, KH, KW = weight.shape
@@ -138,6 +143,8 @@ def _wsplit(weight):
         check(lib.dro_weight_split(ptr(weight), Cout, Cin, KH, KW, ptr(ent[1]), ptr(ent[2]),
                                    stream_of(weight)), "dro_weight_split")
         ent[0] = _GEN[0]
+    if _XPOLICY[0] == "3x3fwd":
+        return ent[1], None
     return ent[1], ent[2]
 
 
