@@ -301,7 +301,7 @@ def roofline_conv(device, iters=50, traffic_file=None):
 
     def launch():
         _lib.check(lib.dro_convgru_gates_forward(sl, 4, _lib.ptr(wzr), _lib.ptr(bzr), B, Hf, Wf, hd, KH, KW,
-                                                 _lib.ptr(zr), _lib.ptr(rh), _lib.ptr(ws), nws, st),
+                                                 _lib.ptr(zr), _lib.ptr(rh), None, _lib.ptr(ws), nws, st),
                    "dro_convgru_gates_forward")
     for _ in range(5):
         launch()

@@ -9,8 +9,9 @@
 // mean) reduction over the 2N maps with 0.85^(n-i-1) decay (:231-269), and the
 // smoothness term (:273-299, utils/depth.py:147-199).  The reference runs
 // ~25 ATen kernels per (i, j) pair forward (18 pairs for KITTI it8) plus the
-// automask pass per (i, j); here the whole loss is 3 launches forward and 3
-// backward.
+// automask pass per (i, j); here the whole loss is 3 launches forward (the
+// automask maps once per (ref, batch), the tile kernel, a one-block finalize)
+// and 2 backward.
 //
 // Tiling: a workgroup owns an 8x64 output tile of one (prediction, batch).
 // The warped reference is synthesised once per tile into LDS with a 1-pixel
@@ -51,6 +52,8 @@ struct PhotoArgs {
   int tiles_x, tiles_y;
   // workspace views
   unsigned char* sel;
+  float* am;        // [N,B,HW] automask (unwarped) photometric maps, once per (ref, batch)
+  float* part_inv;  // [n,B,tiles] sums of the inverse depth (its mean normalises smoothness)
   float* mean;      // [n,B]
   float* U;         // [n,B,2]
   float* part_ph;   // [n,B,tiles]
@@ -152,16 +155,36 @@ __device__ __forceinline__ void cams_full(const PhotoArgs& a, int b, float ki[9]
   scaled_K(a.ref_K + 9 * b, 1.f, false, kr);
 }
 
-// ------------------------------------------------------------------ per-(i,b) mean of inv depth
-__global__ __launch_bounds__(1024) void photo_mean_kernel(PhotoArgs a) {
-  __shared__ float scratch[16];
-  const size_t HW = (size_t)a.H * a.W;
-  const float* src = a.inv + (size_t)blockIdx.x * HW;
-  float s = 0.f;
-  for (size_t k = threadIdx.x; k < HW; k += blockDim.x) s += src[k];
-  float v[1] = {s};
-  block_sum<1>(v, scratch);
-  if (threadIdx.x == 0) a.mean[blockIdx.x] = v[0] / (float)HW;
+// ------------------------------------------------------------------ automask maps
+// The unwarped-reference photometric map (multiview_photometric_loss_mf.py:346-351)
+// depends on (ref j, batch b) only; the reference recomputes it for every
+// prediction, the forward kernel reads it from here (same arithmetic, same values).
+__global__ __launch_bounds__(kThreads) void photo_automask_kernel(PhotoArgs a) {
+  constexpr int PL = H1 * W1;
+  __shared__ float tgt[3 * PL];
+  __shared__ float raw[3 * PL];
+  const int jb = blockIdx.z, j = jb / a.B, b = jb % a.B;
+  const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+  const int H = a.H, W = a.W;
+  const size_t HW = (size_t)H * W;
+  const float* img = a.image + (size_t)b * 3 * HW;
+  const float* ctx = a.context + ((size_t)j * a.B + b) * 3 * HW;
+  for (int k = threadIdx.x; k < PL; k += kThreads) {
+    const int gy = reflect_idx(y0 + k / W1 - 1, H), gx = reflect_idx(x0 + k % W1 - 1, W);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      tgt[c * PL + k] = img[c * HW + (size_t)gy * W + gx];
+      raw[c * PL + k] = ctx[c * HW + (size_t)gy * W + gx];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kPxPerThread; ++r) {
+    const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
+    if (y0 + ly >= H || x0 + lx >= W) continue;
+    const int o = (ly + 1) * W1 + (lx + 1);
+    a.am[(size_t)jb * HW + (size_t)(y0 + ly) * W + x0 + lx] = photo_value(a, raw, tgt, o, W1, PL);
+  }
 }
 
 // ------------------------------------------------------------------ forward tile kernel
@@ -169,8 +192,7 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
   constexpr int PL = H1 * W1;
   __shared__ float tgt[3 * PL];
   __shared__ float est[3 * PL];
-  __shared__ float raw[3 * PL];
-  __shared__ float scratch[3 * (kThreads / kWave)];
+  __shared__ float scratch[4 * (kThreads / kWave)];
 
   const int ib = blockIdx.z, i = ib / a.B, b = ib % a.B;
   const int tile = blockIdx.y * a.tiles_x + blockIdx.x;
@@ -209,10 +231,6 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
       synth(a, ctx, ki, kr, R, t, gx, gy, invp[(size_t)gy * W + gx], o, nullptr, nullptr);
 #pragma unroll
       for (int c = 0; c < 3; ++c) est[c * PL + k] = o[c];
-      if (a.automask) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) raw[c * PL + k] = ctx[c * HW + (size_t)gy * W + gx];
-      }
     }
     __syncthreads();
 #pragma unroll
@@ -232,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
         accm[r] += vw;
       }
       if (a.automask) {
-        const float vu = photo_value(a, raw, tgt, o, W1, PL);
+        const float vu = a.am[((size_t)j * a.B + b) * HW + (size_t)(y0 + ly) * W + x0 + lx];
         if (a.reduce_min) {
           if (vu < best[r]) {
             best[r] = vu;
@@ -245,9 +263,10 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
     }
   }
 
-  // selection map + tile partial of the reduced photometric map
-  float v3[3] = {0.f, 0.f, 0.f};
-  const float mean = fmaxf(a.mean[ib], 1e-6f);
+  // selection map + tile partials of the reduced photometric map, the
+  // smoothness sums (unnormalised: the mean of the inverse depth is a common
+  // positive factor, divided out in photo_finalize_kernel) and the inverse depth
+  float v3[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < kPxPerThread; ++r) {
     const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
@@ -263,54 +282,73 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
     // smoothness (utils/depth.py:166-199): normalised inv-depth gradients
     // weighted by exp(-mean_c |image gradient|)
     const int o = (ly + 1) * W1 + (lx + 1);
-    const float d0 = invp[gp] / mean;
+    const float d0 = invp[gp];
+    v3[3] += d0;
     if (gx < W - 1) {
-      const float g = d0 - invp[gp + 1] / mean;
+      const float g = d0 - invp[gp + 1];
       const float gi = (fabsf(tgt[o] - tgt[o + 1]) + fabsf(tgt[PL + o] - tgt[PL + o + 1]) +
                         fabsf(tgt[2 * PL + o] - tgt[2 * PL + o + 1])) / 3.f;
       v3[1] += fabsf(g * expf(-gi));
     }
     if (gy < H - 1) {
-      const float g = d0 - invp[gp + W] / mean;
+      const float g = d0 - invp[gp + W];
       const float gi = (fabsf(tgt[o] - tgt[o + W1]) + fabsf(tgt[PL + o] - tgt[PL + o + W1]) +
                         fabsf(tgt[2 * PL + o] - tgt[2 * PL + o + W1])) / 3.f;
       v3[2] += fabsf(g * expf(-gi));
     }
   }
   (void)M;
-  block_sum<3>(v3, scratch);
+  block_sum<4>(v3, scratch);
   if (threadIdx.x == 0) {
     const int tiles = a.tiles_x * a.tiles_y;
     a.part_ph[(size_t)ib * tiles + tile] = v3[0];
     a.part_sm[((size_t)ib * tiles + tile) * 2 + 0] = v3[1];
     a.part_sm[((size_t)ib * tiles + tile) * 2 + 1] = v3[2];
+    a.part_inv[(size_t)ib * tiles + tile] = v3[3];
   }
 }
 
 // ------------------------------------------------------------------ forward finalize (1 block)
-__global__ __launch_bounds__(256) void photo_finalize_kernel(PhotoArgs a, float* __restrict__ out) {
+// Per (i,b) one wave sums the tile partials (strided lanes, then a fixed
+// shuffle tree: deterministic); the inverse-depth mean (inv_depths_normalize,
+// utils/depth.py:147-163: clamp 1e-6) normalises the smoothness sums.
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(1024) void photo_finalize_kernel(PhotoArgs a, float* __restrict__ out) {
   __shared__ double ph[64], sx[64], sy[64];
   const int tiles = a.tiles_x * a.tiles_y;
   const int nb = a.n * a.B;
-  // per (i,b): sums over tiles (fixed order -> deterministic)
-  for (int ib = threadIdx.x; ib < nb; ib += blockDim.x) {
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < tiles; ++k) {
+  const double HWd = (double)a.H * a.W;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int ib = wid; ib < nb; ib += nw) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int k = lane; k < tiles; k += 64) {
       s0 += a.part_ph[(size_t)ib * tiles + k];
       s1 += a.part_sm[((size_t)ib * tiles + k) * 2 + 0];
       s2 += a.part_sm[((size_t)ib * tiles + k) * 2 + 1];
+      s3 += a.part_inv[(size_t)ib * tiles + k];
     }
-    a.U[ib * 2 + 0] = (float)s1;
-    a.U[ib * 2 + 1] = (float)s2;
-    if (ib < 64) {
+    s0 = wave_sum_d(s0);
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    s3 = wave_sum_d(s3);
+    if (lane == 0) {
+      const float mean = (float)(s3 / HWd);
+      const double mc = (double)fmaxf(mean, 1e-6f);
+      a.mean[ib] = mean;
+      a.U[ib * 2 + 0] = (float)(s1 / mc);
+      a.U[ib * 2 + 1] = (float)(s2 / mc);
       ph[ib] = s0;
-      sx[ib] = s1;
-      sy[ib] = s2;
+      sx[ib] = s1 / mc;
+      sy[ib] = s2 / mc;
     }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double HW = (double)a.H * a.W;
     const int M = a.automask ? 2 * a.N : a.N;
     double photo = 0.0, smooth = 0.0;
     for (int i = 0; i < a.n; ++i) {
@@ -320,7 +358,7 @@ __global__ __launch_bounds__(256) void photo_finalize_kernel(PhotoArgs a, float*
         qx += sx[i * a.B + b];
         qy += sy[i * a.B + b];
       }
-      double li = p / (a.B * HW);
+      double li = p / (a.B * HWd);
       if (!a.reduce_min) li /= M;
       photo += pow(0.85, (double)(a.n - i - 1)) * li;
       const double mx = qx / ((double)a.B * a.H * (a.W - 1));
@@ -534,7 +572,7 @@ using namespace dro;
 
 namespace {
 struct PhotoLayout {
-  size_t sel, mean, U, part_ph, part_sm, part_pose, total;
+  size_t sel, am, part_inv, mean, U, part_ph, part_sm, part_pose, total;
 };
 
 PhotoLayout photo_layout(int B, int N, int n, int H, int W) {
@@ -545,6 +583,10 @@ PhotoLayout photo_layout(int B, int N, int n, int H, int W) {
   size_t off = 0;
   L.sel = off;
   off = al(off + (size_t)n * B * HW);
+  L.am = off;
+  off = al(off + sizeof(float) * N * B * HW);
+  L.part_inv = off;
+  off = al(off + sizeof(float) * n * B * tiles);
   L.mean = off;
   off = al(off + sizeof(float) * n * B);
   L.U = off;
@@ -603,6 +645,8 @@ int photo_setup(PhotoArgs& a, const float* image, const float* context, const fl
   a.tiles_x = (W + TW - 1) / TW;
   a.tiles_y = (H + TH - 1) / TH;
   a.sel = (unsigned char*)(ws + L.sel);
+  a.am = (float*)(ws + L.am);
+  a.part_inv = (float*)(ws + L.part_inv);
   a.mean = (float*)(ws + L.mean);
   a.U = (float*)(ws + L.U);
   a.part_ph = (float*)(ws + L.part_ph);
@@ -631,11 +675,13 @@ extern "C" int dro_photometric_forward(const float* image, const float* context,
     return DRO_E_NULL;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(photo_mean_kernel, dim3(n * B), dim3(1024), 0, s, a);
-  if ((st = launch_status("photo_mean_kernel launch failed"))) return st;
+  if (automask) {
+    hipLaunchKernelGGL(photo_automask_kernel, dim3(a.tiles_x, a.tiles_y, N * B), dim3(kThreads), 0, s, a);
+    if ((st = launch_status("photo_automask_kernel launch failed"))) return st;
+  }
   hipLaunchKernelGGL(photo_fwd_kernel, dim3(a.tiles_x, a.tiles_y, n * B), dim3(kThreads), 0, s, a);
   if ((st = launch_status("photo_fwd_kernel launch failed"))) return st;
-  hipLaunchKernelGGL(photo_finalize_kernel, dim3(1), dim3(256), 0, s, a, out);
+  hipLaunchKernelGGL(photo_finalize_kernel, dim3(1), dim3(1024), 0, s, a, out);
   return launch_status("photo_finalize_kernel launch failed");
 }
 
