@@ -717,6 +717,8 @@ __device__ __forceinline__ __attribute__((address_space(4))) const char* kernarg
 template <int KH, int KW>
 struct HaloShapeW {
   static constexpr int T = KH * KW;
+  // 3x3: taps split 5 + 4 over the wave pairs (all 9 taps per wave over half
+  // the pixels measured no faster and needs 512 registers per lane)
   static constexpr bool TAPSPLIT = T == 9;
   static constexpr int TPW = TAPSPLIT ? 5 : T;   // accumulators (taps) per wave
   static constexpr int TH = HaloShape<32, KH, KW>::TH, TW = 64 / TH;
@@ -843,15 +845,24 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[tp][r] = 0.f;
 
+  unsigned long long* const stp = a.stamps ? a.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
+  auto stamp = [&](int k) {   // diagnostics (dro_debug_conv_stamps): 0 set-up, 12 first tile
+                                // staged, 1 prologue, 2.. tile iterations (<= 8), 13 loop done, 14 end
+    if (stp && threadIdx.x == 0 && k < 15) stp[k] = __builtin_amdgcn_s_memtime();
+  };
+  const int dbg = a.dbg;      // 1 skip the loop's loads, 2 its MFMAs, 4 its LDS stores (invalid results)
+  stamp(0);
   if (tbeg < tend) {
     load(tbeg);
     store(0);
   }
+  stamp(12);
   __syncthreads();
+  stamp(1);
   for (int tl = tbeg; tl < tend; ++tl) {
     const int buf = (tl - tbeg) & 1;
     const bool more = tl + 1 < tend;
-    if (more) load(tl + 1);
+    if (more && !(dbg & 1)) load(tl + 1);
     const float* Gs = smem + buf * STAGE;
     const float* Xs = Gs + 64 * GPAD;
     const float* ga = Gs + hi * GPAD + wo * 32 + (lane & 31);
@@ -859,6 +870,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
     constexpr int KS = TAPSPLIT ? 32 : 16;        // k-steps (pixel pairs) per wave
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+      if (dbg & 2) break;
       const int pp = 2 * ((TAPSPLIT ? 0 : w2 * 16) + s);   // even pixel of this k-step
       const float av = ga[pp * GPAD];
       const int poff = (pp / TW) * HWd + (pp % TW);
@@ -871,9 +883,11 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
         }
       }
     }
-    if (more) store(buf ^ 1);
+    if (more && !(dbg & 4)) store(buf ^ 1);
     __syncthreads();
+    if (tl - tbeg < 8) stamp(2 + tl - tbeg);
   }
+  stamp(13);
   float* wpart = a.part + (size_t)blockIdx.y * Cout * Cin * T;
   const int c = c0 + (lane & 31);
   if (TAPSPLIT) {
@@ -915,6 +929,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
       if (lane == 0 && o < Cout) a.bpart[(size_t)blockIdx.y * Cout + o] = v;
     }
   }
+  stamp(14);
 }
 
 // dW[o][c][tap] = sum_s part[s][o][c][tap]; db[o] = sum_s bpart[s][o]
@@ -1884,6 +1899,12 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
   a.bpart = reinterpret_cast<float*>(ws + align256((size_t)wh.splits * Cout * Cin * T * sizeof(float)));
   m.nuse = nuse;
   m.use_tiles = B * wh.tiles_img;
+  a.stamps = g_conv_stamps;
+  a.dbg = 0;
+  if (g_conv_stamps) {
+    const char* e = getenv("DRO_CONV_DBG");
+    a.dbg = e ? atoi(e) : 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
 #define DRO_WHM(KH_, KW_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_, true>), grid, dim3(256), 0, s, m))
