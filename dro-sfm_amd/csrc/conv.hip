@@ -734,7 +734,15 @@ struct HaloShapeW {
 };
 
 template <int KH, int KW, int GACT, bool MULTI>
-__global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>::T P) {
+// Two blocks per CU (waves_per_eu 2: accumulators move from AGPRs to VGPRs,
+// <= 256 registers, no scratch): one block's loads and stores overlap the
+// other's MFMAs -- with one wave per SIMD each pixel tile cost its MFMAs PLUS
+// its load/store phase (tools/wgrad_stamps.py).  -DDRO_WH_WAVES=1 builds the
+// one-block variant for A/B.
+#ifndef DRO_WH_WAVES
+#define DRO_WH_WAVES 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRO_WH_WAVES))) void wgrad_halo_kernel(typename WgParam<MULTI>::T P) {
   const IgArgs& a = WgParam<MULTI>::ig(P);
   using S = HaloShapeW<KH, KW>;
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
