@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   if (PF == 2 && chunk_of(1) < cend) load(sb, chunk_of(1));
   __syncthreads();
   stamp(1);
-  const int dbg = a.dbg;
+  const int dbg = ablation_flags(a.dbg);
   if (PF == 1) {
     for (int it = 0; it < nit; ++it) {
       const int buf = it & 1;
@@ -734,15 +734,7 @@ struct HaloShapeW {
 };
 
 template <int KH, int KW, int GACT, bool MULTI>
-// Two blocks per CU (waves_per_eu 2: accumulators move from AGPRs to VGPRs,
-// <= 256 registers, no scratch): one block's loads and stores overlap the
-// other's MFMAs -- with one wave per SIMD each pixel tile cost its MFMAs PLUS
-// its load/store phase (tools/wgrad_stamps.py).  -DDRO_WH_WAVES=1 builds the
-// one-block variant for A/B.
-#ifndef DRO_WH_WAVES
-#define DRO_WH_WAVES 2
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRO_WH_WAVES))) void wgrad_halo_kernel(typename WgParam<MULTI>::T P) {
+__global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>::T P) {
   const IgArgs& a = WgParam<MULTI>::ig(P);
   using S = HaloShapeW<KH, KW>;
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
@@ -858,7 +850,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRO_WH_WAVE
                                 // staged, 1 prologue, 2.. tile iterations (<= 8), 13 loop done, 14 end
     if (stp && threadIdx.x == 0 && k < 15) stp[k] = __builtin_amdgcn_s_memtime();
   };
-  const int dbg = a.dbg;      // 1 skip the loop's loads, 2 its MFMAs, 4 its LDS stores (invalid results)
+  const int dbg = ablation_flags(a.dbg);      // 1 skip the loop's loads, 2 its MFMAs, 4 its LDS stores (invalid results)
   stamp(0);
   if (tbeg < tend) {
     load(tbeg);

@@ -101,6 +101,15 @@ struct IgArgs {
                                 // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)
 };
 
+// The K-loop ablations exist only in a diagnostic build (-DDRO_CONV_ABLATE=1,
+// for tools/conv_stamps.py and tools/wgrad_stamps.py): in the product build
+// the flags fold to 0.  A runtime ablation branch cost the weight-gradient
+// kernel its full unroll (1x5 multi-use launch 123 -> 176 us).
+#ifndef DRO_CONV_ABLATE
+#define DRO_CONV_ABLATE 0
+#endif
+__device__ __forceinline__ int ablation_flags(int dbg) { return DRO_CONV_ABLATE ? dbg : 0; }
+
 __device__ __forceinline__ float act_fwd(float v, int act) {
   switch (act) {
     case 1: return fmaxf(v, 0.f);

@@ -234,21 +234,40 @@ __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
   if (gdepth && live) gdepth[b * P + p] = gd_total * dd;
 }
 
-__global__ void pose_finalize_kernel(const float* __restrict__ partial, int nblk, int npose,
-                                     const float* __restrict__ pose, int pose_mode,
-                                     float* __restrict__ gpose) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One 64-lane block per pose: lanes 0..59 = 5 row groups x 12 components
+// stride over the pose's [nblk][12] partials (coalesced), then the 5 group
+// sums are added in a fixed order (deterministic).  The photometric loss hands
+// in 240 tile partials per pose: one serial thread per pose took 51 us there.
+__global__ __launch_bounds__(64) void pose_finalize_kernel(const float* __restrict__ partial, int nblk,
+                                                           int npose, const float* __restrict__ pose,
+                                                           int pose_mode, float* __restrict__ gpose) {
+  constexpr int G = 5;   // row groups
+  __shared__ float sh[G * 12];
+  __shared__ float s[12];
+  const int i = blockIdx.x, lane = threadIdx.x;
   if (i >= npose) return;
-  float s[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) s[k] = 0.f;
-  for (int j = 0; j < nblk; ++j) {
-    const float* src = partial + ((size_t)i * nblk + j) * 12;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) s[k] += src[k];
+  if (lane < G * 12) {
+    const int comp = lane % 12, g = lane / 12;
+    const float* src = partial + (size_t)i * nblk * 12 + comp;
+    float v = 0.f;
+    for (int j = g; j < nblk; j += G) v += src[(size_t)j * 12];
+    sh[lane] = v;
   }
-  const int ps = pose_stride(pose_mode);
-  store_pose_grad(pose + (size_t)i * ps, pose_mode, s, s + 9, gpose + (size_t)i * ps);
+  __syncthreads();
+  if (lane < 12) {
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) v += sh[g * 12 + lane];
+    s[lane] = v;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    float r[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) r[k] = s[k];
+    const int ps = pose_stride(pose_mode);
+    store_pose_grad(pose + (size_t)i * ps, pose_mode, r, r + 9, gpose + (size_t)i * ps);
+  }
 }
 
 // ------------------------------------------------------------------ plane sweep (forward only)
@@ -316,7 +335,8 @@ __global__ __launch_bounds__(256) void plane_sweep_wide_kernel(WarpArgs a, const
 
 int launch_pose_finalize(const float* partial, int nblk, int npose, const float* pose,
                          int pose_mode, float* gpose, hipStream_t s) {
-  hipLaunchKernelGGL(pose_finalize_kernel, dim3((npose + 63) / 64), dim3(64), 0, s, partial, nblk,
+  if (npose <= 0) return 0;
+  hipLaunchKernelGGL(pose_finalize_kernel, dim3(npose), dim3(64), 0, s, partial, nblk,
                      npose, pose, pose_mode, gpose);
   return launch_status("pose_finalize_kernel launch failed");
 }

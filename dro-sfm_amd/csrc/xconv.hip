@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(IgArgs a) {
   };
   stamp(0);
   if (stp && threadIdx.x == blockDim.x - 64) stp[15] = __builtin_amdgcn_s_memtime();
-  const int dbg = a.dbg;   // diagnostics: 1 skip the loop's loads, 2 its MFMAs, 4 its LDS stores
+  const int dbg = ablation_flags(a.dbg);   // diagnostics: 1 skip the loop's loads, 2 its MFMAs, 4 its LDS stores
   // one register stage: chunk c+1 is loaded before chunk c's MFMAs and
   // stored after them.  (Measured alternative: store c+1 after the MFMAs and
   // re-issue c+2 at once -- no faster per iteration, +1.8k cycles of prologue.)

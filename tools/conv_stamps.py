@@ -3,6 +3,8 @@
 reductions -> epilogue, per block, in shader-clock cycles.
 
 usage: python tools/conv_stamps.py    (runs the bench roofline shape and a 1x1)
+Ablations (STAMP_DBG=1,2,4) need a diagnostic build:
+make -C dro-sfm_amd/csrc clean all EXTRA=-DDRO_CONV_ABLATE=1
 """
 import ctypes
 import os

@@ -3,7 +3,9 @@
 set-up -> first tile staged -> prologue -> each pixel tile -> loop done -> end.
 
 usage: python tools/wgrad_stamps.py     (STAMP_DBG=0,1,2,4 for the ablations:
-                                          1 no loads, 2 no MFMAs, 4 no LDS stores)
+                                          1 no loads, 2 no MFMAs, 4 no LDS stores;
+                                          they need a diagnostic build:
+                                          make -C dro-sfm_amd/csrc clean all EXTRA=-DDRO_CONV_ABLATE=1)
 """
 import ctypes
 import os
