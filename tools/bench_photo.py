@@ -1,0 +1,59 @@
+"""Photometric loss micro-benchmark at the KITTI metric shape (B=2, N=2, n=9,
+192x640): forward + backward of hip.photometric_loss, HIP events per phase.
+Run under `rocprofv3 --kernel-trace --stats` for the per-kernel split.
+usage: python tools/bench_photo.py [--iters 50] [--n 9]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import dro_sfm_amd.hip as hip  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--n", type=int, default=9)
+    ap.add_argument("--B", type=int, default=2)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, N, n, H, W = args.B, 2, args.n, 192, 640
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    low = torch.rand(B, 3, H // 8, W // 8, generator=g, device=dev)
+    img = (torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
+           + 0.1 * torch.rand(B, 3, H, W, generator=g, device=dev)).clamp(0, 1)
+    ctx = torch.stack([(torch.roll(img, 3 * (j + 1), 3) * 0.9
+                        + 0.1 * torch.rand(B, 3, H, W, generator=g, device=dev)) for j in range(N)])
+    invs = (0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g, device=dev)).requires_grad_(True)
+    pose = torch.cat([0.1 * torch.randn(N, n, B, 3, generator=g, device=dev),
+                      0.02 * torch.randn(N, n, B, 3, generator=g, device=dev)], 3).requires_grad_(True)
+    K = torch.tensor([[371.8, 0.0, 314.1], [0.0, 369.4, 88.5], [0.0, 0.0, 1.0]],
+                     device=dev).unsqueeze(0).repeat(B, 1, 1)
+    for _ in range(3):
+        loss, _ = hip.photometric_loss(img, ctx, invs, pose, K)
+        loss.backward()
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    f = b = 0.0
+    for _ in range(args.iters):
+        e[0].record()
+        loss, _ = hip.photometric_loss(img, ctx, invs, pose, K)
+        e[1].record()
+        loss.backward()
+        e[2].record()
+        torch.cuda.synchronize()
+        f += e[0].elapsed_time(e[1])
+        b += e[1].elapsed_time(e[2])
+    print(f"photometric B={B} N={N} n={n} {H}x{W}: fwd {1e3 * f / args.iters:.1f} us, "
+          f"bwd {1e3 * b / args.iters:.1f} us (incl. autograd glue), loss {float(loss):.6f}, "
+          f"|ginv| {float(invs.grad.abs().sum()):.6e}, |gpose| {float(pose.grad.abs().sum()):.6e}")
+
+
+if __name__ == "__main__":
+    main()
