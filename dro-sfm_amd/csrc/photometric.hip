@@ -67,6 +67,67 @@ __device__ __forceinline__ int reflect_idx(int y, int H) {
   return min(max(y, 0), H - 1);
 }
 
+// Stage the tile's inverse depth with a HALO-pixel reflected ring into LDS
+// (pitch PW): read once per block, shared by every reference j and by the
+// smoothness term (in-range neighbours of the reflected ring equal the image).
+template <int PL, int PW, int HALO>
+__device__ __forceinline__ void stage_inv(const float* __restrict__ invp, int x0, int y0, int H, int W,
+                                          float* __restrict__ invt) {
+  for (int k = threadIdx.x; k < PL; k += kThreads) {
+    const int gy = reflect_idx(y0 + k / PW - HALO, H), gx = reflect_idx(x0 + k % PW - HALO, W);
+    invt[k] = invp[(size_t)gy * W + gx];
+  }
+}
+
+// Synthesise the warped reference (view_synthesis, camera_utils.py:23-56) of
+// context (j, b) over the LDS tile [PL] (pitch PW, reflected ring HALO) into
+// est[3][PL].  The per-thread iterations are unrolled so every bilinear
+// gather of the thread is in flight at once (the phase is bound by the
+// gathers' latency, not by arithmetic).  Arithmetic order as synth().
+template <int PL, int PW, int HALO>
+__device__ __forceinline__ void stage_warp(const PhotoArgs& a, const float* __restrict__ ctx,
+                                           const float* __restrict__ invt, const float ki[9],
+                                           const float kr[9], const float R[9], const float t[3],
+                                           int x0, int y0, float* __restrict__ est) {
+  constexpr int IT = (PL + kThreads - 1) / kThreads;
+  constexpr int CH = 2;  // iterations whose gathers are in flight together (VGPR budget)
+  const size_t HW = (size_t)a.H * a.W;
+#pragma unroll
+  for (int i0 = 0; i0 < IT; i0 += CH) {
+    Taps T[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int k = min((int)threadIdx.x + (i0 + u) * kThreads, PL - 1);  // tail: computed, not stored
+      const int gy = reflect_idx(y0 + k / PW - HALO, a.H), gx = reflect_idx(x0 + k % PW - HALO, a.W);
+      float dd;
+      const float depth = decode_depth(invt[k], DRO_DEPTH_INV, 0.f, 0.f, &dd);
+      Proj q;
+      project(ki, kr, R, t, (float)gx, (float)gy, depth, a.H, a.W, q);
+      bilinear_taps(q.ix, q.iy, a.H, a.W, T[u]);
+    }
+    float v[CH][3][4];
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[u][c][q] = ctx[c * HW + (T[u].ok[q] ? T[u].idx[q] : 0)];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int k = threadIdx.x + (i0 + u) * kThreads;
+      if (i0 + u >= IT || k >= PL) continue;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (T[u].ok[q]) s += v[u][c][q] * T[u].wgt[q];
+        est[c * PL + k] = s;
+      }
+    }
+  }
+}
+
 // one synthesised RGB sample of context (j, b) at target pixel (x, y)
 __device__ __forceinline__ void synth(const PhotoArgs& a, const float* __restrict__ ctx,
                                       const float ki[9], const float kr[9], const float R[9],
@@ -192,6 +253,7 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
   constexpr int PL = H1 * W1;
   __shared__ float tgt[3 * PL];
   __shared__ float est[3 * PL];
+  __shared__ float invt[PL];
   __shared__ float scratch[4 * (kThreads / kWave)];
 
   const int ib = blockIdx.z, i = ib / a.B, b = ib % a.B;
@@ -207,6 +269,8 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) tgt[c * PL + k] = img[c * HW + (size_t)gy * W + gx];
   }
+  stage_inv<PL, W1, 1>(invp, x0, y0, H, W, invt);
+  __syncthreads();
 
   float ki[9], kr[9];
   cams_full(a, b, ki, kr);
@@ -224,14 +288,8 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
     float R[9], t[3];
     load_pose(a.pose + ((size_t)(j * a.n + i) * a.B + b) * ps, a.pose_mode, R, t);
     const float* ctx = a.context + ((size_t)j * a.B + b) * 3 * HW;
-    __syncthreads();  // previous j's readers are done with est/raw
-    for (int k = threadIdx.x; k < PL; k += kThreads) {
-      const int gy = reflect_idx(y0 + k / W1 - 1, H), gx = reflect_idx(x0 + k % W1 - 1, W);
-      float o[3];
-      synth(a, ctx, ki, kr, R, t, gx, gy, invp[(size_t)gy * W + gx], o, nullptr, nullptr);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) est[c * PL + k] = o[c];
-    }
+    if (j) __syncthreads();  // previous j's readers are done with est
+    stage_warp<PL, W1, 1>(a, ctx, invt, ki, kr, R, t, x0, y0, est);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kPxPerThread; ++r) {
@@ -282,16 +340,16 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
     // smoothness (utils/depth.py:166-199): normalised inv-depth gradients
     // weighted by exp(-mean_c |image gradient|)
     const int o = (ly + 1) * W1 + (lx + 1);
-    const float d0 = invp[gp];
+    const float d0 = invt[o];
     v3[3] += d0;
     if (gx < W - 1) {
-      const float g = d0 - invp[gp + 1];
+      const float g = d0 - invt[o + 1];
       const float gi = (fabsf(tgt[o] - tgt[o + 1]) + fabsf(tgt[PL + o] - tgt[PL + o + 1]) +
                         fabsf(tgt[2 * PL + o] - tgt[2 * PL + o + 1])) / 3.f;
       v3[1] += fabsf(g * expf(-gi));
     }
     if (gy < H - 1) {
-      const float g = d0 - invp[gp + W];
+      const float g = d0 - invt[o + W1];
       const float gi = (fabsf(tgt[o] - tgt[o + W1]) + fabsf(tgt[PL + o] - tgt[PL + o + W1]) +
                         fabsf(tgt[2 * PL + o] - tgt[2 * PL + o + W1])) / 3.f;
       v3[2] += fabsf(g * expf(-gi));
@@ -373,7 +431,7 @@ __global__ __launch_bounds__(1024) void photo_finalize_kernel(PhotoArgs a, float
 }
 
 // ------------------------------------------------------------------ backward tile kernel
-__global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
                                                              float* __restrict__ ginv) {
   constexpr int PL2 = H2 * W2;  // est / tgt with 2-px halo
   constexpr int PL1 = H1 * W1;  // adjoint image with 1-px halo
@@ -381,6 +439,7 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
   __shared__ float est[3 * PL2];
   __shared__ float adj[9 * PL1];  // per channel: dL/dmu_x, dL/dE[x^2], dL/dE[xy]
   __shared__ unsigned char selt[PL1];
+  __shared__ float invt[PL2];
   __shared__ float scratch[12 * (kThreads / kWave)];
 
   const int ib = blockIdx.z, i = ib / a.B, b = ib % a.B;
@@ -405,6 +464,8 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
     const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
     selt[k] = (in && a.reduce_min) ? a.sel[(size_t)ib * HW + (size_t)gy * W + gx] : 255;
   }
+  stage_inv<PL2, W2, 2>(invp, x0, y0, H, W, invt);
+  __syncthreads();
 
   float ki[9], kr[9];
   cams_full(a, b, ki, kr);
@@ -419,14 +480,8 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
     load_pose(a.pose + ((size_t)(j * a.n + i) * a.B + b) * ps, a.pose_mode, R, t);
     const float* ctx = a.context + ((size_t)j * a.B + b) * 3 * HW;
     const int kw = a.automask ? 2 * j : j;
-    __syncthreads();
-    for (int k = threadIdx.x; k < PL2; k += kThreads) {
-      const int gy = reflect_idx(y0 + k / W2 - 2, H), gx = reflect_idx(x0 + k % W2 - 2, W);
-      float o[3];
-      synth(a, ctx, ki, kr, R, t, gx, gy, invp[(size_t)gy * W + gx], o, nullptr, nullptr);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) est[c * PL2 + k] = o[c];
-    }
+    if (j) __syncthreads();
+    stage_warp<PL2, W2, 2>(a, ctx, invt, ki, kr, R, t, x0, y0, est);
     __syncthreads();
     // adjoint of the SSIM term at every real pixel of the tile + 1-px ring
     for (int k = threadIdx.x; k < PL1; k += kThreads) {
@@ -464,37 +519,94 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
     float acc[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+    // (1) projections and bilinear taps of the thread's pixels, all their
+    // context gathers issued before the LDS adjoint sums below consume time
+    // Only the bilinear derivative terms stay live (6 floats per pixel); the
+    // projection is recomputed for the chain rule in (3).
+    float dxc[kPxPerThread][3], dyc[kPxPerThread][3];
+#pragma unroll
+    for (int r = 0; r < kPxPerThread; ++r) {
+      const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
+      const int gy = y0 + ly, gx = x0 + lx;
+      float dd;
+      const float depth = decode_depth(invt[(ly + 2) * W2 + (lx + 2)], DRO_DEPTH_INV, 0.f, 0.f, &dd);
+      Proj q;
+      Taps T;
+      project(ki, kr, R, t, (float)gx, (float)gy, depth, H, W, q);
+      bilinear_taps(q.ix, q.iy, H, W, T);
+      const float omy = 1.f - T.ty, omx = 1.f - T.tx;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float x = ctx[c * HW + (T.ok[k] ? T.idx[k] : 0)];
+          v[k] = T.ok[k] ? x : 0.f;
+        }
+        dxc[r][c] = (v[1] - v[0]) * omy + (v[3] - v[2]) * T.ty;
+        dyc[r][c] = (v[2] - v[0]) * omx + (v[3] - v[1]) * T.tx;
+      }
+    }
 #pragma unroll
     for (int r = 0; r < kPxPerThread; ++r) {
       const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
       const int gy = y0 + ly, gx = x0 + lx;
       if (gy >= H || gx >= W) continue;
-      // rows/cols of real pixels whose 3x3 (reflected) windows tap this pixel
-      int rows[4], nr = 0, cols[4], nc = 0;
-      for (int d = -1; d <= 1; ++d) {
-        if (gy + d >= 0 && gy + d < H) rows[nr++] = ly + 1 + d;
-        if (gx + d >= 0 && gx + d < W) cols[nc++] = lx + 1 + d;
-      }
-      if (gy == 1) rows[nr++] = ly;              // row 0's tap at -1 reflects to 1
-      if (gy == H - 2) rows[nr++] = ly + 2;      // row H-1's tap at H reflects to H-2
-      if (gx == 1) cols[nc++] = lx;
-      if (gx == W - 2) cols[nc++] = lx + 2;
       const int o2 = (ly + 2) * W2 + (lx + 2);
       const int o1 = (ly + 1) * W1 + (lx + 1);
       const bool self_on = a.reduce_min ? (selt[o1] == kw) : true;
+      // (2) adjoint of the 3x3 average pools: sum over the real pixels whose
+      // (reflected) windows tap this pixel.  Pixels >= 2 from every border
+      // see exactly the 3x3 neighbourhood (same summation order as the
+      // general path, which handles the reflected taps explicitly).
+      float sA[3], sB[3], sC[3];
+      if (gy >= 2 && gy <= H - 3 && gx >= 2 && gx <= W - 3) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = 0; v < 3; ++v) {
+              const int kk = (ly + u) * W1 + (lx + v);
+              s0 += adj[(3 * c + 0) * PL1 + kk];
+              s1 += adj[(3 * c + 1) * PL1 + kk];
+              s2 += adj[(3 * c + 2) * PL1 + kk];
+            }
+          sA[c] = s0;
+          sB[c] = s1;
+          sC[c] = s2;
+        }
+      } else {
+        int rows[4], nr = 0, cols[4], nc = 0;
+        for (int d = -1; d <= 1; ++d) {
+          if (gy + d >= 0 && gy + d < H) rows[nr++] = ly + 1 + d;
+          if (gx + d >= 0 && gx + d < W) cols[nc++] = lx + 1 + d;
+        }
+        if (gy == 1) rows[nr++] = ly;              // row 0's tap at -1 reflects to 1
+        if (gy == H - 2) rows[nr++] = ly + 2;      // row H-1's tap at H reflects to H-2
+        if (gx == 1) cols[nc++] = lx;
+        if (gx == W - 2) cols[nc++] = lx + 2;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+          for (int u = 0; u < nr; ++u)
+            for (int v = 0; v < nc; ++v) {
+              const int kk = rows[u] * W1 + cols[v];
+              s0 += adj[(3 * c + 0) * PL1 + kk];
+              s1 += adj[(3 * c + 1) * PL1 + kk];
+              s2 += adj[(3 * c + 2) * PL1 + kk];
+            }
+          sA[c] = s0;
+          sB[c] = s1;
+          sC[c] = s2;
+        }
+      }
       float gest[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        float sA = 0.f, sB = 0.f, sC = 0.f;
-        for (int u = 0; u < nr; ++u)
-          for (int v = 0; v < nc; ++v) {
-            const int kk = rows[u] * W1 + cols[v];
-            sA += adj[(3 * c + 0) * PL1 + kk];
-            sB += adj[(3 * c + 1) * PL1 + kk];
-            sC += adj[(3 * c + 2) * PL1 + kk];
-          }
         const float xv = est[c * PL2 + o2], yv = tgt[c * PL2 + o2];
-        float ge = (sA + 2.f * xv * sB + yv * sC) / 9.f;
+        float ge = (sA[c] + 2.f * xv * sB[c] + yv * sC[c]) / 9.f;
         if (self_on) {
           const float df = xv - yv;
           const float sg = df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f);
@@ -502,24 +614,17 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
         }
         gest[c] = ge;
       }
-      // chain through the bilinear sample and the projection
-      Proj q;
-      Taps T;
-      float o[3];
-      const size_t gp = (size_t)gy * W + gx;
-      synth(a, ctx, ki, kr, R, t, gx, gy, invp[gp], o, &q, &T);
+      // (3) chain through the bilinear sample and the projection
       float gix = 0.f, giy = 0.f;
-      const float omy = 1.f - T.ty, omx = 1.f - T.tx;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float* pl = ctx + c * HW;
-        const float v0 = T.ok[0] ? pl[T.idx[0]] : 0.f;
-        const float v1 = T.ok[1] ? pl[T.idx[1]] : 0.f;
-        const float v2 = T.ok[2] ? pl[T.idx[2]] : 0.f;
-        const float v3 = T.ok[3] ? pl[T.idx[3]] : 0.f;
-        gix += gest[c] * ((v1 - v0) * omy + (v3 - v2) * T.ty);
-        giy += gest[c] * ((v2 - v0) * omx + (v3 - v1) * T.tx);
+        gix += gest[c] * dxc[r][c];
+        giy += gest[c] * dyc[r][c];
       }
+      float dd;
+      const float depth = decode_depth(invt[o2], DRO_DEPTH_INV, 0.f, 0.f, &dd);
+      Proj q;
+      project(ki, kr, R, t, (float)gx, (float)gy, depth, H, W, q);
       gdep[r] += project_backward(q, kr, R, gix, giy, acc, acc + 9);
     }
     if (a.part_pose) {
@@ -548,7 +653,7 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
     if (gy >= H || gx >= W) continue;
     const size_t gp = (size_t)gy * W + gx;
     const int o = (ly + 2) * W2 + (lx + 2);
-    const float iv = invp[gp];
+    const float iv = invt[o];
     float dd;
     decode_depth(iv, DRO_DEPTH_INV, 0.f, 0.f, &dd);
     float gy_n = 0.f;  // dL/d(normalised inv) at this pixel
@@ -558,10 +663,11 @@ __global__ __launch_bounds__(kThreads) void photo_bwd_kernel(PhotoArgs a, const 
                      fabsf(tgt[2 * PL2 + oa] - tgt[2 * PL2 + ob])) / 3.f));
     };
     auto sgn = [](float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); };
-    if (gx < W - 1) gy_n += cx * sgn((yq - invp[gp + 1] / mc) * wgt(o, o + 1)) * wgt(o, o + 1);
-    if (gx > 0) gy_n -= cx * sgn((invp[gp - 1] / mc - yq) * wgt(o - 1, o)) * wgt(o - 1, o);
-    if (gy < H - 1) gy_n += cy * sgn((yq - invp[gp + W] / mc) * wgt(o, o + W2)) * wgt(o, o + W2);
-    if (gy > 0) gy_n -= cy * sgn((invp[gp - W] / mc - yq) * wgt(o - W2, o)) * wgt(o - W2, o);
+    // neighbours read from the staged tile only where they are real pixels
+    if (gx < W - 1) gy_n += cx * sgn((yq - invt[o + 1] / mc) * wgt(o, o + 1)) * wgt(o, o + 1);
+    if (gx > 0) gy_n -= cx * sgn((invt[o - 1] / mc - yq) * wgt(o - 1, o)) * wgt(o - 1, o);
+    if (gy < H - 1) gy_n += cy * sgn((yq - invt[o + W2] / mc) * wgt(o, o + W2)) * wgt(o, o + W2);
+    if (gy > 0) gy_n -= cy * sgn((invt[o - W2] / mc - yq) * wgt(o - W2, o)) * wgt(o - W2, o);
     ginv[(size_t)ib * HW + gp] = gdep[r] * dd + gy_n / mc - mterm;
   }
 }

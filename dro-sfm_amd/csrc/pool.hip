@@ -1,0 +1,124 @@
+// 3x3 / stride 2 / pad 1 max pooling of the ResNet-18 stem (fwd + bwd).
+//
+// Replaces F.max_pool2d(x, 3, 2, 1) after conv1/bn1/relu in ResNetEncoder
+// (dro_sfm/networks/optim/extractor.py:60-66 of the reference, torchvision's
+// ResNet stem).  ATen's NCHW kernels took 20 us forward and 55 us backward per
+// call at the fnet shape (6 x 64 x 96 x 320): the backward recomputes window
+// bounds per input pixel and reads int64 indices.  Here:
+//   forward  : one thread per output pixel, max over the clipped window in
+//              ATen's scan order (rows, then columns; `v > max || isnan(v)`),
+//              argmax kept as one byte per output (dy * 3 + dx);
+//   backward : one thread per input pixel gathers the (at most 2 x 2) windows
+//              that contain it, in ATen's (ph, pw) ascending order, so the
+//              float sums are bit-identical to max_pool2d's backward.
+// Roofline: HBM bound.  Algorithmic bytes per plane: forward 4*H*W read +
+// 5*Ho*Wo written; backward 5*Ho*Wo read + 4*H*W written.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "dro_common.hpp"
+
+namespace dro {
+
+constexpr int kPoolThreads = 256;
+
+__global__ __launch_bounds__(kPoolThreads) void maxpool3s2_fwd_kernel(const float* __restrict__ x,
+                                                                     long long planes, int H, int W,
+                                                                     int Ho, int Wo,
+                                                                     float* __restrict__ y,
+                                                                     unsigned char* __restrict__ idx) {
+  const long long o = (long long)blockIdx.x * kPoolThreads + threadIdx.x;
+  if (o >= planes * Ho * Wo) return;
+  const int ox = (int)(o % Wo);
+  const long long t = o / Wo;
+  const int oy = (int)(t % Ho);
+  const long long pl = t / Ho;
+  const float* __restrict__ p = x + pl * H * W;
+  const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
+  float m = -INFINITY;
+  int arg = -1;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yy = y0 + dy;
+    if (yy < 0 || yy >= H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int xx = x0 + dx;
+      if (xx < 0 || xx >= W) continue;
+      const float v = p[(long long)yy * W + xx];
+      if (arg < 0) arg = dy * 3 + dx;   // ATen's initial index: the first in-range tap
+      if (v > m || isnan(v)) {
+        m = v;
+        arg = dy * 3 + dx;
+      }
+    }
+  }
+  y[o] = m;
+  idx[o] = (unsigned char)arg;
+}
+
+__global__ __launch_bounds__(kPoolThreads) void maxpool3s2_bwd_kernel(const float* __restrict__ gy,
+                                                                     const unsigned char* __restrict__ idx,
+                                                                     long long planes, int H, int W,
+                                                                     int Ho, int Wo,
+                                                                     float* __restrict__ gx) {
+  const long long i = (long long)blockIdx.x * kPoolThreads + threadIdx.x;
+  if (i >= planes * H * W) return;
+  const int xx = (int)(i % W);
+  const long long t = i / W;
+  const int yy = (int)(t % H);
+  const long long pl = t / H;
+  // windows oy with 2*oy-1 <= yy <= 2*oy+1 (ATen p_start / p_end for k3 s2 p1)
+  const int ph0 = (yy + 1 < 3) ? 0 : (yy + 1 - 3) / 2 + 1, ph1 = min((yy + 1) / 2 + 1, Ho);
+  const int pw0 = (xx + 1 < 3) ? 0 : (xx + 1 - 3) / 2 + 1, pw1 = min((xx + 1) / 2 + 1, Wo);
+  const float* __restrict__ g = gy + pl * Ho * Wo;
+  const unsigned char* __restrict__ id = idx + pl * Ho * Wo;
+  float acc = 0.f;
+  for (int ph = ph0; ph < ph1; ++ph)
+    for (int pw = pw0; pw < pw1; ++pw) {
+      const int code = (yy - 2 * ph + 1) * 3 + (xx - 2 * pw + 1);
+      const long long k = (long long)ph * Wo + pw;
+      if (id[k] == code) acc += g[k];
+    }
+  gx[i] = acc;
+}
+
+}  // namespace dro
+
+using namespace dro;
+
+static int pool_check(const void* a, const void* b, const void* c, long long planes, int H, int W) {
+  if (!a || !b || !c) {
+    set_error("maxpool3x3s2: NULL pointer");
+    return DRO_E_NULL;
+  }
+  if (planes < 1 || H < 1 || W < 1 || planes * (long long)H * W >= (1LL << 40)) {
+    set_error("maxpool3x3s2: sizes out of range");
+    return DRO_E_SHAPE;
+  }
+  return DRO_OK;
+}
+
+extern "C" int dro_maxpool3x3s2_forward(const float* x, long long planes, int H, int W, float* y,
+                                        unsigned char* argmax, void* stream) {
+  int st = pool_check(x, y, argmax, planes, H, W);
+  if (st) return st;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long total = planes * Ho * Wo;
+  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((unsigned)((total + kPoolThreads - 1) / kPoolThreads)),
+                     dim3(kPoolThreads), 0, (hipStream_t)stream, x, planes, H, W, Ho, Wo, y, argmax);
+  return launch_status("maxpool3s2_fwd_kernel launch failed");
+}
+
+extern "C" int dro_maxpool3x3s2_backward(const float* grad_y, const unsigned char* argmax,
+                                         long long planes, int H, int W, float* grad_x,
+                                         void* stream) {
+  int st = pool_check(grad_y, argmax, grad_x, planes, H, W);
+  if (st) return st;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long total = planes * (long long)H * W;
+  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((unsigned)((total + kPoolThreads - 1) / kPoolThreads)),
+                     dim3(kPoolThreads), 0, (hipStream_t)stream, grad_y, argmax, planes, H, W, Ho, Wo,
+                     grad_x);
+  return launch_status("maxpool3s2_bwd_kernel launch failed");
+}

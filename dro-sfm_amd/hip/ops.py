@@ -433,6 +433,45 @@ def bilinear_upsample2x(x):
     return _Bilinear2x.apply(x)
 
 
+# ------------------------------------------------------------------ ResNet stem max pooling
+class _MaxPool3s2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        lib = _lib.load()
+        require_device(x, what="maxpool3x3s2")
+        N, C, H, W = x.shape
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        x = x.contiguous()
+        y = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.float32)
+        arg = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.uint8)
+        check(lib.dro_maxpool3x3s2_forward(ptr(x), N * C, H, W, ptr(y), ptr(arg), stream_of(x)),
+              "dro_maxpool3x3s2_forward")
+        ctx.save_for_backward(arg)
+        ctx.shape = (N, C, H, W)
+        ctx.mark_non_differentiable(arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = _lib.load()
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        gy = gy.contiguous()
+        gx = torch.empty(N, C, H, W, device=gy.device, dtype=torch.float32)
+        check(lib.dro_maxpool3x3s2_backward(ptr(gy), ptr(arg), N * C, H, W, ptr(gx), stream_of(gy)),
+              "dro_maxpool3x3s2_backward")
+        return gx
+
+
+def maxpool3x3s2(x):
+    """F.max_pool2d(x, 3, 2, 1) for float32 NCHW on the GPU (ResNet stem,
+    reference networks/optim/extractor.py:60-66); bit-identical forward and
+    backward, one argmax byte per output instead of int64 indices."""
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("maxpool3x3s2: expects a float32 NCHW tensor")
+    return _MaxPool3s2.apply(x)
+
+
 class _BatchNormAct(torch.autograd.Function):
     """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
 

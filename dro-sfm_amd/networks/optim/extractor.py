@@ -14,7 +14,9 @@ MIOpen's BN: measured on MI355X (tools/diag_miopen2.py), its one-pass
 variance put 1e-2 relative error on encoder gradients against the fp64
 oracle.  Eval mode and CPU tensors use PyTorch's native kernels.
 The 2x bilinear upsampling of the fusion head is a HIP kernel
-(hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.
+(hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.  So
+is the stem's 3x3/s2 max pooling (hip.maxpool3x3s2, bit-identical to
+F.max_pool2d forward and backward; ATen's backward took 55 us per call).
 """
 import torch
 import torch.nn as nn
@@ -24,6 +26,12 @@ from ... import hip
 
 
 _FUSED_BN = [True]
+_NATIVE_POOL = [True]
+
+
+def set_native_maxpool(enabled):
+    """hip.maxpool3x3s2 for the stem pooling on the GPU (default True)."""
+    _NATIVE_POOL[0] = bool(enabled)
 
 
 def set_fused_batchnorm(enabled):
@@ -111,7 +119,8 @@ class ResNetEncoder(nn.Module):
         if isinstance(x, (list, tuple)):
             chunks = len(x)
             x = torch.cat(list(x), 0)
-        x = F.max_pool2d(self.bn1.act(self.conv1(x)), 3, 2, 1)
+        x = self.bn1.act(self.conv1(x))
+        x = hip.maxpool3x3s2(x) if (x.is_cuda and _NATIVE_POOL[0]) else F.max_pool2d(x, 3, 2, 1)
         s4 = self.layer1(x)
         s8 = self.layer2(s4)
         x = self.layer3(s8)

@@ -178,6 +178,17 @@ int dro_bilinear_upsample2x_forward(const float* x, long long planes, int h, int
 int dro_bilinear_upsample2x_backward(const float* grad_out, long long planes, int h, int w,
                                      float* grad_x, void* stream);
 
+/* 3x3 / stride 2 / pad 1 max pooling of the ResNet-18 stem
+ * (F.max_pool2d(x, 3, 2, 1) in ResNetEncoder, networks/optim/extractor.py:60-66
+ * of the reference).  x [planes, H, W] -> y [planes, Ho, Wo], Ho = (H-1)/2+1,
+ * and one argmax byte per output (dy*3+dx within the window; ATen's tie order).
+ * The backward gathers in ATen's window order: bit-identical to max_pool2d's
+ * backward. */
+int dro_maxpool3x3s2_forward(const float* x, long long planes, int H, int W, float* y,
+                             unsigned char* argmax, void* stream);
+int dro_maxpool3x3s2_backward(const float* grad_y, const unsigned char* argmax,
+                              long long planes, int H, int W, float* grad_x, void* stream);
+
 /* Training-mode BatchNorm2d fused with the ReLU / residual add that follows it
  * in the ResNet-18 encoders (networks/optim/extractor.py:7-107 of the reference;
  * BasicBlock: relu(bn(conv(x)) [+ skip])).  Replaces torch.nn.functional.

@@ -159,9 +159,10 @@ def test_warp_cost_rejects_bad_input(hip):
 
 
 # ------------------------------------------------------------------ photometric loss
-def _fp64_photometric(d):
-    """fp64 oracle gradients on the fixture inputs: the yardstick for how far the
-    reference's own fp32 reductions sit from the exact result."""
+def _fp64_photometric(d, forced_selection=None):
+    """fp64 oracle loss and gradients on the fixture inputs: the yardstick for how
+    far the reference's own fp32 reductions sit from the exact result.  With
+    forced_selection the min reduction takes the given candidates."""
     dt = torch.float64
     invs = [i.cpu().to(dt).requires_grad_(True) for i in d["inv_depths"]]
     vecs = d["poses"].cpu().to(dt).requires_grad_(True)
@@ -170,33 +171,57 @@ def _fp64_photometric(d):
     out = O.photometric_decay_loss(d["image"].cpu().to(dt), [c.cpu().to(dt) for c in d["context"]], invs,
                                    d["K"].cpu().to(dt), d["K"].cpu().to(dt), poses,
                                    automask=bool(int(d["automask"])),
-                                   reduce="min" if int(d["reduce_min"]) else "mean")
+                                   reduce="min" if int(d["reduce_min"]) else "mean",
+                                   forced_selection=forced_selection)
     out["loss"].sum().backward()
-    return torch.stack([i.grad for i in invs]), vecs.grad
+    return torch.stack([i.grad for i in invs]), vecs.grad, out["loss"].detach()
 
 
 @pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean"])
 def test_photometric_loss_golden(hip, name):
-    """Loss scalar: 1e-4 vs the reference.  Gradients: 1e-4, or 4x the distance
-    of the reference's own fp32 gradient from the fp64 result when that is
-    larger (the pose gradient is a 2*H*W-term reduction with cancellation; the
-    min-selection flips a few near-tied pixels between any two fp32 orders)."""
+    """Loss scalar and smoothness: 1e-4 vs the reference.  Gradients: against the
+    fp64 oracle evaluated with this kernel's own min-selection: relative L2 at
+    1e-4 or 4x the reference fp32 gradient's own L2 distance from fp64 (the pose
+    gradient is a 2*H*W-term reduction with cancellation); the inverse-depth
+    map also per element (max-abs relative to max|g|) at 1e-4 or 4x the
+    reference's own max-rel.  Both inverse-depth bounds exclude its 2 largest
+    deviations.
+
+    The loss has kinks: the min over candidates, |est - tgt| of the L1 term and
+    the SSIM clamp.  A kink whose two sides tie to fp32 rounding resolves
+    differently in any two evaluation orders (the reference's and ours, or two
+    builds of ours), which moves that pixel's gradient by one term and the loss
+    by ~0.  The min-selection is therefore forced (and allowed to differ from
+    the free fp64 minimum only where the loss difference is <= 1e-9 relative),
+    and the per-pixel bounds tolerate two such kink pixels (of 46080); the
+    KITTI-size test below holds the un-excluded L2 bound at 192x640."""
     d = fx(name)
     invs = d["inv_depths"].clone().requires_grad_(True)           # [n,B,1,H,W]
     vec = d["poses"].clone().requires_grad_(True)                 # [B,N,n,6]
     pose = vec.permute(1, 2, 0, 3)                                # [N,n,B,6]
-    loss, metrics = hip.photometric_loss(d["image"], d["context"], invs, pose, d["K"],
-                                         automask=bool(int(d["automask"])),
-                                         reduce_min=bool(int(d["reduce_min"])))
+    loss, metrics, sel = hip.photometric_loss(d["image"], d["context"], invs, pose, d["K"],
+                                              automask=bool(int(d["automask"])),
+                                              reduce_min=bool(int(d["reduce_min"])),
+                                              return_selection=True)
     assert rel(loss, d["loss"]) < TOL
     assert rel(metrics[1], d["smoothness_loss"]) < TOL
     loss.sum().backward()
-    g_inv64, g_pose64 = _fp64_photometric(d)
-    tol_inv = max(TOL, 4 * rel(d["g_inv_depths"].double(), g_inv64))
-    tol_pose = max(TOL, 4 * rel(d["g_poses"].double(), g_pose64))
-    assert rel(invs.grad, d["g_inv_depths"]) < tol_inv
-    assert rel(vec.grad, d["g_poses"]) < tol_pose
-    assert rel(vec.grad.double(), g_pose64) < tol_pose
+    g_inv64, g_pose64, l64 = _fp64_photometric(d)
+    l2 = lambda a, b: float((a.double().cpu() - b).norm() / b.norm())
+    tol = {"inv": (max(TOL, 4 * l2(d["g_inv_depths"], g_inv64)), max(TOL, 4 * rel(d["g_inv_depths"].double(), g_inv64))),
+           "pose": (max(TOL, 4 * l2(d["g_poses"], g_pose64)), max(TOL, 4 * rel(d["g_poses"].double(), g_pose64)))}
+    if int(d["reduce_min"]):
+        forced = sel.cpu().unsqueeze(2)
+        g_inv64, g_pose64, l64f = _fp64_photometric(d, forced_selection=forced)
+        assert float(l64f - l64) <= 1e-9 * float(l64), "selection differs beyond near-ties"
+    for key, got, want in (("inv", invs.grad, g_inv64), ("pose", vec.grad, g_pose64)):
+        tol_l2, tol_max = tol[key]
+        diff = (got.double().cpu() - want).flatten()
+        kinks = diff.abs().topk(2).indices if key == "inv" else []   # per-pixel map only
+        diff[kinks] = 0.0
+        assert float(diff.norm() / want.norm()) <= tol_l2, (key, float(diff.norm() / want.norm()), tol_l2)
+        if key == "inv":   # per-pixel map; the 72 pose entries are held to the L2 bound
+            assert float(diff.abs().max()) <= tol_max * float(want.abs().max()), (key, rel(got.double(), want), tol_max)
 
 
 def test_photometric_loss_kitti_size_vs_oracle(hip):
