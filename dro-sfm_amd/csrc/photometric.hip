@@ -248,6 +248,25 @@ __global__ __launch_bounds__(kThreads) void photo_automask_kernel(PhotoArgs a) {
   }
 }
 
+// XCD-aware block order.  Workgroups are dispatched round-robin over the 8
+// XCDs (linear id % 8), each with its own 4 MB L2.  With the natural order
+// every XCD sees every tile of every (prediction, batch) and the context
+// images all n predictions gather from (2 refs x B x 1.5 MB at 192x640) miss
+// its L2.  When the tile count divides by 8, XCD x gets a contiguous band of
+// tile rows for all (i, b) instead: the band's context rows are gathered by
+// n predictions from one L2.  (1-D grid of tiles * planes blocks.)
+__device__ __forceinline__ void block_tile(const PhotoArgs& a, int& tile, int& plane) {
+  const int L = blockIdx.x, tiles = a.tiles_x * a.tiles_y;
+  if (tiles % 8 == 0) {
+    const int per = tiles / 8, x = L % 8, k = L / 8;
+    tile = x * per + k % per;
+    plane = k / per;
+  } else {
+    tile = L % tiles;
+    plane = L / tiles;
+  }
+}
+
 // ------------------------------------------------------------------ forward tile kernel
 __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
   constexpr int PL = H1 * W1;
@@ -256,9 +275,10 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
   __shared__ float invt[PL];
   __shared__ float scratch[4 * (kThreads / kWave)];
 
-  const int ib = blockIdx.z, i = ib / a.B, b = ib % a.B;
-  const int tile = blockIdx.y * a.tiles_x + blockIdx.x;
-  const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+  int tile, ib;
+  block_tile(a, tile, ib);
+  const int i = ib / a.B, b = ib % a.B;
+  const int y0 = (tile / a.tiles_x) * TH, x0 = (tile % a.tiles_x) * TW;
   const int H = a.H, W = a.W;
   const size_t HW = (size_t)H * W;
   const float* img = a.image + (size_t)b * 3 * HW;
@@ -442,9 +462,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
   __shared__ float invt[PL2];
   __shared__ float scratch[12 * (kThreads / kWave)];
 
-  const int ib = blockIdx.z, i = ib / a.B, b = ib % a.B;
-  const int tile = blockIdx.y * a.tiles_x + blockIdx.x;
-  const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+  int tile, ib;
+  block_tile(a, tile, ib);
+  const int i = ib / a.B, b = ib % a.B;
+  const int y0 = (tile / a.tiles_x) * TH, x0 = (tile % a.tiles_x) * TW;
   const int H = a.H, W = a.W;
   const size_t HW = (size_t)H * W;
   const float* img = a.image + (size_t)b * 3 * HW;
@@ -785,7 +806,7 @@ extern "C" int dro_photometric_forward(const float* image, const float* context,
     hipLaunchKernelGGL(photo_automask_kernel, dim3(a.tiles_x, a.tiles_y, N * B), dim3(kThreads), 0, s, a);
     if ((st = launch_status("photo_automask_kernel launch failed"))) return st;
   }
-  hipLaunchKernelGGL(photo_fwd_kernel, dim3(a.tiles_x, a.tiles_y, n * B), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(photo_fwd_kernel, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a);
   if ((st = launch_status("photo_fwd_kernel launch failed"))) return st;
   hipLaunchKernelGGL(photo_finalize_kernel, dim3(1), dim3(1024), 0, s, a, out);
   return launch_status("photo_finalize_kernel launch failed");
@@ -808,7 +829,7 @@ extern "C" int dro_photometric_backward(const float* image, const float* context
   }
   if (!grad_pose) a.part_pose = nullptr;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(photo_bwd_kernel, dim3(a.tiles_x, a.tiles_y, n * B), dim3(kThreads), 0, s, a,
+  hipLaunchKernelGGL(photo_bwd_kernel, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a,
                      grad_out, grad_inv_depths);
   if ((st = launch_status("photo_bwd_kernel launch failed"))) return st;
   if (grad_pose) {
