@@ -154,9 +154,19 @@ def roofline_photometric(B, device, iters=20):
     bwd_bytes = HW * B * (12 + 12 * NREF) + HW * B * n * 9
     total_bytes = fwd_bytes + bwd_bytes
     achieved = total_bytes / ((fwd_ms + bwd_ms) * 1e-3) / 1e9
+    # HBM bytes of a call pair at this shape from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over
+    # tools/bench_photo.py (profiles/r2_photometric_counters.json, FETCH_SIZE x2 for gfx950)
+    traffic = None
+    pf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2_photometric_counters.json")
+    if os.path.exists(pf) and n == 9 and (H, W) == (192, 640) and B == 2:
+        pc = json.load(open(pf))
+        traffic = int(sum(v["hbm_fetch_bytes_corrected"] for v in pc["xcd_band_order"].values())
+                      + sum(pc["write_bytes_per_call"].values()))
     return {"bound": "hbm", "kernel": "photometric fwd+bwd (photo_fwd_kernel + photo_bwd_kernel)",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "note": "latency-bound, not HBM-bound: VALU issue ~16% of the chip, ~49% of wave cycles "
+                    "waiting (profiles/r2_photometric_counters.json)",
             "algorithmic_bytes": int(total_bytes), "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)}
 
 
