@@ -54,6 +54,12 @@ def load():
     _sig(lib.dro_bilinear_upsample2x_backward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_maxpool3x3s2_forward, P, ctypes.c_longlong, I, I, P, P, S)
     _sig(lib.dro_maxpool3x3s2_backward, P, P, ctypes.c_longlong, I, I, P, S)
+    _sig(lib.dro_depth_metrics_blocks, I, I)
+    _sig(lib.dro_depth_metrics_workspace_bytes, I, restype=Z)
+    _sig(lib.dro_depth_metrics_prepare, P, P, I, I, I, I, I, F, F, I, I, I, I, P, P, P, S)
+    _sig(lib.dro_depth_metrics_reduce, P, P, P, I, I, I, F, F, I, I, I, I, P, P, S)
+    _sig(lib.dro_depth_metrics_median_workspace_bytes, I, restype=Z)
+    _sig(lib.dro_depth_metrics_median, P, P, I, I, I, P, P, S)
     _sig(lib.dro_batchnorm_workspace_bytes, I, I, I, restype=Z)
     _sig(lib.dro_batchnorm_relu_forward, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P, P, P, Z, S)
     _sig(lib.dro_batchnorm_relu_backward, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, Z, S)
@@ -84,6 +90,8 @@ EXPORTED = (
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
     "dro_maxpool3x3s2_forward", "dro_maxpool3x3s2_backward",
+    "dro_depth_metrics_blocks", "dro_depth_metrics_workspace_bytes", "dro_depth_metrics_prepare",
+    "dro_depth_metrics_reduce", "dro_depth_metrics_median_workspace_bytes", "dro_depth_metrics_median",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv2d_forward", "dro_convgru_gates_forward",

@@ -472,6 +472,58 @@ def maxpool3x3s2(x):
     return _MaxPool3s2.apply(x)
 
 
+# ------------------------------------------------------------------ depth evaluation metrics
+def crop_rect(crop, H, W):
+    """Crop rectangle (y1, y2, x1, x2) of compute_depth_metrics
+    (dro_sfm/utils/depth.py:287-298): 'garg' (KITTI, fractions of the gt size,
+    Python float products truncated by int()), 'eigen_nyu' (fixed), else none."""
+    if crop == "garg":
+        return (int(0.40810811 * H), int(0.99189189 * H), int(0.03594771 * W), int(0.96405229 * W))
+    if crop == "eigen_nyu":
+        return (20, 459, 24, 615)
+    return (-1, -1, -1, -1)
+
+
+def depth_metrics(gt, pred, min_depth, max_depth, crop="", use_gt_scale=True):
+    """compute_depth_metrics (dro_sfm/utils/depth.py:259-343) on the GPU.
+
+    gt [B,1,H,W], pred [B,1,h,w] depths (float32).  Returns a float32 tensor [9]:
+    abs_rel, sq_rel, rmse, rmse_log, a1, a2, a3, SILog, iabs_diff (batch means).
+    One prepare pass (upsample, validity, ratios), the per-image median of the
+    valid gt/pred ratios by an on-device radix select (the reference's
+    torch.median: the lower middle element), one reduce pass.  No host
+    synchronisation (the reference synchronises per image)."""
+    lib = _lib.load()
+    require_device(gt, pred, what="depth_metrics")
+    if gt.dim() != 4 or pred.dim() != 4 or gt.shape[1] != 1 or pred.shape[1] != 1 or gt.shape[0] != pred.shape[0]:
+        raise RuntimeError("depth_metrics: gt [B,1,H,W] and pred [B,1,h,w] expected")
+    B, _, H, W = gt.shape
+    h, w = pred.shape[-2:]
+    y1, y2, x1, x2 = crop_rect(crop, H, W)
+    gt, pred = gt.contiguous(), pred.contiguous()
+    nblk = lib.dro_depth_metrics_blocks(H, W)
+    pred_up = torch.empty(B, H * W, device=gt.device, dtype=torch.float32)
+    ratio = torch.empty_like(pred_up)
+    counts = torch.empty(B, nblk, device=gt.device, dtype=torch.int32)
+    st = stream_of(gt)
+    check(lib.dro_depth_metrics_prepare(ptr(gt), ptr(pred), B, H, W, h, w, float(min_depth), float(max_depth),
+                                        y1, y2, x1, x2, ptr(pred_up), ptr(ratio), ptr(counts), st),
+          "dro_depth_metrics_prepare")
+    scale = None
+    if use_gt_scale:
+        scale = torch.empty(B, device=gt.device, dtype=torch.float32)
+        mws = torch.empty(lib.dro_depth_metrics_median_workspace_bytes(B) // 4 + 1, device=gt.device,
+                          dtype=torch.int32)
+        check(lib.dro_depth_metrics_median(ptr(ratio), ptr(counts), B, H, W, ptr(scale), ptr(mws), st),
+              "dro_depth_metrics_median")
+    ws = torch.empty(lib.dro_depth_metrics_workspace_bytes(B) // 8 + 1, device=gt.device, dtype=torch.float64)
+    out = torch.empty(9, device=gt.device, dtype=torch.float32)
+    check(lib.dro_depth_metrics_reduce(ptr(gt), ptr(pred_up), ptr(scale), B, H, W, float(min_depth),
+                                       float(max_depth), y1, y2, x1, x2, ptr(out), ptr(ws), st),
+          "dro_depth_metrics_reduce")
+    return out
+
+
 class _BatchNormAct(torch.autograd.Function):
     """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
 

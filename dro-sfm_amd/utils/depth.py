@@ -24,3 +24,14 @@ def disp_to_depth(disp, min_depth, max_depth):
     lo, hi = 1.0 / max_depth, 1.0 / min_depth
     scaled = lo + (hi - lo) * disp
     return scaled, 1.0 / scaled
+
+
+def compute_depth_metrics(config, gt, pred, use_gt_scale=True):
+    """compute_depth_metrics (dro_sfm/utils/depth.py:259-343 of the reference),
+    same signature and return value: a tensor [9] of abs_rel, sq_rel, rmse,
+    rmse_log, a1, a2, a3, SILog, iabs_diff averaged over the batch.  `config`
+    needs .crop ('garg', 'eigen_nyu' or other), .min_depth and .max_depth.
+    Computed by the HIP metrics kernels (csrc/metrics.hip); GPU tensors only."""
+    from .. import hip
+    return hip.depth_metrics(gt, pred, config.min_depth, config.max_depth, crop=config.crop,
+                             use_gt_scale=use_gt_scale).type_as(gt)

@@ -189,6 +189,32 @@ int dro_maxpool3x3s2_forward(const float* x, long long planes, int H, int W, flo
 int dro_maxpool3x3s2_backward(const float* grad_y, const unsigned char* argmax,
                               long long planes, int H, int W, float* grad_x, void* stream);
 
+/* Depth evaluation metrics (compute_depth_metrics, dro_sfm/utils/depth.py:259-343
+ * of the reference).  gt [B,1,H,W] metric depth, pred [B,1,h,w] predicted depth.
+ * prepare: pred_up [B,H,W] = max(bilinear(pred, align_corners=True), 1e-6),
+ *   ratio [B,H,W] = gt / pred_up where valid (min < gt < max, inside the crop
+ *   rectangle [y1,y2) x [x1,x2) unless y1 < 0) and +inf elsewhere, and
+ *   block_counts [B, dro_depth_metrics_blocks(H,W)] valid pixels per block.
+ * reduce: with scale [B] (the per-image median of the valid ratios; NULL = no
+ *   ground-truth scaling) writes metrics[9] = batch means of abs_rel, sq_rel,
+ *   rmse, rmse_log, a1, a2, a3, SILog, iabs_diff.  Per-pixel terms in fp32 as
+ *   the reference writes them, sums in fp64 in a fixed order (deterministic). */
+int dro_depth_metrics_blocks(int H, int W);
+size_t dro_depth_metrics_workspace_bytes(int B);
+int dro_depth_metrics_prepare(const float* gt, const float* pred, int B, int H, int W, int h, int w,
+                              float min_depth, float max_depth, int crop_y1, int crop_y2,
+                              int crop_x1, int crop_x2, float* pred_up, float* ratio,
+                              int* block_counts, void* stream);
+/* median: scale[b] = the ((n_b - 1) / 2)-th smallest valid ratio of image b
+ * (torch.median's lower middle element; 1 when n_b = 0), by a 4-pass radix
+ * select on the device (no host round trip). */
+size_t dro_depth_metrics_median_workspace_bytes(int B);
+int dro_depth_metrics_median(const float* ratio, const int* block_counts, int B, int H, int W,
+                             float* scale, void* workspace, void* stream);
+int dro_depth_metrics_reduce(const float* gt, const float* pred_up, const float* scale, int B, int H,
+                             int W, float min_depth, float max_depth, int crop_y1, int crop_y2,
+                             int crop_x1, int crop_x2, float* metrics, void* workspace, void* stream);
+
 /* Training-mode BatchNorm2d fused with the ReLU / residual add that follows it
  * in the ResNet-18 encoders (networks/optim/extractor.py:7-107 of the reference;
  * BasicBlock: relu(bn(conv(x)) [+ skip])).  Replaces torch.nn.functional.

@@ -432,6 +432,48 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
                                       max_depth)
 
 
+# ============================================================================ evaluation
+def depth_metrics(gt, pred, min_depth, max_depth, crop="", use_gt_scale=True):
+    """compute_depth_metrics (utils/depth.py:259-343): per image, valid pixels
+    (min < gt < max, garg / eigen_nyu crop :287-298), optional median scaling
+    (:313-315), then the nine metrics (:320-341) averaged over the batch."""
+    B, _, H, W = gt.shape
+    if pred.shape[-2:] != gt.shape[-2:]:                            # interpolate_image (image.py:166-196)
+        pred = F.interpolate(pred, size=(H, W), mode="bilinear", align_corners=True)
+    pred = pred.clamp(min=1e-6)
+    crop_mask = None
+    if crop == "garg":
+        crop_mask = torch.zeros(H, W, dtype=torch.bool, device=gt.device)
+        crop_mask[int(0.40810811 * H):int(0.99189189 * H), int(0.03594771 * W):int(0.96405229 * W)] = True
+    elif crop == "eigen_nyu":
+        crop_mask = torch.zeros(H, W, dtype=torch.bool, device=gt.device)
+        crop_mask[20:459, 24:615] = True
+    acc = [0.0] * 9
+    for pred_i, gt_i in zip(pred, gt):
+        gt_i, pred_i = gt_i.squeeze(), pred_i.squeeze()
+        valid = (gt_i > min_depth) & (gt_i < max_depth)
+        if crop_mask is not None:
+            valid = valid & crop_mask
+        if valid.sum() == 0:
+            continue
+        gt_i, pred_i = gt_i[valid], pred_i[valid]
+        if use_gt_scale:
+            pred_i = pred_i * torch.median(gt_i / pred_i)
+            pred_i = pred_i.clamp(min_depth, max_depth)
+        pred_i = pred_i.clamp(min_depth, max_depth)
+        thresh = torch.max(gt_i / pred_i, pred_i / gt_i)
+        diff = gt_i - pred_i
+        d = gt_i.log() - pred_i.log()
+        vals = [torch.mean(diff.abs() / gt_i), torch.mean(diff ** 2 / gt_i), torch.sqrt(torch.mean(diff ** 2)),
+                torch.sqrt(torch.mean((gt_i.log() - pred_i.log()) ** 2)),
+                (thresh < 1.25).to(gt.dtype).mean(), (thresh < 1.25 ** 2).to(gt.dtype).mean(),
+                (thresh < 1.25 ** 3).to(gt.dtype).mean(),
+                ((d ** 2).mean() - d.sum() ** 2 / len(d) ** 2) ** 0.5,
+                torch.mean((1.0 / pred_i - 1.0 / gt_i).abs())]
+        acc = [a + v for a, v in zip(acc, vals)]
+    return torch.tensor([float(a) / B for a in acc], dtype=gt.dtype)
+
+
 def rel_err(a, b):
     """max |a-b| / max(|b|) -- the relative metric the parity tests quote."""
     a, b = a.detach().double(), b.detach().double()

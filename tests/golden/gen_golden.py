@@ -469,6 +469,31 @@ def gen_full():
              **{"metric_" + k: v for k, v in out["metrics"].items()}, **grad_checksums(net2, None))
 
 
+def gen_metrics():
+    """compute_depth_metrics (utils/depth.py:259-343) on LiDAR-like sparse ground
+    truth: garg crop with a lower-resolution prediction, and no crop with a
+    same-resolution prediction; the last image of each batch has no valid pixel."""
+    from types import SimpleNamespace
+    from dro_sfm.utils.depth import compute_depth_metrics
+    g = torch.Generator().manual_seed(77)
+    for name, crop, (H, W), (h, w), lo, hi in (("metrics_garg", "garg", (96, 320), (48, 160), 1e-3, 80.0),
+                                               ("metrics_nocrop", "", (64, 96), (64, 96), 0.2, 10.0)):
+        B = 3
+        gt = torch.zeros(B, 1, H, W)
+        keep = torch.rand(B, 1, H, W, generator=g) < 0.3
+        gt[keep] = (lo + 1.0 + (hi - lo - 1.0) * torch.rand(B, 1, H, W, generator=g))[keep]
+        gt[-1] = 0.0                                                   # empty image
+        base = torch.nn.functional.interpolate(torch.rand(B, 1, 6, 10, generator=g), size=(h, w),
+                                               mode="bilinear", align_corners=False)
+        pred = (0.5 + (hi / 2) * base) * (1.0 + 0.05 * torch.randn(B, 1, h, w, generator=g))
+        cfg = SimpleNamespace(crop=crop, min_depth=lo, max_depth=hi)
+        out_s = compute_depth_metrics(cfg, gt, pred, use_gt_scale=True)
+        out_u = compute_depth_metrics(cfg, gt, pred, use_gt_scale=False)
+        save(name, gt=gt, pred=pred, metrics_scaled=out_s, metrics_unscaled=out_u,
+             min_depth=torch.tensor(lo), max_depth=torch.tensor(hi),
+             crop=np.array({"": 0, "garg": 1, "eigen_nyu": 2}[crop], dtype=np.int32))
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: golden fixtures can only be regenerated in the build container")
@@ -483,3 +508,5 @@ if __name__ == "__main__":
         gen_network_parts()
     if "full" in which:
         gen_full()
+    if "metrics" in which:
+        gen_metrics()

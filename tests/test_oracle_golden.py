@@ -225,3 +225,15 @@ def test_train_step(tag, version, kind):
             ref = d[key]
             worst = max(worst, abs(float(v.grad.double().sum()) - float(ref[0])) / (float(ref[1]) + 1e-12))
     assert worst < 1e-3
+
+
+@pytest.mark.parametrize("name", ["metrics_garg", "metrics_nocrop"])
+@pytest.mark.parametrize("scaled", [True, False])
+def test_depth_metrics(name, scaled):
+    """compute_depth_metrics (utils/depth.py:259-343): the restatement reproduces
+    the reference's nine metrics bit for bit on sparse LiDAR-like ground truth
+    (garg crop + upsampled prediction; no crop; an image without valid pixels)."""
+    d = load_fixture(os.path.join(G, name + ".npz"))
+    crop = {0: "", 1: "garg", 2: "eigen_nyu"}[int(d["crop"])]
+    out = O.depth_metrics(d["gt"], d["pred"], float(d["min_depth"]), float(d["max_depth"]), crop, scaled)
+    assert torch.equal(out, d["metrics_scaled" if scaled else "metrics_unscaled"])
