@@ -215,6 +215,17 @@ int dro_depth_metrics_reduce(const float* gt, const float* pred_up, const float*
                              int W, float min_depth, float max_depth, int crop_y1, int crop_y2,
                              int crop_x1, int crop_x2, float* metrics, void* workspace, void* stream);
 
+/* Resize + ToTensor of decoded uint8 RGB frames, bit-identical to Pillow's
+ * BILINEAR resampling (torchvision Resize on PIL images, datasets/
+ * augmentations.py:69-111, then ToTensor :149-160 of the reference).
+ * src [N, H0, W0, 3] uint8 -> dst [N, 3, H, W] float32 (value / 255).
+ * xbounds [W][2] / ybounds [H][2] = (first input index, tap count) and
+ * xcoef [W][KX] / ycoef [H][KY] = Pillow's 22-bit fixed-point weights per
+ * output column / row; tmp [N, H0, W, 3] uint8 holds the horizontal pass. */
+int dro_resize_rgb8_to_tensor(const unsigned char* src, int N, int H0, int W0, int H, int W,
+                              const int* xbounds, const int* xcoef, int KX, const int* ybounds,
+                              const int* ycoef, int KY, unsigned char* tmp, float* dst, void* stream);
+
 /* Training-mode BatchNorm2d fused with the ReLU / residual add that follows it
  * in the ResNet-18 encoders (networks/optim/extractor.py:7-107 of the reference;
  * BasicBlock: relu(bn(conv(x)) [+ skip])).  Replaces torch.nn.functional.

@@ -474,6 +474,42 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="", use_gt_scale=True):
     return torch.tensor([float(a) / B for a in acc], dtype=gt.dtype)
 
 
+# ============================================================================ data pipeline
+def resize_bilinear_pil(a, H, W):
+    """Pillow's Image.resize((W, H), BILINEAR) of a uint8 HWC array, as
+    torchvision Resize calls it in resize_sample_image_and_intrinsics
+    (datasets/augmentations.py:69-111).  Pillow (not in /root/reference; 12.2
+    here) Resample.c: triangle filter of support max(in/out, 1), double
+    weights normalised per output then rounded to 22-bit fixed point, a
+    horizontal pass into a uint8 image, then a vertical pass; each output =
+    clip8((2^21 + sum w*x) >> 22).  Pinned bit-exactly against PIL itself
+    (tests/test_oracle_golden.py::test_resize_matches_pillow)."""
+    import numpy as np
+    prec = 22
+
+    def one_pass(img, axis, out_size):
+        in_size = img.shape[axis]
+        scale = in_size / out_size
+        filterscale = max(scale, 1.0)
+        ss = 1.0 / filterscale
+        img = np.moveaxis(img, axis, 0).astype(np.int64)
+        out = np.empty((out_size,) + img.shape[1:], np.int64)
+        for o in range(out_size):
+            center = (o + 0.5) * scale
+            xmin = max(int(center - filterscale + 0.5), 0)
+            n = min(int(center + filterscale + 0.5), in_size) - xmin
+            w = [max(0.0, 1.0 - abs((x + xmin - center + 0.5) * ss)) for x in range(n)]
+            tot = sum(w)
+            w = [v / tot for v in w] if tot else w
+            acc = np.full(img.shape[1:], 1 << (prec - 1), np.int64)
+            for x in range(n):
+                acc += int(w[x] * (1 << prec) + (0.5 if w[x] >= 0 else -0.5)) * img[xmin + x]
+            out[o] = np.clip(acc >> prec, 0, 255)
+        return np.moveaxis(out, 0, axis).astype(np.uint8)
+
+    return one_pass(one_pass(a, 1, W), 0, H)
+
+
 def rel_err(a, b):
     """max |a-b| / max(|b|) -- the relative metric the parity tests quote."""
     a, b = a.detach().double(), b.detach().double()

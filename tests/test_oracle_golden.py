@@ -237,3 +237,15 @@ def test_depth_metrics(name, scaled):
     crop = {0: "", 1: "garg", 2: "eigen_nyu"}[int(d["crop"])]
     out = O.depth_metrics(d["gt"], d["pred"], float(d["min_depth"]), float(d["max_depth"]), crop, scaled)
     assert torch.equal(out, d["metrics_scaled" if scaled else "metrics_unscaled"])
+
+
+@pytest.mark.parametrize("shape", [((375, 1242), (192, 640)), ((480, 640), (240, 320)), ((50, 40), (96, 81))])
+def test_resize_matches_pillow(shape):
+    """The Pillow BILINEAR restatement (the reference's Resize on PIL frames,
+    datasets/augmentations.py:69-111) reproduces PIL itself bit for bit."""
+    import numpy as np
+    from PIL import Image
+    (h0, w0), (H, W) = shape
+    a = np.random.default_rng(h0).integers(0, 256, (h0, w0, 3), dtype=np.uint8)
+    want = np.asarray(Image.fromarray(a).resize((W, H), Image.BILINEAR))
+    assert np.array_equal(O.resize_bilinear_pil(a, H, W), want)

@@ -1,0 +1,52 @@
+"""GPU resize + ToTensor of KITTI frames (csrc/resize.hip) against the
+reference's CPU path: PIL BILINEAR resize + ToTensor per frame (what each
+data-loader worker does, datasets/augmentations.py:69-160).  One training
+step's frames at the metric config: B=2 targets + 2x2 context = 6 frames,
+375x1242 -> 192x640.  usage: python tools/bench_resize.py [--iters 50]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from PIL import Image  # noqa: E402
+
+from dro_sfm_amd.datasets.gpu_transforms import resize_to_tensor  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    N, h0, w0, H, W = 6, 375, 1242, 192, 640
+    frames = np.random.default_rng(0).integers(0, 256, (N, h0, w0, 3), dtype=np.uint8)
+    fd = torch.from_numpy(frames).cuda()
+    resize_to_tensor(fd, (H, W))
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        out = resize_to_tensor(fd, (H, W))
+    e1.record()
+    torch.cuda.synchronize()
+    gpu_ms = e0.elapsed_time(e1) / args.iters
+    pil = [Image.fromarray(f) for f in frames]
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        ref = [torch.from_numpy(np.asarray(p.resize((W, H), Image.BILINEAR)).copy()).permute(2, 0, 1).float().div(255)
+               for p in pil]
+    cpu_ms = 1e3 * (time.perf_counter() - t0) / reps
+    same = all(torch.equal(out[i].cpu(), ref[i]) for i in range(N))
+    mb = (N * h0 * w0 * 3 + 2 * N * h0 * W * 3 + N * 3 * H * W * 4) / 1e6
+    print(f"resize+to_tensor {N} frames {h0}x{w0} -> {H}x{W}: gpu {gpu_ms * 1e3:.1f} us "
+          f"({mb / gpu_ms:.0f} GB/s algorithmic over {mb:.1f} MB), PIL on 1 CPU thread {cpu_ms:.2f} ms; "
+          f"bit-identical: {same}")
+
+
+if __name__ == "__main__":
+    main()
