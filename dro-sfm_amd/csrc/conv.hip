@@ -973,19 +973,20 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits)
 }
 
 // G = alpha * dout * act'(y) (only when act != none or alpha != 1)
-__global__ __launch_bounds__(256) void grad_pre_kernel(int act, float alpha, int Cout, size_t HW,
-                                                       size_t total, const float* __restrict__ dout,
+// grid (pixel blocks, B * Cout planes): no 64-bit division per element
+__global__ __launch_bounds__(256) void grad_pre_kernel(int act, float alpha, int Cout, int HW,
+                                                       const float* __restrict__ dout,
                                                        Slice y, float* __restrict__ G) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    float d = alpha * dout[i];
-    if (act) {
-      const size_t b = i / ((size_t)Cout * HW), rem = i - b * Cout * HW;
-      const size_t o = rem / HW, pix = rem - o * HW;
-      d *= act_bwd(y.p[(b * y.ctot + y.coff + o) * HW + pix], act);
-    }
-    G[i] = d;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= HW) return;
+  const int plane = blockIdx.y;                 // b * Cout + o (wave-uniform)
+  const size_t i = (size_t)plane * HW + pix;
+  float d = alpha * dout[i];
+  if (act) {
+    const int b = plane / Cout, o = plane - b * Cout;
+    d *= act_bwd(y.p[((size_t)b * y.ctot + y.coff + o) * HW + pix], act);
   }
+  G[i] = d;
 }
 
 }  // namespace dro
@@ -1744,12 +1745,13 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   a.galpha = fold ? alpha : 1.f;
   a.gy = (fold && act) ? y->data : nullptr;
   if (pre && !fold) {
-    const size_t total = (size_t)Cout * P;
-    size_t blocks = (total + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
+    if ((long long)B * Cout > 65535 || HW >= ((size_t)1 << 31)) {
+      set_error("conv2d_backward: B * Cout or H * W out of range for the gradient pre-pass");
+      return DRO_E_SHAPE;
+    }
     float* G = reinterpret_cast<float*>(ws_pre);
-    hipLaunchKernelGGL(grad_pre_kernel, dim3((unsigned)blocks), dim3(256), 0, s, act, alpha, Cout, HW,
-                       total, dout, to_slice(y), G);
+    hipLaunchKernelGGL(grad_pre_kernel, dim3((unsigned)((HW + 255) / 256), (unsigned)(B * Cout)), dim3(256), 0, s,
+                       act, alpha, Cout, (int)HW, dout, to_slice(y), G);
     if ((st = launch_status("grad_pre_kernel launch failed"))) return st;
     a.G = G;
   } else {
@@ -1928,7 +1930,8 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
 // stage 2 (after the q-gate backward, drh = dL/d(r*h)):  dr~ = drh h r (1-r);  dh += drh r
 // z = zr[:, :hd], r = zr[:, hd:], dz~ / dr~ written into dzr likewise.
 namespace dro {
-__global__ __launch_bounds__(256) void gru_elem_kernel(int stage, int hd, size_t HW, size_t total,
+// grid (pixel blocks over hd * HW, B): no 64-bit division per element
+__global__ __launch_bounds__(256) void gru_elem_kernel(int stage, int hd, int HW,
                                                        const float* __restrict__ dhn,
                                                        const float* __restrict__ zr,
                                                        const float* __restrict__ q,
@@ -1937,20 +1940,21 @@ __global__ __launch_bounds__(256) void gru_elem_kernel(int stage, int hd, size_t
                                                        float* __restrict__ dq,
                                                        float* __restrict__ dzr,
                                                        float* __restrict__ dh) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const size_t b = i / ((size_t)hd * HW), rem = i - b * hd * HW;
-    const size_t zi = b * 2 * hd * HW + rem, ri = zi + (size_t)hd * HW;
-    if (stage == 1) {
-      const float gn = dhn[i], z = zr[zi], qv = q[i], hv = h[i];
-      dq[i] = gn * z * (1.f - qv * qv);
-      dzr[zi] = gn * (qv - hv) * z * (1.f - z);
-      dh[i] = gn * (1.f - z);
-    } else {
-      const float d = drh[i], r = zr[ri];
-      dzr[ri] = d * h[i] * r * (1.f - r);
-      dh[i] += d * r;
-    }
+  const int n = hd * HW;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const size_t b = blockIdx.y;
+  const size_t i = b * n + j;
+  const size_t zi = b * 2 * n + j, ri = zi + n;
+  if (stage == 1) {
+    const float gn = dhn[i], z = zr[zi], qv = q[i], hv = h[i];
+    dq[i] = gn * z * (1.f - qv * qv);
+    dzr[zi] = gn * (qv - hv) * z * (1.f - z);
+    dh[i] = gn * (1.f - z);
+  } else {
+    const float d = drh[i], r = zr[ri];
+    dzr[ri] = d * h[i] * r * (1.f - r);
+    dh[i] += d * r;
   }
 }
 }  // namespace dro
@@ -1967,10 +1971,12 @@ extern "C" int dro_gru_backward_elem(int stage, int B, int hd, int H, int W, con
     set_error("gru_backward_elem: NULL pointer");
     return DRO_E_NULL;
   }
-  const size_t HW = (size_t)H * W, total = (size_t)B * hd * HW;
-  size_t blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(gru_elem_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                     stage, hd, HW, total, dhn, zr, q, h, drh, dq, dzr, dh);
+  if (B > 65535 || (long long)hd * H * W >= (1LL << 31)) {
+    set_error("gru_backward_elem: sizes out of range");
+    return DRO_E_SHAPE;
+  }
+  const int n = hd * H * W;
+  hipLaunchKernelGGL(gru_elem_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)B), dim3(256), 0,
+                     (hipStream_t)stream, stage, hd, H * W, dhn, zr, q, h, drh, dq, dzr, dh);
   return launch_status("gru_elem_kernel launch failed");
 }

@@ -22,17 +22,16 @@ namespace dro {
 
 constexpr int kPoolThreads = 256;
 
-__global__ __launch_bounds__(kPoolThreads) void maxpool3s2_fwd_kernel(const float* __restrict__ x,
-                                                                     long long planes, int H, int W,
+// grid (pixel blocks, planes): 32-bit pixel arithmetic inside a plane (64-bit
+// division/modulo by runtime sizes costs more than the memory traffic here)
+__global__ __launch_bounds__(kPoolThreads) void maxpool3s2_fwd_kernel(const float* __restrict__ x, int H, int W,
                                                                      int Ho, int Wo,
                                                                      float* __restrict__ y,
                                                                      unsigned char* __restrict__ idx) {
-  const long long o = (long long)blockIdx.x * kPoolThreads + threadIdx.x;
-  if (o >= planes * Ho * Wo) return;
-  const int ox = (int)(o % Wo);
-  const long long t = o / Wo;
-  const int oy = (int)(t % Ho);
-  const long long pl = t / Ho;
+  const int o = blockIdx.x * kPoolThreads + threadIdx.x;
+  if (o >= Ho * Wo) return;
+  const int oy = o / Wo, ox = o - oy * Wo;
+  const size_t pl = blockIdx.y;
   const float* __restrict__ p = x + pl * H * W;
   const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
   float m = -INFINITY;
@@ -45,7 +44,7 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool3s2_fwd_kernel(const floa
     for (int dx = 0; dx < 3; ++dx) {
       const int xx = x0 + dx;
       if (xx < 0 || xx >= W) continue;
-      const float v = p[(long long)yy * W + xx];
+      const float v = p[yy * W + xx];
       if (arg < 0) arg = dy * 3 + dx;   // ATen's initial index: the first in-range tap
       if (v > m || isnan(v)) {
         m = v;
@@ -53,21 +52,18 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool3s2_fwd_kernel(const floa
       }
     }
   }
-  y[o] = m;
-  idx[o] = (unsigned char)arg;
+  y[pl * Ho * Wo + o] = m;
+  idx[pl * Ho * Wo + o] = (unsigned char)arg;
 }
 
 __global__ __launch_bounds__(kPoolThreads) void maxpool3s2_bwd_kernel(const float* __restrict__ gy,
                                                                      const unsigned char* __restrict__ idx,
-                                                                     long long planes, int H, int W,
-                                                                     int Ho, int Wo,
+                                                                     int H, int W, int Ho, int Wo,
                                                                      float* __restrict__ gx) {
-  const long long i = (long long)blockIdx.x * kPoolThreads + threadIdx.x;
-  if (i >= planes * H * W) return;
-  const int xx = (int)(i % W);
-  const long long t = i / W;
-  const int yy = (int)(t % H);
-  const long long pl = t / H;
+  const int i = blockIdx.x * kPoolThreads + threadIdx.x;
+  if (i >= H * W) return;
+  const int yy = i / W, xx = i - yy * W;
+  const size_t pl = blockIdx.y;
   // windows oy with 2*oy-1 <= yy <= 2*oy+1 (ATen p_start / p_end for k3 s2 p1)
   const int ph0 = (yy + 1 < 3) ? 0 : (yy + 1 - 3) / 2 + 1, ph1 = min((yy + 1) / 2 + 1, Ho);
   const int pw0 = (xx + 1 < 3) ? 0 : (xx + 1 - 3) / 2 + 1, pw1 = min((xx + 1) / 2 + 1, Wo);
@@ -77,10 +73,10 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool3s2_bwd_kernel(const floa
   for (int ph = ph0; ph < ph1; ++ph)
     for (int pw = pw0; pw < pw1; ++pw) {
       const int code = (yy - 2 * ph + 1) * 3 + (xx - 2 * pw + 1);
-      const long long k = (long long)ph * Wo + pw;
+      const int k = ph * Wo + pw;
       if (id[k] == code) acc += g[k];
     }
-  gx[i] = acc;
+  gx[pl * H * W + i] = acc;
 }
 
 }  // namespace dro
@@ -92,7 +88,7 @@ static int pool_check(const void* a, const void* b, const void* c, long long pla
     set_error("maxpool3x3s2: NULL pointer");
     return DRO_E_NULL;
   }
-  if (planes < 1 || H < 1 || W < 1 || planes * (long long)H * W >= (1LL << 40)) {
+  if (planes < 1 || planes > 65535 || H < 1 || W < 1 || (long long)H * W >= (1LL << 30)) {
     set_error("maxpool3x3s2: sizes out of range");
     return DRO_E_SHAPE;
   }
@@ -104,9 +100,8 @@ extern "C" int dro_maxpool3x3s2_forward(const float* x, long long planes, int H,
   int st = pool_check(x, y, argmax, planes, H, W);
   if (st) return st;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  const long long total = planes * Ho * Wo;
-  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((unsigned)((total + kPoolThreads - 1) / kPoolThreads)),
-                     dim3(kPoolThreads), 0, (hipStream_t)stream, x, planes, H, W, Ho, Wo, y, argmax);
+  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((Ho * Wo + kPoolThreads - 1) / kPoolThreads, (unsigned)planes),
+                     dim3(kPoolThreads), 0, (hipStream_t)stream, x, H, W, Ho, Wo, y, argmax);
   return launch_status("maxpool3s2_fwd_kernel launch failed");
 }
 
@@ -116,9 +111,7 @@ extern "C" int dro_maxpool3x3s2_backward(const float* grad_y, const unsigned cha
   int st = pool_check(grad_y, argmax, grad_x, planes, H, W);
   if (st) return st;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  const long long total = planes * (long long)H * W;
-  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((unsigned)((total + kPoolThreads - 1) / kPoolThreads)),
-                     dim3(kPoolThreads), 0, (hipStream_t)stream, grad_y, argmax, planes, H, W, Ho, Wo,
-                     grad_x);
+  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((H * W + kPoolThreads - 1) / kPoolThreads, (unsigned)planes),
+                     dim3(kPoolThreads), 0, (hipStream_t)stream, grad_y, argmax, H, W, Ho, Wo, grad_x);
   return launch_status("maxpool3s2_bwd_kernel launch failed");
 }

@@ -126,22 +126,22 @@ __device__ __forceinline__ void bl2_src(int dst, int n, int& i0, int& i1, float&
   l1 = s - (float)i0;
 }
 
-__global__ __launch_bounds__(256) void bilinear2x_fwd_kernel(const float* __restrict__ x, long long planes,
-                                                            int h, int w, float* __restrict__ out) {
+// grid (pixel blocks, planes): 32-bit in-plane arithmetic (64-bit division by
+// runtime sizes dominated these launches)
+__global__ __launch_bounds__(256) void bilinear2x_fwd_kernel(const float* __restrict__ x, int h, int w,
+                                                            float* __restrict__ out) {
   const int H = 2 * h, W = 2 * w;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= planes * H * W) return;
-  const int X = (int)(idx % W);
-  const long long t = idx / W;
-  const int Y = (int)(t % H);
-  const long long pl = t / H;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= H * W) return;
+  const int Y = i / W, X = i - Y * W;
+  const size_t pl = blockIdx.y;
   int y0, y1, x0, x1;
   float ly, lx;
   bl2_src(Y, h, y0, y1, ly);
   bl2_src(X, w, x0, x1, lx);
   const float* p = x + pl * h * w;
   const float a = p[y0 * w + x0], b = p[y0 * w + x1], c = p[y1 * w + x0], d = p[y1 * w + x1];
-  out[idx] = (1.f - ly) * ((1.f - lx) * a + lx * b) + ly * ((1.f - lx) * c + lx * d);
+  out[pl * H * W + i] = (1.f - ly) * ((1.f - lx) * a + lx * b) + ly * ((1.f - lx) * c + lx * d);
 }
 
 // weight of input index i in the taps of output index dst
@@ -152,15 +152,13 @@ __device__ __forceinline__ float bl2_weight(int dst, int n, int i) {
   return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
 }
 
-__global__ __launch_bounds__(256) void bilinear2x_bwd_kernel(const float* __restrict__ gout, long long planes,
-                                                            int h, int w, float* __restrict__ gx) {
+__global__ __launch_bounds__(256) void bilinear2x_bwd_kernel(const float* __restrict__ gout, int h, int w,
+                                                            float* __restrict__ gx) {
   const int H = 2 * h, W = 2 * w;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= planes * h * w) return;
-  const int xi = (int)(idx % w);
-  const long long t = idx / w;
-  const int yi = (int)(t % h);
-  const long long pl = t / h;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= h * w) return;
+  const int yi = i / w, xi = i - yi * w;
+  const size_t pl = blockIdx.y;
   const float* g = gout + pl * H * W;
   float wx[4];
 #pragma unroll
@@ -170,19 +168,19 @@ __global__ __launch_bounds__(256) void bilinear2x_bwd_kernel(const float* __rest
   }
   float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int Y = 2 * yi - 1 + i;
+  for (int r = 0; r < 4; ++r) {
+    const int Y = 2 * yi - 1 + r;
     if (Y < 0 || Y >= H) continue;
     const float wy = bl2_weight(Y, h, yi);
-    float r = 0.f;
+    float q = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int X = 2 * xi - 1 + j;
-      if (wx[j] != 0.f) r += wx[j] * g[(long long)Y * W + X];
+      if (wx[j] != 0.f) q += wx[j] * g[Y * W + X];
     }
-    acc += wy * r;
+    acc += wy * q;
   }
-  gx[idx] = acc;
+  gx[pl * h * w + i] = acc;
 }
 
 }  // namespace dro
@@ -237,7 +235,7 @@ static int bl2_check(const float* a, const float* b, long long planes, int h, in
     set_error("bilinear_upsample2x: NULL pointer");
     return DRO_E_NULL;
   }
-  if (planes < 1 || h < 1 || w < 1 || planes * 4LL * h * w >= (1LL << 40)) {
+  if (planes < 1 || planes > 65535 || h < 1 || w < 1 || 4LL * h * w >= (1LL << 30)) {
     set_error("bilinear_upsample2x: sizes out of range");
     return DRO_E_SHAPE;
   }
@@ -248,9 +246,8 @@ extern "C" int dro_bilinear_upsample2x_forward(const float* x, long long planes,
                                                float* out, void* stream) {
   int st = bl2_check(x, out, planes, h, w);
   if (st) return st;
-  const long long total = planes * 4LL * h * w;
-  hipLaunchKernelGGL(bilinear2x_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, planes, h, w, out);
+  hipLaunchKernelGGL(bilinear2x_fwd_kernel, dim3((4 * h * w + 255) / 256, (unsigned)planes), dim3(256), 0,
+                     (hipStream_t)stream, x, h, w, out);
   return launch_status("bilinear2x_fwd_kernel launch failed");
 }
 
@@ -258,8 +255,7 @@ extern "C" int dro_bilinear_upsample2x_backward(const float* grad_out, long long
                                                 int w, float* grad_x, void* stream) {
   int st = bl2_check(grad_out, grad_x, planes, h, w);
   if (st) return st;
-  const long long total = planes * (long long)h * w;
-  hipLaunchKernelGGL(bilinear2x_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, grad_out, planes, h, w, grad_x);
+  hipLaunchKernelGGL(bilinear2x_bwd_kernel, dim3((h * w + 255) / 256, (unsigned)planes), dim3(256), 0,
+                     (hipStream_t)stream, grad_out, h, w, grad_x);
   return launch_status("bilinear2x_bwd_kernel launch failed");
 }
