@@ -7,10 +7,13 @@ intrinsics scaled by out/in), duplicate_sample (:186-211), colorjitter_sample
 (:213-258) and to_tensor_sample (:149-184).  At 8 GPUs x ~100 frames/s each
 the PIL resize of 375x1242 KITTI frames on the host becomes the bottleneck.
 Here decoded frames travel to the GPU as uint8 (a quarter of the float
-bytes) and csrc/resize.hip resamples them bit-identically to Pillow and
-writes the float CHW tensors directly.  Colour jittering stays out (the
-reference's yamls for the metric config train without it -- jittering is a
-data-loader option); decoding stays on the host.
+bytes) and csrc/resize.hip resamples them bit-identically to Pillow, applies
+torchvision's ColorJitter (the reference default jittering = (0.2, 0.2, 0.2,
+0.05), configs/default_config.py:145) bit-identically to Pillow's
+ImageEnhance / HSV arithmetic, and writes the float CHW tensors.  The
+jitter's random order and factors are drawn on the host from torch's global
+generator in torchvision's get_params order, one draw per frame as the
+reference's per-image transform call.  Decoding stays on the host.
 """
 import ctypes
 from functools import lru_cache
@@ -104,5 +107,102 @@ def resize_sample_to_tensor(sample, shape):
         K = sample["intrinsics"].clone()
         K[..., 0, :] *= W / W0
         K[..., 1, :] *= H / H0
+        out["intrinsics"] = K
+    return out
+
+
+def _check_frames(frames, what):
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
+        raise RuntimeError(f"{what}: expects uint8 [N, H, W, 3] frames")
+    if not frames.is_cuda:
+        raise RuntimeError(f"dro_sfm_amd.{what}: tensors must live on a ROCm device (no CPU fallback)")
+
+
+def resize_rgb8(frames, shape):
+    """uint8 [N, H0, W0, 3] -> uint8 [N, H, W, 3], Pillow BILINEAR (the resized PIL image)."""
+    lib = _lib.load()
+    _check_frames(frames, "resize_rgb8")
+    N, H0, W0, _ = frames.shape
+    H, W = int(shape[0]), int(shape[1])
+    frames = frames.contiguous()
+    xb, xk, KX = _tables(W0, W, frames.device)
+    yb, yk, KY = _tables(H0, H, frames.device)
+    tmp = torch.empty(N, H0, W, 3, device=frames.device, dtype=torch.uint8)
+    out = torch.empty(N, H, W, 3, device=frames.device, dtype=torch.uint8)
+    check(lib.dro_resize_rgb8(ptr(frames), N, H0, W0, H, W, ptr(xb), ptr(xk), KX, ptr(yb), ptr(yk), KY,
+                              ptr(tmp), ptr(out), stream_of(out)), "dro_resize_rgb8")
+    return out
+
+
+def rgb8_to_tensor(frames):
+    """ToTensor of uint8 [N, H, W, 3] frames -> float32 [N, 3, H, W] (value / 255)."""
+    lib = _lib.load()
+    _check_frames(frames, "rgb8_to_tensor")
+    N, H, W, _ = frames.shape
+    frames = frames.contiguous()
+    out = torch.empty(N, 3, H, W, device=frames.device, dtype=torch.float32)
+    check(lib.dro_rgb8_to_tensor(ptr(frames), N, H, W, ptr(out), stream_of(out)), "dro_rgb8_to_tensor")
+    return out
+
+
+def colorjitter_params(jittering, n, generator=None):
+    """torchvision ColorJitter.get_params for n frames (one draw per frame, as
+    the reference applies its transform object per image):
+    (brightness, contrast, saturation, hue) -> ranges [max(0, 1 - x), 1 + x]
+    and [-hue, hue] (augmentations.py:236-245); per frame randperm(4), then
+    uniform brightness, contrast, saturation, hue factors.  Returns
+    (order [n, 4] int, factors [n, 3] float, hue [n] float)."""
+    b, c, s, h = jittering
+    rng = [(max(0.0, 1 - b), 1 + b), (max(0.0, 1 - c), 1 + c), (max(0.0, 1 - s), 1 + s)]
+    orders, factors, hues = [], [], []
+    for _ in range(n):
+        orders.append(torch.randperm(4, generator=generator).tolist())
+        factors.append([float(torch.empty(1).uniform_(lo, hi, generator=generator)) for lo, hi in rng])
+        hues.append(float(torch.empty(1).uniform_(-h, h, generator=generator)))
+    return orders, factors, hues
+
+
+def color_jitter_(frames, orders, factors, hues):
+    """In-place ColorJitter of uint8 [N, H, W, 3] frames on the GPU with the
+    given per-frame order / factors / hue factors (colorjitter_params)."""
+    lib = _lib.load()
+    _check_frames(frames, "color_jitter")
+    if not frames.is_contiguous():
+        raise RuntimeError("color_jitter_: frames must be contiguous (in place)")
+    N, H, W, _ = frames.shape
+    prm = np.zeros((N, 8), np.int32)
+    for i in range(N):
+        prm[i, :4] = orders[i]
+        prm[i, 4:7] = np.asarray(factors[i], np.float32).view(np.int32)
+        prm[i, 7] = int(hues[i] * 255) & 255        # np.array(h * 255).astype(np.uint8): trunc, wrap
+    prm_d = torch.from_numpy(prm).to(frames.device)
+    ws = torch.empty(N, device=frames.device, dtype=torch.int64)
+    check(lib.dro_color_jitter_rgb8(ptr(frames), N, H, W, ptr(prm_d), ptr(ws), stream_of(frames)),
+          "dro_color_jitter_rgb8")
+    return frames
+
+
+def train_transforms(sample, image_shape, jittering, generator=None):
+    """train_transforms (reference datasets/transforms.py:8-31) on the GPU for a
+    batch whose 'rgb' is uint8 [B, H0, W0, 3] and 'rgb_context' a list of
+    those: resize_sample -> duplicate_sample -> colorjitter_sample ->
+    to_tensor_sample.  colorjitter_sample's own `random.random() < prob`
+    gate has prob = 1.0 in the reference, so every batch is jittered."""
+    out = dict(sample)
+    frames = [sample["rgb"]] + list(sample["rgb_context"])
+    H0, W0 = sample["rgb"].shape[1:3]
+    resized = [resize_rgb8(f, image_shape) if len(image_shape) else f.contiguous() for f in frames]
+    originals = [rgb8_to_tensor(r) for r in resized]
+    if len(jittering) > 0:
+        for r in resized:
+            orders, factors, hues = colorjitter_params(jittering, r.shape[0], generator)
+            color_jitter_(r, orders, factors, hues)
+    tensors = [rgb8_to_tensor(r) for r in resized]
+    out["rgb"], out["rgb_context"] = tensors[0], tensors[1:]
+    out["rgb_original"], out["rgb_context_original"] = originals[0], originals[1:]
+    if "intrinsics" in sample and len(image_shape):
+        K = sample["intrinsics"].clone()
+        K[..., 0, :] *= image_shape[1] / W0
+        K[..., 1, :] *= image_shape[0] / H0
         out["intrinsics"] = K
     return out

@@ -61,6 +61,9 @@ def load():
     _sig(lib.dro_depth_metrics_median_workspace_bytes, I, restype=Z)
     _sig(lib.dro_depth_metrics_median, P, P, I, I, I, P, P, S)
     _sig(lib.dro_resize_rgb8_to_tensor, P, I, I, I, I, I, P, P, I, P, P, I, P, P, S)
+    _sig(lib.dro_color_jitter_rgb8, P, I, I, I, P, P, S)
+    _sig(lib.dro_resize_rgb8, P, I, I, I, I, I, P, P, I, P, P, I, P, P, S)
+    _sig(lib.dro_rgb8_to_tensor, P, I, I, I, P, S)
     _sig(lib.dro_batchnorm_workspace_bytes, I, I, I, restype=Z)
     _sig(lib.dro_batchnorm_relu_forward, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P, P, P, Z, S)
     _sig(lib.dro_batchnorm_relu_backward, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, Z, S)
@@ -93,7 +96,7 @@ EXPORTED = (
     "dro_maxpool3x3s2_forward", "dro_maxpool3x3s2_backward",
     "dro_depth_metrics_blocks", "dro_depth_metrics_workspace_bytes", "dro_depth_metrics_prepare",
     "dro_depth_metrics_reduce", "dro_depth_metrics_median_workspace_bytes", "dro_depth_metrics_median",
-    "dro_resize_rgb8_to_tensor",
+    "dro_resize_rgb8_to_tensor", "dro_color_jitter_rgb8", "dro_resize_rgb8", "dro_rgb8_to_tensor",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv2d_forward", "dro_convgru_gates_forward",

@@ -226,6 +226,21 @@ int dro_resize_rgb8_to_tensor(const unsigned char* src, int N, int H0, int W0, i
                               const int* xbounds, const int* xcoef, int KX, const int* ybounds,
                               const int* ycoef, int KY, unsigned char* tmp, float* dst, void* stream);
 
+/* torchvision ColorJitter over PIL frames (colorjitter_sample,
+ * datasets/augmentations.py:213-258 of the reference), in place on uint8
+ * [N, H, W, 3] frames, bit-identical to Pillow's ImageEnhance / HSV code.
+ * params [N][8] 32-bit words per frame: order[4] (0 brightness, 1 contrast,
+ * 2 saturation, 3 hue), brightness / contrast / saturation factors (float
+ * bits), hue delta (uint8 added to H).  workspace: N x uint64. */
+/* Resize alone (uint8 HWC out: the resized PIL image) and ToTensor alone, for
+ * the jittered path: resize -> jitter in place -> to tensor. */
+int dro_resize_rgb8(const unsigned char* src, int N, int H0, int W0, int H, int W,
+                    const int* xbounds, const int* xcoef, int KX, const int* ybounds,
+                    const int* ycoef, int KY, unsigned char* tmp, unsigned char* dst, void* stream);
+int dro_rgb8_to_tensor(const unsigned char* src, int N, int H, int W, float* dst, void* stream);
+int dro_color_jitter_rgb8(unsigned char* frames, int N, int H, int W, const int* params,
+                          unsigned long long* workspace, void* stream);
+
 /* Training-mode BatchNorm2d fused with the ReLU / residual add that follows it
  * in the ResNet-18 encoders (networks/optim/extractor.py:7-107 of the reference;
  * BasicBlock: relu(bn(conv(x)) [+ skip])).  Replaces torch.nn.functional.

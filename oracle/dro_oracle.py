@@ -510,6 +510,32 @@ def resize_bilinear_pil(a, H, W):
     return one_pass(one_pass(a, 1, W), 0, H)
 
 
+def color_jitter_pil(a, order, factors, hue):
+    """torchvision ColorJitter.forward over a PIL image (colorjitter_sample,
+    datasets/augmentations.py:213-258): ops in `order` (0 brightness, 1
+    contrast, 2 saturation, 3 hue) through torchvision's functional_pil --
+    ImageEnhance.Brightness / Contrast / Color(factor).enhance, and adjust_hue:
+    H of img.convert('HSV') += np.array(hue * 255).astype(np.uint8) (wrapping),
+    merged back to RGB.  torchvision is not installed here; this restates its
+    published functional_pil on Pillow 12.2, which is the arithmetic checked."""
+    import numpy as np
+    from PIL import Image, ImageEnhance
+    img = Image.fromarray(a)
+    for op in order:
+        if op == 0:
+            img = ImageEnhance.Brightness(img).enhance(factors[0])
+        elif op == 1:
+            img = ImageEnhance.Contrast(img).enhance(factors[1])
+        elif op == 2:
+            img = ImageEnhance.Color(img).enhance(factors[2])
+        else:
+            h, s, v = img.convert("HSV").split()
+            np_h = np.array(h, dtype=np.uint8)
+            np_h += np.uint8(int(hue * 255) & 255)
+            img = Image.merge("HSV", (Image.fromarray(np_h, "L"), s, v)).convert("RGB")
+    return np.asarray(img)
+
+
 def rel_err(a, b):
     """max |a-b| / max(|b|) -- the relative metric the parity tests quote."""
     a, b = a.detach().double(), b.detach().double()
