@@ -109,6 +109,120 @@ __global__ __launch_bounds__(256) void convex_up_bwd_kernel(
   }
 }
 
+// One thread per OUTPUT pixel (b, y*r+a, x*r+c), lanes running along the
+// output row (c fastest): r x more threads than the per-(a, y, x) kernels
+// above (30 720 -> 245 760 at KITTI B=2, which left 3/4 of the chip idle) and
+// every output store a contiguous row segment.  Per output the arithmetic is
+// the per-(a, y, x) kernels' inner iteration, so results are bit-identical;
+// the backward sums the inverse-depth tap gradients of the r sub-pixel lanes
+// of one (a, y, x) in lane order c = 0..r-1 (the old loop order) before the
+// atomics.  Requires 64 % r == 0 (r-lane groups inside one wave).
+__device__ __forceinline__ void cu_decode(int idx, int h, int w, int r, int& b, int& a, int& y, int& x, int& c) {
+  const int wr = w * r;
+  const int q = idx % wr;
+  int t = idx / wr;
+  x = q / r;
+  c = q - x * r;
+  y = t % h;
+  t /= h;
+  a = t % r;
+  b = t / r;
+}
+
+__global__ __launch_bounds__(256) void convex_up_fwd_px_kernel(const float* __restrict__ inv,
+                                                               const float* __restrict__ mask, int B,
+                                                               int h, int w, int r, float add, float mul,
+                                                               float* __restrict__ out) {
+  const int hw = h * w;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * r * hw * r) return;
+  int b, a, y, x, c;
+  cu_decode(idx, h, w, r, b, a, y, x, c);
+  const int pix = y * w + x;
+  float d[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    d[k] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? inv[(size_t)b * hw + yy * w + xx] : 0.f;
+  }
+  const float* mb = mask + (size_t)b * 9 * r * r * hw + pix;
+  float m[9], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = mb[(size_t)(k * r * r + a * r + c) * hw];
+    mx = fmaxf(mx, m[k]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = expf(m[k] - mx);
+    s += m[k];
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc += (m[k] / s) * d[k];
+  out[((size_t)b * h * r + (size_t)y * r + a) * (w * r) + (size_t)x * r + c] = __fadd_rn(add, __fmul_rn(mul, acc));
+}
+
+__global__ __launch_bounds__(256) void convex_up_bwd_px_kernel(
+    const float* __restrict__ inv, const float* __restrict__ mask, const float* __restrict__ gout,
+    int B, int h, int w, int r, float mul, float* __restrict__ ginv, float* __restrict__ gmask) {
+  const int hw = h * w;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = idx < B * r * hw * r;     // whole r-lane groups are live or not
+  int b, a, y, x, c;
+  cu_decode(live ? idx : 0, h, w, r, b, a, y, x, c);
+  const int pix = y * w + x;
+  float d[9], gd[9];
+  bool ok[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    ok[k] = yy >= 0 && yy < h && xx >= 0 && xx < w;
+    d[k] = ok[k] ? inv[(size_t)b * hw + yy * w + xx] : 0.f;
+  }
+  const float* mb = mask + (size_t)b * 9 * r * r * hw + pix;
+  const float G = __fmul_rn(gout[((size_t)b * h * r + (size_t)y * r + a) * (w * r) + (size_t)x * r + c], mul);
+  float m[9], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = mb[(size_t)(k * r * r + a * r + c) * hw];
+    mx = fmaxf(mx, m[k]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = expf(m[k] - mx);
+    s += m[k];
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = m[k] / s;
+    gd[k] = m[k] * G;
+    dot += m[k] * (G * d[k]);
+  }
+  if (live) {
+    float* gmb = gmask + (size_t)b * 9 * r * r * hw + pix;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) gmb[(size_t)(k * r * r + a * r + c) * hw] = m[k] * (G * d[k] - dot);
+  }
+  if (ginv) {
+    const int lane = threadIdx.x & 63, base = lane - c;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      float t = 0.f;
+      for (int cc = 0; cc < r; ++cc) t += __shfl(gd[k], base + cc, 64);   // c = 0..r-1 in order
+      gd[k] = t;
+    }
+    if (live && c == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+        if (ok[k]) atomicAdd(ginv + (size_t)b * hw + (y + k / 3 - 1) * w + (x + k % 3 - 1), gd[k]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Bilinear 2x upsampling (align_corners=False) of the feature/context trunks:
 // F.interpolate(x, scale_factor=2, mode="bilinear") in networks/optim/
@@ -192,7 +306,7 @@ static int up_check(const float* inv, const float* mask, int B, int h, int w, in
     set_error("convex_upsample: NULL input");
     return DRO_E_NULL;
   }
-  if (B < 1 || h < 1 || w < 1 || ratio < 1 || ratio > kMaxR) {
+  if (B < 1 || h < 1 || w < 1 || ratio < 1 || ratio > kMaxR || (long long)B * ratio * ratio * h * w >= (1LL << 31)) {
     set_error("convex_upsample: sizes out of range (ratio 1..8)");
     return DRO_E_SHAPE;
   }
@@ -208,6 +322,11 @@ extern "C" int dro_convex_upsample_forward(const float* inv, const float* mask, 
     return DRO_E_NULL;
   }
   const int total = B * ratio * h * w;
+  if (64 % ratio == 0) {
+    hipLaunchKernelGGL(convex_up_fwd_px_kernel, dim3((total * ratio + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, inv, mask, B, h, w, ratio, add, mul, out);
+    return launch_status("convex_up_fwd_px_kernel launch failed");
+  }
   hipLaunchKernelGGL(convex_up_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, inv, mask, B, h, w, ratio, add, mul, out);
   return launch_status("convex_up_fwd_kernel launch failed");
@@ -225,6 +344,11 @@ extern "C" int dro_convex_upsample_backward(const float* inv, const float* mask,
   hipStream_t s = (hipStream_t)stream;
   if (grad_inv && (st = launch_zero(grad_inv, (size_t)B * h * w, s))) return st;
   const int total = B * ratio * h * w;
+  if (64 % ratio == 0) {
+    hipLaunchKernelGGL(convex_up_bwd_px_kernel, dim3((total * ratio + 255) / 256), dim3(256), 0, s, inv, mask,
+                       grad_out, B, h, w, ratio, mul, grad_inv, grad_mask);
+    return launch_status("convex_up_bwd_px_kernel launch failed");
+  }
   hipLaunchKernelGGL(convex_up_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, inv, mask,
                      grad_out, B, h, w, ratio, mul, grad_inv, grad_mask);
   return launch_status("convex_up_bwd_kernel launch failed");
