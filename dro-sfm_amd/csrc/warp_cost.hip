@@ -21,7 +21,10 @@
 
 namespace dro {
 
-constexpr int kCPT = 8;        // channels per thread
+#ifndef DRO_WARP_CPT
+#define DRO_WARP_CPT 4
+#endif
+constexpr int kCPT = DRO_WARP_CPT;   // channels per thread
 constexpr int kGroups = 4;     // channel groups (waves) per workgroup
 constexpr int kGeoThreads = 256;
 
@@ -112,36 +115,43 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* _
 __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
     WarpArgs a, const float* __restrict__ gcost, float* __restrict__ gfmap,
     float* __restrict__ gfref, float* __restrict__ gxy) {
+  // the block's kGroups waves share 64 pixels: their sampling-position
+  // gradients are summed through LDS (fixed wave order) before one atomic pair
+  // per pixel and block, instead of one per wave (those all hit one address)
+  __shared__ float red[kGroups][kWave][2];
   const int P = a.h * a.w;
-  const int p = blockIdx.x * kWave + (threadIdx.x & 63);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int p = blockIdx.x * kWave + lane;
   const int b = blockIdx.z;
-  const int c0 = (blockIdx.y * kGroups + (threadIdx.x >> 6)) * kCPT;
-  if (p >= P || c0 >= a.C) return;
-  const int cn = min(kCPT, a.C - c0);
+  const int c0 = (blockIdx.y * kGroups + wave) * kCPT;
+  const bool active = p < P && c0 < a.C;   // inactive lanes still join the block's barriers
+  const int pp = active ? p : 0;
+  const int cn = active ? min(kCPT, a.C - c0) : 0;
+  const int cb = c0 < a.C ? c0 : 0;
 
   float ki[9], kr[9];
   cams(a, b, ki, kr);
   float dd;
-  const float depth = decode_depth(a.depth[b * P + p], a.depth_mode, a.min_disp, a.span, &dd);
-  const float u = (float)(p % a.w), v = (float)(p / a.w);
+  const float depth = decode_depth(a.depth[b * P + pp], a.depth_mode, a.min_disp, a.span, &dd);
+  const float u = (float)(pp % a.w), v = (float)(pp / a.w);
   const float scaleN = a.reduce_mean ? 1.f / (float)a.N : 1.f;
 
   float f[kCPT], gf[kCPT], g[kCPT];
-  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
+  const float* fm = a.fmap + ((size_t)b * a.C + cb) * P + pp;
 #pragma unroll
   for (int c = 0; c < kCPT; ++c) {
     f[c] = (c < cn) ? fm[(size_t)c * P] : 0.f;
     gf[c] = 0.f;
   }
   if (a.reduce_mean) {
-    const float* gp = gcost + ((size_t)b * a.C + c0) * P + p;
+    const float* gp = gcost + ((size_t)b * a.C + cb) * P + pp;
 #pragma unroll
     for (int c = 0; c < kCPT; ++c) g[c] = (c < cn) ? gp[(size_t)c * P] * scaleN : 0.f;
   }
   const int ps = pose_stride(a.pose_mode);
   for (int n = 0; n < a.N; ++n) {
     if (!a.reduce_mean) {
-      const float* gp = gcost + (((size_t)n * a.B + b) * a.C + c0) * P + p;
+      const float* gp = gcost + (((size_t)n * a.B + b) * a.C + cb) * P + pp;
 #pragma unroll
       for (int c = 0; c < kCPT; ++c) g[c] = (c < cn) ? gp[(size_t)c * P] : 0.f;
     }
@@ -151,8 +161,8 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
     project(ki, kr, R, t, u, v, depth, a.h, a.w, q);
     Taps T;
     bilinear_taps(q.ix, q.iy, a.h, a.w, T);
-    const float* fr = a.fmap_ref + (((size_t)n * a.B + b) * a.C + c0) * P;
-    float* gr = gfref ? gfref + (((size_t)n * a.B + b) * a.C + c0) * P : nullptr;
+    const float* fr = a.fmap_ref + (((size_t)n * a.B + b) * a.C + cb) * P;
+    float* gr = gfref ? gfref + (((size_t)n * a.B + b) * a.C + cb) * P : nullptr;
     const float omy = 1.f - T.ty, omx = 1.f - T.tx;
     float gix = 0.f, giy = 0.f;
 #pragma unroll
@@ -179,13 +189,25 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
       }
     }
     if (gxy) {
-      float* dst = gxy + ((size_t)(n * a.B + b) * P + p) * 2;
-      atomicAdd(dst, gix);
-      atomicAdd(dst + 1, giy);
+      red[wave][lane][0] = gix;
+      red[wave][lane][1] = giy;
+      __syncthreads();
+      if (wave == 0 && p < P) {
+        float sx = 0.f, sy = 0.f;
+#pragma unroll
+        for (int w = 0; w < kGroups; ++w) {
+          sx += red[w][lane][0];
+          sy += red[w][lane][1];
+        }
+        float* dst = gxy + ((size_t)(n * a.B + b) * P + p) * 2;
+        atomicAdd(dst, sx);
+        atomicAdd(dst + 1, sy);
+      }
+      __syncthreads();
     }
   }
   if (gfmap) {
-    float* out = gfmap + ((size_t)b * a.C + c0) * P + p;
+    float* out = gfmap + ((size_t)b * a.C + cb) * P + pp;
 #pragma unroll
     for (int c = 0; c < kCPT; ++c)
       if (c < cn) out[(size_t)c * P] = a.acc_fmap ? out[(size_t)c * P] + gf[c] : gf[c];
