@@ -223,6 +223,71 @@ __global__ __launch_bounds__(256) void convex_up_bwd_px_kernel(
   }
 }
 
+// Backward with one wave per sub-pixel column c and lanes along 64 consecutive
+// low-res pixels: every mask load and mask-gradient store of a wave is one
+// contiguous 256-B row segment (the row-along-x mapping above stores 8 x 32 B).
+// The r waves of a block are the r columns c of one (b, a, 64-pixel run); the
+// inverse-depth tap gradients are summed over c through LDS in the order
+// c = 0..r-1 (as the per-(a, y, x) kernel's loop) before the atomics.
+// Block = 64 * r threads (r <= 8).
+__global__ __launch_bounds__(512) void convex_up_bwd_cw_kernel(
+    const float* __restrict__ inv, const float* __restrict__ mask, const float* __restrict__ gout,
+    int B, int h, int w, int r, float mul, float* __restrict__ ginv, float* __restrict__ gmask) {
+  __shared__ float red[kMaxR][9][64];
+  const int hw = h * w;
+  const int lane = threadIdx.x & 63, c = threadIdx.x >> 6;
+  const int a = blockIdx.y, b = blockIdx.z;
+  const int pix = blockIdx.x * 64 + lane;
+  const bool live = pix < hw;
+  const int pp = live ? pix : 0;
+  const int y = pp / w, x = pp - y * w;
+  float d[9];
+  bool ok[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    ok[k] = yy >= 0 && yy < h && xx >= 0 && xx < w;
+    d[k] = ok[k] ? inv[(size_t)b * hw + yy * w + xx] : 0.f;
+  }
+  const float* mb = mask + (size_t)b * 9 * r * r * hw + pp;
+  const float G = __fmul_rn(gout[((size_t)b * h * r + (size_t)y * r + a) * (w * r) + (size_t)x * r + c], mul);
+  float m[9], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = mb[(size_t)(k * r * r + a * r + c) * hw];
+    mx = fmaxf(mx, m[k]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = expf(m[k] - mx);
+    s += m[k];
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = m[k] / s;
+    red[c][k][lane] = m[k] * G;
+    dot += m[k] * (G * d[k]);
+  }
+  if (live) {
+    float* gmb = gmask + (size_t)b * 9 * r * r * hw + pix;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) gmb[(size_t)(k * r * r + a * r + c) * hw] = m[k] * (G * d[k] - dot);
+  }
+  if (ginv) {
+    __syncthreads();
+    if (c == 0 && live) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        float t = 0.f;
+        for (int cc = 0; cc < r; ++cc) t += red[cc][k][lane];
+        if (ok[k]) atomicAdd(ginv + (size_t)b * hw + (y + k / 3 - 1) * w + (x + k % 3 - 1), t);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Bilinear 2x upsampling (align_corners=False) of the feature/context trunks:
 // F.interpolate(x, scale_factor=2, mode="bilinear") in networks/optim/
@@ -344,6 +409,11 @@ extern "C" int dro_convex_upsample_backward(const float* inv, const float* mask,
   hipStream_t s = (hipStream_t)stream;
   if (grad_inv && (st = launch_zero(grad_inv, (size_t)B * h * w, s))) return st;
   const int total = B * ratio * h * w;
+  if (B <= 65535) {
+    hipLaunchKernelGGL(convex_up_bwd_cw_kernel, dim3((h * w + 63) / 64, ratio, B), dim3(64 * ratio), 0, s, inv,
+                       mask, grad_out, B, h, w, ratio, mul, grad_inv, grad_mask);
+    return launch_status("convex_up_bwd_cw_kernel launch failed");
+  }
   if (64 % ratio == 0) {
     hipLaunchKernelGGL(convex_up_bwd_px_kernel, dim3((total * ratio + 255) / 256), dim3(256), 0, s, inv, mask,
                        grad_out, B, h, w, ratio, mul, grad_inv, grad_mask);
