@@ -373,7 +373,21 @@ def cpu_baseline(model, budget_s=12.0, max_steps=40):
             "sample": f"{steps} timed steps (+1 warmup; ~{budget_s:.0f} s budget) of the full training "
                       f"step, B={B}, {H}x{W}, "
                       f"N={NREF}, {VERSION}, CPU oracle oracle/dro_oracle.py, torch {torch.__version__}",
-            "sec_per_step": round(sec, 3)}
+            "sec_per_step": round(sec, 3), "sec_per_step_min_max": [round(min(times), 3), round(max(times), 3)],
+            "cpu_model": _cpu_model(), "cpu_capability": torch.backends.cpu.get_cpu_capability(),
+            "host_cpus": os.cpu_count()}
+
+
+def _cpu_model():
+    """The host CPU's model name (/proc/cpuinfo, as lscpu prints it)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 # ----------------------------------------------------------------------------- main

@@ -27,8 +27,11 @@ Batched weight gradients (direct path, default on): the recurrent update
 blocks apply every weight once per iteration, so instead of one weight-gradient
 launch + one split reduction per use, each use is queued (sources, output
 gradient, saved output kept alive) and all uses of a weight are reduced by ONE
-dro_conv2d_weight_grad_multi launch at the end of backward (engine final
-callback, before the trainer's gradient all-reduce).  set_batched_weight_grads.
+dro_conv2d_weight_grad_multi launch: from the parameter's post-accumulate hook
+(flush_param_grads, called by the trainer's gradient buckets -- autograd runs
+it once the last use has been back-propagated, so the bucket's all-reduce
+overlaps the rest of the backward), or at the end of backward (engine final
+callback) for whatever is still queued.  set_batched_weight_grads.
 
 Split-bf16 engine (set_split_engine, default off): the 1x5 / 5x1 / 3x3 / 1x1
 forward and data-gradient GEMMs run on bf16 MFMA over operands split into three
@@ -273,7 +276,6 @@ class DroWgradUse(ctypes.Structure):
 _BATCH = [True]
 _PENDING = {}
 _PENDING_CB = [False]
-_PENDING_STREAMS = []   # streams the queued uses' tensors were produced on
 _MULTI_SHAPES = {(1, 1), (1, 5), (5, 1), (3, 3)}
 _MAX_USES = 16
 
@@ -294,17 +296,39 @@ def _queue_weight_grad(srcs, wshape, act, alpha, dout, y, gw, gb):
     key = (gw.data_ptr(), gb.data_ptr() if gb is not None else 0, B, H, W, act, float(alpha),
            tuple(t.shape[1] for t in srcs))
     ent = _PENDING.get(key)
-    if ent is None:
-        ent = _PENDING[key] = ((B, H, W, Cin, Cout, KH, KW, act, float(alpha), gw, gb, len(srcs)), [])
-    ent[1].append((list(srcs), dout, y))
     cur = torch.cuda.current_stream()
-    if all(s != cur for s in _PENDING_STREAMS):
-        _PENDING_STREAMS.append(cur)
+    if ent is None:
+        ent = _PENDING[key] = ((B, H, W, Cin, Cout, KH, KW, act, float(alpha), gw, gb, len(srcs)), [], [])
+    ent[1].append((list(srcs), dout, y))
+    if all(s != cur for s in ent[2]):
+        ent[2].append(cur)
     if not _PENDING_CB[0]:
         _PENDING_CB[0] = True
         stream = torch.cuda.current_stream()
         torch.autograd.Variable._execution_engine.queue_callback(lambda: flush_weight_grads(stream))
     return True
+
+
+def _covers(t, ptr_):
+    return t is not None and t.data_ptr() <= ptr_ < t.data_ptr() + t.numel() * t.element_size()
+
+
+def flush_param_grads(param):
+    """Launch now the queued weight gradients that write into `param.grad`
+    (trainers/dp_trainer.GradBuckets calls this from the parameter's
+    post-accumulate hook: autograd runs that hook once every use of the
+    parameter has been back-propagated, so the queue holds all of its uses and
+    its bucket's all-reduce can start while the rest of the backward runs).
+    Returns the stream the launches were queued on, or None."""
+    g = param.grad
+    if g is None or not _PENDING:
+        return None
+    p0 = g.data_ptr()
+    keys = [k for k, (meta, _, _) in _PENDING.items() if _covers(meta[9], p0) or _covers(meta[10], p0)]
+    if not keys:
+        return None
+    items = [_PENDING.pop(k) for k in keys]
+    return _launch_weight_grads(items, items[0][2][0])
 
 
 def flush_weight_grads(stream=None):
@@ -313,21 +337,23 @@ def flush_weight_grads(stream=None):
     _PENDING_CB[0] = False
     if not _PENDING:
         return
-    lib = _lib.load()
     items = list(_PENDING.values())
     _PENDING.clear()
-    stream = stream or torch.cuda.current_stream()
-    for s in _PENDING_STREAMS:        # uses queued from other streams (concurrent blocks)
-        if s != stream:
-            stream.wait_stream(s)
-            for _, uses in items:
+    _launch_weight_grads(items, stream or torch.cuda.current_stream())
+
+
+def _launch_weight_grads(items, stream):
+    lib = _lib.load()
+    for _, uses, streams in items:       # uses queued from other streams (concurrent blocks)
+        for s in streams:
+            if s != stream:
+                stream.wait_stream(s)
                 for srcs, dout, y in uses:
                     for x in (*srcs, dout, y):
                         if x is not None:
                             x.record_stream(stream)
-    _PENDING_STREAMS.clear()
     with torch.cuda.stream(stream):
-        for meta, uses in items:
+        for meta, uses, _ in items:
             B, H, W, Cin, Cout, KH, KW, act, alpha, gw, gb, nsrc = meta
             for c0 in range(0, len(uses), _MAX_USES):
                 chunk = uses[c0:c0 + _MAX_USES]
@@ -344,6 +370,7 @@ def flush_weight_grads(stream=None):
                                                        ctypes.c_float(alpha), ptr(gw), ptr(gb), 1,
                                                        ptr(ws), nb, stream_of(gw)),
                       "dro_conv2d_weight_grad_multi")
+    return stream
 
 
 _WS = {}

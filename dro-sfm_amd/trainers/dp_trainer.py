@@ -22,6 +22,11 @@ provides it MI355X-first:
     bucket's adopted gradients are copied into the flat buffer with one
     multi-tensor launch (torch._foreach_copy_) -- ~160 add launches per step
     become a handful;
+  * the conv-engine weights whose gradients are written in place (batched
+    over all uses of a weight) get their weight-gradient launch from their own
+    post-accumulate hook, i.e. as soon as autograd has back-propagated their
+    last use, so the update blocks' buckets are reduced while the encoders'
+    backward still runs;
   * parameters that never receive a gradient (DepthPoseNet.cnet, dead in the
     reference forward) are discovered on the first step and left out;
   * initial parameters and buffers are broadcast from rank 0 (BatchNorm keeps
@@ -51,11 +56,32 @@ def init_distributed(backend=None):
 
 
 class GradBuckets:
-    """Flat gradient storage + bucketed, backward-overlapped all-reduce."""
+    """Flat gradient storage + bucketed, backward-overlapped all-reduce.
 
-    def __init__(self, params, bucket_mb=25.0, group=None, groups=()):
+    Gradients come in two kinds:
+      * adopted: autograd produces the tensor (.grad is None at the start of a
+        step); a complete bucket copies them into the flat buffer;
+      * direct: the hip conv engine accumulates them in place into the flat
+        .grad views (hip/conv.py, `_dro_direct_used`), batched per weight.
+    Autograd runs every parameter's post-accumulate hook once per backward,
+    after the last use of that parameter has been back-propagated (for a
+    direct one the hook sees the None the conv returned).  For a direct
+    parameter the hook first launches its queued weight-gradient kernel
+    (`direct_flush`, hip.conv.flush_param_grads on the GPU) and records the
+    stream it went to; then it counts down like any other.  A bucket is
+    complete when all its parameters' hooks have run: the current stream waits
+    for every stream that wrote into it, the adopted gradients are gathered,
+    and an event marks the gathered state -- the all-reduce, issued later
+    from whichever stream runs that hook, waits for that event first.
+    """
+
+    def __init__(self, params, bucket_mb=25.0, group=None, groups=(), direct_flush=None,
+                 always_reduce=False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # always_reduce: issue the collectives even at world size 1 (tests of the
+        # RCCL path inside a captured graph on a single-GPU box)
+        self.reduce = self.world > 1 or (always_reduce and dist.is_initialized())
         self.params = _adjacent_order([p for p in params if p.requires_grad], groups)
         if any(p.dtype != torch.float32 for p in self.params):
             raise RuntimeError("GradBuckets: fp32 parameters only")
@@ -65,9 +91,14 @@ class GradBuckets:
             self.offsets[p] = off
             p.grad = self.flat[off:off + p.numel()].view_as(p)
             off += p.numel()
+        if direct_flush is None and self.flat.is_cuda:
+            from ..hip.conv import flush_param_grads as direct_flush
+        self.direct_flush = direct_flush
         self.bucket_bytes = int(bucket_mb * 1024 * 1024)
         self.active = None            # params that receive gradients (learned on step 1)
         self.buckets, self._pending, self._seen = [], [], set()
+        self.issued = []              # bucket indices in issue order (last step; tests)
+        self.issued_in_backward = 0   # of those, issued from backward hooks (tests)
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         for p in self.params:
             # hip convs may accumulate this gradient in place (hip/conv.py, direct path)
@@ -85,20 +116,16 @@ class GradBuckets:
         if cur:
             self.buckets.append(cur)
         self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b}
-        # gradients adopted from autograd (.grad = None at the start of a step)
+        # gradients adopted from autograd (.grad = None at the start of a step);
+        # the direct ones stay flat views and are written in place
         self._adopt = [[p for p in b if not _direct_used(p)] for b in self.buckets]
-        # gradients written in place by the hip convs (side stream, joined at the end
-        # of backward) fire no hook: their buckets are reduced in finish()
-        self._deferred = [any(_direct_used(p) for p in b) for b in self.buckets]
-        self._need = [sum(not _direct_used(p) for p in b) for b in self.buckets]
-        # ONE all-reduce order, identical on every rank (the build is decided from
-        # all-reduced flags): hook-completed buckets in backward order, then the
-        # deferred ones.  A bucket is issued only after every bucket before it in
-        # this order, so ranks whose buckets complete in different orders -- or
-        # not at all on some step (a gradient that never arrives) -- still pair
-        # their collectives one for one (as DDP's in-order bucket launch does).
-        self._order = ([b for b in range(len(self.buckets)) if not self._deferred[b]] +
-                       [b for b in range(len(self.buckets)) if self._deferred[b]])
+        self._need = [len(b) for b in self.buckets]
+        # ONE all-reduce order, identical on every rank: backward order.  A bucket
+        # is issued only after every bucket before it in this order, so ranks
+        # whose buckets complete in different orders -- or not at all on some
+        # step (a gradient that never arrives) -- still pair their collectives
+        # one for one (as DDP's in-order bucket launch does).
+        self._order = list(range(len(self.buckets)))
 
     def _slice(self, bucket):
         """One contiguous flat slice covering a bucket (slots of inactive params
@@ -108,20 +135,24 @@ class GradBuckets:
         return self.flat[lo:hi]
 
     def _on_grad(self, p):
-        if _direct_used(p):
-            # written in place by the hip convs (the hook also fires for the None
-            # autograd receives); its bucket is reduced in finish()
-            return
+        direct = _direct_used(p)
+        wrote = None
+        if direct and self.direct_flush is not None:
+            # every use of p is back-propagated: launch its queued weight gradient
+            wrote = self.direct_flush(p)
         if self.active is None:
             self._seen.add(p)
             return
         b = self._bucket_of.get(p)
-        if b is None:
+        if b is None or self._ready[b]:
             return
         if self.flat.is_cuda:
             # the hook runs on the stream that produced this gradient (the context
-            # encoders' backward runs on side streams): remember it for the bucket
+            # encoders' backward runs on side streams), the in-place weight
+            # gradient went to `wrote`: remember both for the bucket
             self._bstreams[b].add(torch.cuda.current_stream())
+            if wrote is not None:
+                self._bstreams[b].add(wrote)
         self._left[b] -= 1
         if self._left[b] == 0:
             self._complete(b)
@@ -129,21 +160,30 @@ class GradBuckets:
 
     def _complete(self, b):
         """Bucket b's gradients are final: order the current stream after every
-        stream that produced one of them, then gather them into the flat buffer."""
+        stream that produced or wrote one of them, gather the adopted ones into
+        the flat buffer, and mark that point with an event."""
         if self.flat.is_cuda:
             cur = torch.cuda.current_stream()
             for st in self._bstreams[b]:
                 if st != cur:
                     cur.wait_stream(st)
         self._gather(b)
+        if self.flat.is_cuda:
+            self._events[b] = torch.cuda.Event()
+            self._events[b].record(torch.cuda.current_stream())
         self._ready[b] = True
 
     def _issue_ready(self):
-        """Issue the all-reduce of every ready bucket at the head of the order."""
+        """Issue the all-reduce of every ready bucket at the head of the order.
+        The issuing stream first waits for the bucket's completion event: the
+        bucket may have been gathered on another stream."""
         while self._next < len(self._order) and self._ready[self._order[self._next]]:
             b = self._order[self._next]
             self._next += 1
-            if self.world > 1:
+            self.issued.append(b)
+            if self.reduce:
+                if self._events[b] is not None:
+                    torch.cuda.current_stream().wait_event(self._events[b])
                 self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
                                                      group=self.group, async_op=True))
 
@@ -172,9 +212,11 @@ class GradBuckets:
     def zero(self):
         self.flat.zero_()
         self._pending = []
+        self.issued = []
         if self.active is not None:
             self._left = list(self._need)
             self._ready = [False] * len(self.buckets)
+            self._events = [None] * len(self.buckets)
             self._next = 0
             self._bstreams = [set() for _ in self.buckets]
             for ps in self._adopt:
@@ -183,6 +225,7 @@ class GradBuckets:
 
     def finish(self):
         """Complete every bucket's all-reduce and average over ranks."""
+        self.issued_in_backward = len(self.issued)
         if self.active is None:
             seen = self._seen | {p for p in self.params if _direct_used(p)}
             if self.world > 1:
@@ -190,13 +233,13 @@ class GradBuckets:
                 dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
                 seen = {p for p, f in zip(self.params, flags.tolist()) if f > 0}
             self._build(seen)
-            if self.world > 1:                               # step 1: reduce synchronously
+            if self.reduce:                                  # step 1: reduce synchronously
                 for b in self.buckets:
                     dist.all_reduce(self._slice(b), op=dist.ReduceOp.SUM, group=self.group)
         else:
-            # deferred buckets, and buckets some of whose gradients never arrived
-            # this step (their missing slots are the zeros of zero()): complete
-            # them, then issue everything not issued yet, in the common order
+            # buckets some of whose gradients never arrived this step (their
+            # missing slots are the zeros of zero()): complete them, then issue
+            # everything not issued yet, in the common order
             for b in range(len(self.buckets)):
                 if not self._ready[b]:
                     self._complete(b)
@@ -269,7 +312,15 @@ class FlatAdam(torch.optim.Optimizer):
     layout ({'state': {i: {'step', 'exp_avg', 'exp_avg_sq'}}, 'param_groups':
     [{..., 'params': [0..n-1]}]}), indexed in the order of `params` -- the
     reference saves its Adam state that way under 'optimizer'
-    (model_checkpoint.py:76), so checkpoints interchange in both directions."""
+    (model_checkpoint.py:76), so checkpoints interchange in both directions.
+    `params` is the module's whole parameter list, as the reference's Adam
+    group over depth_net.parameters() (model_wrapper.py:173): frozen
+    parameters (absent from `offsets`) keep their index and never get state.
+    The saved group says capturable=False (a torch.optim.Adam loading it keeps
+    its default code path); this optimizer's own capture safety does not
+    depend on that flag.  One step counter is shared by every parameter: a
+    parameter that first receives a gradient after step 1 is saved with the
+    global step (torch.optim.Adam would count its own)."""
 
     def __init__(self, params, flat_param, flat_grad, lr=2e-4, betas=(0.9, 0.999), eps=1e-8,
                  weight_decay=0.0, offsets=None):
@@ -278,7 +329,7 @@ class FlatAdam(torch.optim.Optimizer):
         _lib.load()
         params = list(params)
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
-                        amsgrad=False, maximize=False, foreach=None, capturable=True,
+                        amsgrad=False, maximize=False, foreach=None, capturable=False,
                         differentiable=False, fused=None)
         super().__init__(params if params else [flat_param], defaults)
         self.params, self.flat_param, self.flat_grad = params, flat_param, flat_grad
@@ -342,7 +393,7 @@ class FlatAdam(torch.optim.Optimizer):
         state = {}
         if float(self.step_t) > 0:               # torch.optim.Adam has no state before its first step
             for i, p in enumerate(self.params):
-                if self.active is not None and p not in self.active:
+                if p not in self.offsets or (self.active is not None and p not in self.active):
                     continue                 # torch.optim.Adam keeps no state without a grad
                 # a CPU step tensor, as torch.optim.Adam(capturable=False) saves it
                 state[i] = {"step": torch.tensor(float(self.step_t), dtype=torch.float32),
@@ -363,9 +414,9 @@ class FlatAdam(torch.optim.Optimizer):
             steps = set()
             for slot, i in enumerate(groups[0]["params"]):
                 st = sd["state"].get(i)
-                if st is None:
-                    continue
                 p = self.params[slot]
+                if st is None or p not in self.offsets:
+                    continue                 # no state, or a parameter frozen here
                 self._slot(self.exp_avg, p).copy_(st["exp_avg"])
                 self._slot(self.exp_avg_sq, p).copy_(st["exp_avg_sq"])
                 steps.add(float(st["step"]))
@@ -399,19 +450,19 @@ class DataParallelTrainer:
     step can be replayed from a hipGraph (GraphedTrainStep)."""
 
     def __init__(self, model, lr=2e-4, bucket_mb=25.0, group=None, betas=(0.9, 0.999), eps=1e-8,
-                 capturable=False):
+                 capturable=False, always_reduce=False):
         self.model = model
         broadcast_module(model, 0, group)
         self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb, group=group,
-                                 groups=param_groups(model))
+                                 groups=param_groups(model), always_reduce=always_reduce)
         dev = self.grads.flat.device
         if dev.type == "cuda":
             # fused Adam over flat buffers (the product path on the GPU)
             self.flat_params = flatten_parameters(self.grads.params, self.grads.offsets,
                                                   self.grads.flat.numel(), dev)
-            # indexed in registration order, like the reference's Adam over
-            # depth_net.parameters() (model_wrapper.py:168-187)
-            order = [p for p in model.parameters() if p.requires_grad]
+            # indexed in registration order over ALL parameters, like the
+            # reference's Adam over depth_net.parameters() (model_wrapper.py:168-187)
+            order = list(model.parameters())
             self.optimizer = FlatAdam(order, self.flat_params, self.grads.flat, lr=lr,
                                       betas=betas, eps=eps, offsets=self.grads.offsets)
         else:

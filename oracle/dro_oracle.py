@@ -413,16 +413,36 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
     return inv_preds, torch.stack([torch.stack(pr, 1) for pr in pose_preds], 2)
 
 
+def flip_lr_intr(K, width):
+    """utils/image.py:61-81 (returned as a new tensor; the reference mutates the
+    batch's intrinsics in place, so everything after the flip sees this K)."""
+    K = K.clone()
+    K[:, 0, 0] = -1 * K[:, 0, 0]
+    K[:, 0, 2] = width - K[:, 0, 2]
+    return K
+
+
 def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", loss_kw=None,
-                    forced_selection=None):
-    """SelfSupModelMF / SupModelMF .forward in training mode with flip disabled
-    (models/SfmModelMF.py:140-189, SelfSupModelMF.py:63-99, SupModelMF.py:78-119)."""
+                    forced_selection=None, flip=False):
+    """SelfSupModelMF / SupModelMF .forward in training mode
+    (models/SfmModelMF.py:106-189, SelfSupModelMF.py:63-99, SupModelMF.py:78-119).
+
+    flip=True is the reference's random left-right flip taken
+    (SfmModelMF.py:110-119, utils/image.py:61-81, 106-130): the net sees the
+    flipped target and refs with K flipped (fx -> -fx, cx -> W - cx), its
+    inverse depths are flipped back, and the loss -- on the UNflipped
+    `*_original` images -- uses the flipped K (the in-place mutation)."""
     loss_kw = loss_kw or {}
-    invs, pvec = depth_pose_net(p, version, min_depth, max_depth, batch["rgb"], batch["rgb_context"],
-                                batch["intrinsics"], training=True)
+    K = batch["intrinsics"]
+    img, refs = batch["rgb"], batch["rgb_context"]
+    if flip:
+        K = flip_lr_intr(K, img.shape[3])
+        img, refs = img.flip(3), [r.flip(3) for r in refs]
+    invs, pvec = depth_pose_net(p, version, min_depth, max_depth, img, refs, K, training=True)
+    if flip:
+        invs = [d.flip(3) for d in invs]
     N, n = pvec.shape[1], pvec.shape[2]
     poses = [[pvec[:, j, i] for i in range(n)] for j in range(N)]
-    K = batch["intrinsics"]
     if kind == "selfsup":
         return photometric_decay_loss(batch["rgb_original"], batch["rgb_context_original"], invs, K,
                                       K, poses, forced_selection=forced_selection, **loss_kw)

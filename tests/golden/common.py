@@ -99,3 +99,61 @@ def to_np(x):
 def load_fixture(path):
     with np.load(path, allow_pickle=False) as z:
         return {k: torch.from_numpy(z[k].copy()) for k in z.files}
+
+
+GRAD_SAMPLE = 2048
+
+
+def grad_sample_index(name, numel, k=GRAD_SAMPLE):
+    """Deterministic sample of k flat indices of parameter `name`'s gradient
+    (the train-step fixtures store gradients of large encoder tensors at these
+    indices; the tests read the same entries).  None: the tensor is small
+    enough to be stored whole."""
+    if numel <= k:
+        return None
+    return torch.randperm(numel, generator=_gen("gidx:" + name))[:k].sort().values
+
+
+def grad_fixture(named_grads, full_prefixes=()):
+    """{'gfull.<name>': whole gradient} for parameters under `full_prefixes` or
+    with <= GRAD_SAMPLE entries, else {'gsamp.<name>': gradient at
+    grad_sample_index(name)} -- per-element values, not checksums."""
+    out = {}
+    for name, g in named_grads:
+        if g is None:
+            continue
+        idx = grad_sample_index(name, g.numel())
+        if idx is None or name.split(".")[0] in full_prefixes:
+            out["gfull." + name] = g.detach().clone()
+        else:
+            out["gsamp." + name] = g.detach().flatten()[idx].clone()
+    return out
+
+
+def grad_errors(named_grads, fixture):
+    """Per parameter: max|g - g_ref| / max|g_ref| over the fixture's stored
+    entries (whole tensors 'gfull.*' or the sampled 'gsamp.*').  Returns
+    {name: error}; every stored gradient must be present in named_grads."""
+    got = dict(named_grads)
+    out = {}
+    for key, ref in fixture.items():
+        if not key.startswith(("gfull.", "gsamp.")):
+            continue
+        name = key.split(".", 1)[1]
+        g = got[name]
+        assert g is not None, f"no gradient for {name}"
+        g = g.detach().cpu()
+        if key.startswith("gsamp."):
+            g = g.flatten()[grad_sample_index(name, g.numel())]
+        else:
+            g = g.reshape(ref.shape)
+        ref = ref.double()
+        out[name] = float((g.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    return out
+
+
+def fval(t):
+    """A scalar fixture entry (stored as float32) back as the Python float the
+    generator passed to the reference (shortest float32 repr: 0.2, not
+    0.2000000030): depth ranges enter 1/min_depth and the validity masks."""
+    return float(np.format_float_positional(np.float32(float(t)), unique=True))

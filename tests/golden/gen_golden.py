@@ -37,7 +37,7 @@ import torch.nn as nn
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from common import det_init, kitti_K, smooth_images, to_np  # noqa: E402
+from common import SCANNET_K_320, det_init, grad_fixture, kitti_K, smooth_images, to_np  # noqa: E402
 
 REF = "/root/reference"
 
@@ -152,8 +152,19 @@ def install_shims():
 # ----------------------------------------------------------------------------- helpers
 def save(name, **arrays):
     path = os.path.join(HERE, name + ".npz")
-    np.savez_compressed(path, **{k: to_np(v).astype(np.float32) if to_np(v).dtype == np.float64
-                                 else to_np(v) for k, v in arrays.items()})
+    arrs = {k: to_np(v).astype(np.float32) if to_np(v).dtype == np.float64 else to_np(v)
+            for k, v in arrays.items()}
+    if os.path.exists(path):
+        # regenerating an existing fixture must reproduce it exactly: keep the
+        # committed file (no byte churn from the zip metadata), fail otherwise
+        with np.load(path, allow_pickle=False) as z:
+            same = set(z.files) == set(arrs) and all(np.array_equal(z[k], arrs[k]) for k in arrs)
+        if same:
+            print(f"  {name}.npz unchanged")
+            return
+        if os.environ.get("GOLDEN_OVERWRITE") != "1":
+            raise SystemExit(f"{name}.npz would change (set GOLDEN_OVERWRITE=1 to rewrite it)")
+    np.savez_compressed(path, **arrs)
     print(f"  wrote {name}.npz ({os.path.getsize(path) / 1024:.0f} KiB)")
 
 
@@ -467,6 +478,90 @@ def gen_full():
         save(f"train_step_{tag}", image=img, refs=torch.stack(refs), K=K, gt_depth=gdepth,
              gt_poses=torch.stack(gpose, 1), loss=out["loss"],
              **{"metric_" + k: v for k, v in out["metrics"].items()}, **grad_checksums(net2, None))
+        # per-element parameter gradients of the same step (it8: update blocks and
+        # heads whole, the encoders at a fixed sample of entries), then the same
+        # step with the left-right flip forced (SfmModelMF.py:110-119: images
+        # flipped, K flipped IN PLACE -- the loss sees fx < 0, cx' = W - cx).
+        # Global RNG state is restored so the fixtures after this one are unchanged.
+        rng = torch.get_rng_state()
+        full = ("update_block_depth", "update_block_pose", "depth_head", "pose_head",
+                "upmask_net") if tag == "it8" else ()
+        save(f"train_step_{tag}_grads", loss=out["loss"],
+             **grad_fixture(((k, q.grad) for k, q in net2.named_parameters()), full))
+        model_f = model_cls(**{**kw, "flip_lr_prob": 1.0})
+        net3 = det_init(DepthPoseNet(version=version, min_depth=mind, max_depth=maxd))
+        model_f.add_depth_net(net3)
+        model_f.train()
+        batch_f = dict(batch, intrinsics=K.clone())
+        out_f = model_f(batch_f)
+        out_f["loss"].sum().backward()
+        save(f"train_step_{tag}_flip", K_after=batch_f["intrinsics"], loss=out_f["loss"],
+             **{"metric_" + k: v for k, v in out_f["metrics"].items()},
+             **grad_fixture(((k, q.grad) for k, q in net3.named_parameters()), full))
+        torch.set_rng_state(rng)
+
+
+def gen_scannet():
+    """ScanNet-style cases (BASELINE configs[2] / configs[4]): the photometric loss
+    at N=4 refs, n=4 predictions (the it12-h count) with automask + min, and a
+    SelfSupModelMF it12-h-out training step with N=4 refs (view5, depth 0.2-10)
+    at 64x96 -- loss, metrics and per-element gradients."""
+    from dro_sfm.networks.depth_pose.DepthPoseNet import DepthPoseNet
+    from dro_sfm.models.SelfSupModelMF import SelfSupModelMF
+    from dro_sfm.geometry.pose import Pose
+    from dro_sfm.losses.multiview_photometric_loss_mf import MultiViewPhotometricDecayLoss
+    g = torch.Generator().manual_seed(44)
+
+    def scannet_K(B, W, H):
+        K = torch.tensor(SCANNET_K_320, dtype=torch.float32)
+        K[0] *= W / 320.0
+        K[1] *= H / 240.0
+        K[2] = torch.tensor([0.0, 0.0, 1.0])
+        return K.unsqueeze(0).repeat(B, 1, 1).contiguous()
+
+    B, H, W, n, N = 2, 48, 64, 4, 4
+    K = scannet_K(B, W, H)
+    image = smooth_images(B, H, W, 61, detail=0.3)
+    ctx = [smooth_images(B, H, W, 62 + j, detail=0.3) for j in range(N)]
+    invs = [0.1 + 2.0 * torch.rand(B, 1, H, W, generator=g) for _ in range(n)]
+    vecs = torch.stack([torch.stack([rand_pose(B, g, 0.05, 0.02) for _ in range(n)], 1) for _ in range(N)], 1)
+    loss_fn = MultiViewPhotometricDecayLoss(ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001,
+                                            C1=1e-4, C2=9e-4, photometric_reduce_op="min", disp_norm=True,
+                                            clip_loss=0.0, progressive_scaling=0.0, padding_mode="zeros",
+                                            automask_loss=True)
+    invs_ = [i.clone().requires_grad_(True) for i in invs]
+    vecs_ = vecs.clone().requires_grad_(True)
+    poses = [[Pose.from_vec(vecs_[:, j, i], "euler") for i in range(n)] for j in range(N)]
+    out = loss_fn(image, ctx, invs_, K, K, poses)
+    out["loss"].sum().backward()
+    save("photo_loss_n4", image=image, context=torch.stack(ctx), inv_depths=torch.stack(invs), poses=vecs,
+         K=K, loss=out["loss"], photometric_loss=out["metrics"]["photometric_loss"],
+         smoothness_loss=out["metrics"]["smoothness_loss"],
+         g_inv_depths=torch.stack([i.grad for i in invs_]), g_poses=vecs_.grad,
+         automask=np.int32(1), reduce_min=np.int32(1))
+
+    # view5 self-supervised training step (it12-h-out, N=4)
+    B, H, W, N = 1, 64, 96, 4
+    mind, maxd = 0.2, 10.0
+    K = scannet_K(B, W, H)
+    img = smooth_images(B, H, W, 71, detail=0.3)
+    refs = [smooth_images(B, H, W, 72 + j, detail=0.3) for j in range(N)]
+    model = SelfSupModelMF(ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4,
+                           C2=9e-4, photometric_reduce_op="min", disp_norm=True, clip_loss=0.0,
+                           progressive_scaling=0.0, padding_mode="zeros", automask_loss=True,
+                           num_scales=4, flip_lr_prob=0.0, rotation_mode="euler", upsample_depth_maps=True,
+                           min_depth=mind, max_depth=maxd)
+    net = det_init(DepthPoseNet(version="it12-h-out", min_depth=mind, max_depth=maxd))
+    model.add_depth_net(net)
+    model.train()
+    batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
+             "intrinsics": K.clone()}
+    out = model(batch)
+    out["loss"].sum().backward()
+    save("train_step_it12h_selfsup_n4", image=img, refs=torch.stack(refs), K=K, loss=out["loss"],
+         min_depth=np.float32(mind), max_depth=np.float32(maxd),
+         **{"metric_" + k: v for k, v in out["metrics"].items()},
+         **grad_fixture(((k, q.grad) for k, q in net.named_parameters()), ("depth_head", "pose_head")))
 
 
 def gen_metrics():
@@ -510,3 +605,5 @@ if __name__ == "__main__":
         gen_full()
     if "metrics" in which:
         gen_metrics()
+    if "scannet" in which:
+        gen_scannet()

@@ -140,3 +140,101 @@ def test_two_rank_gloo_missing_gradient_on_one_rank():
         opt.step()
     ref = torch.cat([p.detach().flatten() for p in model.parameters()])
     assert torch.allclose(p0, ref, rtol=1e-5, atol=1e-6), float((p0 - ref).abs().max())
+
+
+# ---------------------------------------------------------------- in-place (direct) gradients
+_QUEUED = {}
+
+
+class _DirectConv(torch.autograd.Function):
+    """Stands in for the hip conv engine's direct path (hip/conv.py): the weight
+    gradient is queued in backward and written IN PLACE into weight.grad only
+    when flushed; autograd receives None for the weight."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return torch.nn.functional.conv2d(x, w, padding=(0, 2))
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gw = torch.nn.grad.conv2d_weight(x, w.shape, g, padding=(0, 2))
+        _QUEUED[w] = _QUEUED.get(w, 0) + gw
+        return torch.nn.grad.conv2d_input(x.shape, w, g, padding=(0, 2)), None
+
+
+def _fake_flush(p):
+    gw = _QUEUED.pop(p, None)
+    if gw is not None:
+        p.grad.add_(gw)            # the in-place accumulation into the flat view
+    return None
+
+
+class ToyDirect(Toy):
+    """Toy whose middle conv weight takes the direct (in-place) path; with a
+    tiny bucket size it shares a bucket with autograd-produced gradients."""
+
+    def forward(self, batch):
+        w = self.b.weight
+        if getattr(w, "_dro_direct", False) and w.grad is not None:
+            w._dro_direct_used = True
+            x = _DirectConv.apply(torch.relu(self.a(batch["x"])), w) + self.b.bias.view(1, -1, 1, 1)
+        else:
+            x = self.b(torch.relu(self.a(batch["x"])))
+        y = self.c(torch.relu(x).mean((2, 3)))
+        return {"loss": ((y - batch["y"]) ** 2).mean().reshape(1)}
+
+
+def _worker_direct(rank, world, port, steps, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, init_distributed
+    init_distributed("gloo")
+    torch.manual_seed(rank)
+    model = ToyDirect()
+    tr = DataParallelTrainer(model, lr=1e-2, bucket_mb=0.0005)
+    tr.grads.direct_flush = _fake_flush
+    info = []
+    for s in range(steps):
+        tr.step(data(rank, s))
+        assert not _QUEUED, "a queued in-place gradient was never flushed"
+        info.append((list(tr.grads.issued), tr.grads.issued_in_backward, len(tr.grads.buckets)))
+    mixed = [i for i, b in enumerate(tr.grads.buckets)
+             if any(getattr(p, "_dro_direct_used", False) for p in b) and
+             any(not getattr(p, "_dro_direct_used", False) for p in b)]
+    flat = torch.cat([p.detach().flatten() for p in model.parameters()])
+    out[rank] = (flat, info, mixed)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_direct_gradients_in_mixed_bucket():
+    """A weight whose gradient is written in place at flush time (not produced
+    by autograd) sharing a bucket with autograd gradients: its bucket's
+    all-reduce is issued from the backward hooks (overlapped, not deferred to
+    finish()) and only after the in-place write -- ranks stay identical and
+    equal to one process minimising the mean of the two per-rank losses."""
+    steps = 4
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_worker_direct, args=(2, port, steps, out), nprocs=2, join=True)
+        res = dict(out)
+    (p0, info0, mixed), (p1, info1, _) = res[0], res[1]
+    assert mixed, "expected the direct weight in a bucket with autograd gradients"
+    assert torch.equal(p0, p1), "ranks diverged"
+    assert [i[0] for i in info0] == [i[0] for i in info1], "collective order differs between ranks"
+    for issued, in_bwd, nb in info0[1:]:
+        assert issued == list(range(nb)) and in_bwd == nb, (issued, in_bwd, nb)
+    torch.manual_seed(0)
+    model = Toy()
+    opt = torch.optim.Adam(list(model.parameters()), lr=1e-2)
+    for s in range(steps):
+        opt.zero_grad(set_to_none=True)
+        loss = sum(0.5 * model(data(r, s))["loss"].sum() for r in range(2))
+        loss.backward()
+        opt.step()
+    ref = torch.cat([p.detach().flatten() for p in model.parameters()])
+    assert torch.allclose(p0, ref, rtol=1e-5, atol=1e-6), float((p0 - ref).abs().max())

@@ -1,0 +1,162 @@
+"""Data-parallel trainer on the real model, on the GPU.
+
+* Two ranks on ONE GPU (mp.spawn, gloo process group over CUDA tensors),
+  eager steps of DataParallelTrainer(SelfSupModelMF(DepthPoseNet it8)) with the
+  conv engine's in-place (direct, batched) weight gradients on: the ranks end
+  bit-identical, and equal (to fp32 reassociation) to one process minimising
+  the mean of the two per-rank losses -- the exact data-parallel semantics with
+  per-replica BatchNorm statistics (no SyncBN, as the reference).
+* RCCL inside a captured hipGraph: a world-size-1 "nccl" (RCCL) group with the
+  bucket all-reduces forced on (always_reduce), GraphedTrainStep replay vs the
+  eager step from the same state.
+
+Reference: horovod_trainer.py:67-69 (dormant DistributedOptimizer),
+model_wrapper.py:818-822 (DistributedSampler).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, H, W, N = 1, 64, 96, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(seed=0):
+    from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF
+    from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
+    torch.manual_seed(seed)
+    m = SelfSupModelMF(flip_lr_prob=0.0, automask_loss=True, photometric_reduce_op="min", clip_loss=0.0,
+                       smooth_loss_weight=0.001, min_depth=0.5, max_depth=80.0)
+    m.add_depth_net(DepthPoseNet(version="it8-seq4-inter-out", min_depth=0.5, max_depth=80.0))
+    return m.cuda()
+
+
+def _batch(rank, step):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    img = torch.rand(B, 3, H, W, generator=g)
+    refs = [(0.9 * torch.roll(img, 2 + j, 3) + 0.1 * torch.rand(B, 3, H, W, generator=g)) for j in range(N)]
+    K = torch.tensor([[93.0, 0.0, 47.5], [0.0, 92.0, 31.5], [0.0, 0.0, 1.0]]).repeat(B, 1, 1)
+    b = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs, "intrinsics": K}
+    return {k: (v.cuda() if torch.is_tensor(v) else [t.cuda() for t in v]) for k, v in b.items()}
+
+
+def _flat(m):
+    return torch.cat([p.detach().flatten() for p in m.parameters()]).cpu()
+
+
+def _worker(rank, world, port, steps, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.cuda.set_device(0)
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, init_distributed
+    init_distributed("gloo")
+    with torch.backends.cudnn.flags(enabled=False):     # deterministic encoder convs
+        m = _model(seed=rank)                            # rank-0 broadcast must fix this
+        tr = DataParallelTrainer(m, lr=2e-4, bucket_mb=4.0)
+        info = []
+        for s in range(steps):
+            loss, _ = tr.step(_batch(rank, s))
+            torch.cuda.synchronize()
+            info.append((float(loss), list(tr.grads.issued), tr.grads.issued_in_backward,
+                         len(tr.grads.buckets)))
+        direct = sum(bool(getattr(p, "_dro_direct_used", False)) for p in m.parameters())
+        mixed = sum(1 for b in tr.grads.buckets if any(getattr(p, "_dro_direct_used", False) for p in b)
+                    and any(not getattr(p, "_dro_direct_used", False) for p in b))
+        out[rank] = (_flat(m), info, direct, mixed)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+class _TwoHalves(torch.nn.Module):
+    """One process over both ranks' batches: mean of the per-rank losses, each
+    half through its own forward (its own BatchNorm statistics)."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = m
+
+    def forward(self, pair):
+        a, b = pair
+        return {"loss": 0.5 * (self.m(a)["loss"] + self.m(b)["loss"])}
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_one_gpu_real_model_direct_weight_grads():
+    steps = 2
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_worker, args=(2, port, steps, out), nprocs=2, join=True)
+        res = dict(out)
+    (p0, info0, direct, mixed), (p1, info1, _, _) = res[0], res[1]
+    assert direct > 20, "the conv engine's in-place weight gradients were not used"
+    assert torch.equal(p0, p1), "ranks diverged"
+    assert [i[1] for i in info0] == [i[1] for i in info1], "collective order differs between ranks"
+    for _, issued, in_bwd, nb in info0[1:]:
+        # every bucket -- including those holding in-place conv weight gradients --
+        # is issued from the backward hooks, in the common order
+        assert issued == list(range(nb)) and in_bwd == nb, (issued, in_bwd, nb)
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer
+    with torch.backends.cudnn.flags(enabled=False):
+        m = _model(seed=0)
+        tr = DataParallelTrainer(_TwoHalves(m), lr=2e-4, bucket_mb=4.0)
+        for s in range(steps):
+            tr.step((_batch(0, s), _batch(1, s)))
+        torch.cuda.synchronize()
+    ref = _flat(m)
+    err = float((p0 - ref).abs().max())
+    assert err <= 1e-6, err          # 2 Adam steps at lr 2e-4: parameters move <= 4e-4
+
+
+@pytest.mark.timeout(300)
+def test_rccl_all_reduce_inside_captured_graph():
+    """The bucket all-reduces (RCCL, forced on at world size 1) captured inside
+    the step's hipGraph: replay == eager from the same state."""
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep
+    from oracle import dro_oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        with torch.backends.cudnn.flags(enabled=False):
+            batch = _batch(0, 0)
+            K0 = batch["intrinsics"].clone()
+            m = _model()
+            tr = DataParallelTrainer(m, capturable=True, bucket_mb=4.0, always_reduce=True)
+            gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False,))
+            assert len(tr.grads.buckets) > 2 and tr.grads.issued == list(range(len(tr.grads.buckets)))
+            snap_m = {k: v.clone() for k, v in m.state_dict().items()}
+            snap_s = [{k: v.clone() for k, v in st.items()} for st in tr.optimizer.state.values()]
+
+            def restore():
+                with torch.no_grad():
+                    for k, v in m.state_dict().items():
+                        v.copy_(snap_m[k])
+                    for st, sv in zip(tr.optimizer.state.values(), snap_s):
+                        for k in st:
+                            st[k].copy_(sv[k])
+                batch["intrinsics"].copy_(K0)
+
+            restore()
+            lg = gs.step(batch, flip=False)[0].clone()
+            gg = tr.grads.flat.clone()
+            restore()
+            le = tr.step(batch, flip=False)[0].clone()
+            ge = tr.grads.flat.clone()
+            torch.cuda.synchronize()
+        assert O.rel_err(lg.cpu(), le.cpu()) < 1e-5
+        assert float((gg - ge).norm() / ge.norm()) < 1e-4
+    finally:
+        dist.destroy_process_group()

@@ -9,7 +9,7 @@ from types import SimpleNamespace
 import pytest
 import torch
 
-from common import load_fixture
+from common import fval, load_fixture
 from oracle import dro_oracle as O
 
 G = os.path.join(os.path.dirname(__file__), "golden")
@@ -36,7 +36,7 @@ def test_depth_metrics_golden(name, scaled):
     from dro_sfm_amd.utils.depth import compute_depth_metrics
     d = load_fixture(os.path.join(G, name + ".npz"))
     cfg = SimpleNamespace(crop={0: "", 1: "garg", 2: "eigen_nyu"}[int(d["crop"])],
-                          min_depth=float(d["min_depth"]), max_depth=float(d["max_depth"]))
+                          min_depth=fval(d["min_depth"]), max_depth=fval(d["max_depth"]))
     out = compute_depth_metrics(cfg, d["gt"].cuda(), d["pred"].cuda(), use_gt_scale=scaled)
     want = d["metrics_scaled" if scaled else "metrics_unscaled"]
     assert out.is_cuda and out.shape == (9,)

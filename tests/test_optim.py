@@ -2,6 +2,8 @@
 torch.optim.Adam: identical updates (GPU), a learning-rate schedule followed
 by a captured graph (GPU), and the per-parameter state_dict layout the
 reference writes into its checkpoints (model_checkpoint.py:76), both ways."""
+import copy
+
 import pytest
 import torch
 
@@ -150,3 +152,52 @@ def test_flat_adam_lr_schedule_reaches_captured_graph():
         sched_ref.step()
         sched.step()
     assert opt.hyper_t[0].item() == pytest.approx(1e-6, rel=1e-5)
+
+
+@pytest.mark.gpu
+def test_trainer_adam_state_indexes_all_parameters_with_frozen():
+    """The trainer's FlatAdam numbers ALL module parameters, as the reference's
+    Adam group over depth_net.parameters() (model_wrapper.py:173): a frozen
+    parameter keeps its index and no state; the saved group is capturable=False
+    and loads into torch.optim.Adam over model.parameters(), which then
+    continues identically."""
+    import torch.nn as nn
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.ReLU(), nn.Conv2d(8, 8, 3, padding=1),
+                          nn.ReLU(), nn.Conv2d(8, 4, 1)).cuda()
+    model[2].weight.requires_grad_(False)                    # frozen, in the middle
+    twin = copy.deepcopy(model)
+
+    class M(nn.Module):
+        def __init__(self, net):
+            super().__init__()
+            self.net = net
+
+        def forward(self, batch):
+            return {"loss": self.net(batch["x"]).pow(2).mean().reshape(1)}
+
+    tr = DataParallelTrainer(M(model), lr=1e-3)
+    g = torch.Generator().manual_seed(3)
+    xs = [torch.randn(2, 3, 8, 8, generator=g).cuda() for _ in range(5)]
+    for x in xs[:3]:
+        tr.step({"x": x})
+    sd = tr.optimizer.state_dict()
+    names = [n for n, _ in model.named_parameters()]
+    assert sd["param_groups"][0]["params"] == list(range(len(names)))
+    assert sd["param_groups"][0]["capturable"] is False
+    assert names.index("2.weight") not in sd["state"] and len(sd["state"]) == len(names) - 1
+    # torch.optim.Adam over the same module, loaded mid-run, continues identically
+    with torch.no_grad():
+        for a, b in zip(twin.parameters(), model.parameters()):
+            a.copy_(b)
+    ref = torch.optim.Adam(twin.parameters(), lr=1.0)
+    ref.load_state_dict(sd)
+    for x in xs[3:]:
+        tr.step({"x": x})
+        ref.zero_grad(set_to_none=True)
+        twin(x).pow(2).mean().backward()
+        ref.step()
+    torch.cuda.synchronize()
+    for (n, a), b in zip(model.named_parameters(), twin.parameters()):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-7), n

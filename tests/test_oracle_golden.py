@@ -9,7 +9,7 @@ import os
 import pytest
 import torch
 
-from common import load_fixture, load_spec, params_from_spec  # tests/golden on sys.path
+from common import fval, grad_errors, load_fixture, load_spec, params_from_spec  # tests/golden on sys.path
 from oracle import dro_oracle as O
 
 G = os.path.join(os.path.dirname(__file__), "golden")
@@ -40,7 +40,7 @@ def test_depth_cost(name):
     fmap = d["fmap"].clone().requires_grad_(True)
     frefs = [f.clone().requires_grad_(True) for f in d["fmap_ref"]]
     poses = list(d["poses"])
-    inv = O.disp_to_depth(disp, float(d["min_depth"]), float(d["max_depth"]))
+    inv = O.disp_to_depth(disp, fval(d["min_depth"]), fval(d["max_depth"]))
     cost = O.depth_cost_calc(inv, fmap, frefs, poses, d["K"], d["K"], 1.0 / 8)
     assert O.rel_err(cost, d["cost"]) < TOL
     (cost * d["G"]).sum().backward()
@@ -54,7 +54,7 @@ def test_plane_sweep():
     B, C, h, w = d["fmap"].shape
     vol = []
     for v in d["disp"]:
-        inv = O.disp_to_depth(torch.full((B, 1, h, w), float(v)), float(d["min_depth"]), float(d["max_depth"]))
+        inv = O.disp_to_depth(torch.full((B, 1, h, w), float(v)), fval(d["min_depth"]), fval(d["max_depth"]))
         vol.append(O.get_cost_each(d["pose"], d["fmap"], d["fmap_ref"], O.inv2depth(inv), d["K"], d["K"], 1 / 8))
     assert O.rel_err(torch.stack(vol, 1), d["cost"]) < TOL
 
@@ -78,7 +78,7 @@ def test_ssim():
     assert O.rel_err(x.grad, d["g_x"]) < 1e-4
 
 
-@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean"])
+@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean", "photo_loss_n4"])
 def test_photometric_loss(name):
     d = fx(name)
     invs = [i.clone().requires_grad_(True) for i in d["inv_depths"]]
@@ -105,7 +105,7 @@ def test_supervised_loss():
     gt = d["gt_depth"]
     gt_inv = torch.where(gt <= 0, torch.zeros_like(gt), 1.0 / gt.clamp(min=1e-6))
     out = O.supervised_depth_pose_loss(invs, gt_inv, [d["gt_poses"][:, j] for j in range(N)], poses,
-                                       d["K"], d["K"], float(d["min_depth"]), float(d["max_depth"]))
+                                       d["K"], d["K"], fval(d["min_depth"]), fval(d["max_depth"]))
     assert O.rel_err(out["loss"], d["loss"]) < TOL
     assert O.rel_err(out["depth_loss"], d["depth_loss"]) < TOL
     assert O.rel_err(out["pose_loss"], d["pose_loss"]) < TOL
@@ -191,7 +191,7 @@ def test_update_block_pose():
 def test_depth_pose_net(tag, version):
     d = fx(f"depthposenet_{tag}")
     p = spec_params(f"depthposenet_{tag}")
-    mind, maxd = float(d["min_depth"]), float(d["max_depth"])
+    mind, maxd = fval(d["min_depth"]), fval(d["max_depth"])
     with torch.no_grad():
         invs, poses = O.depth_pose_net(dict(p), version, mind, maxd, d["image"], list(d["refs"]),
                                        d["K"], training=True)
@@ -210,7 +210,7 @@ def test_train_step(tag, version, kind):
     d = fx(f"train_step_{tag}")
     dn = fx(f"depthposenet_{tag}")
     p = spec_params(f"depthposenet_{tag}", grad=True)
-    mind, maxd = float(dn["min_depth"]), float(dn["max_depth"])
+    mind, maxd = fval(dn["min_depth"]), fval(dn["max_depth"])
     N = d["refs"].shape[0]
     batch = {"rgb": d["image"], "rgb_context": list(d["refs"]), "rgb_original": d["image"],
              "rgb_context_original": list(d["refs"]), "intrinsics": d["K"], "depth": d["gt_depth"],
@@ -235,7 +235,7 @@ def test_depth_metrics(name, scaled):
     (garg crop + upsampled prediction; no crop; an image without valid pixels)."""
     d = load_fixture(os.path.join(G, name + ".npz"))
     crop = {0: "", 1: "garg", 2: "eigen_nyu"}[int(d["crop"])]
-    out = O.depth_metrics(d["gt"], d["pred"], float(d["min_depth"]), float(d["max_depth"]), crop, scaled)
+    out = O.depth_metrics(d["gt"], d["pred"], fval(d["min_depth"]), fval(d["max_depth"]), crop, scaled)
     assert torch.equal(out, d["metrics_scaled" if scaled else "metrics_unscaled"])
 
 
@@ -249,3 +249,69 @@ def test_resize_matches_pillow(shape):
     a = np.random.default_rng(h0).integers(0, 256, (h0, w0, 3), dtype=np.uint8)
     want = np.asarray(Image.fromarray(a).resize((W, H), Image.BILINEAR))
     assert np.array_equal(O.resize_bilinear_pil(a, H, W), want)
+
+
+def _train_step_oracle(spec_name, version, mind, maxd, batch, kind, dt, flip=False):
+    p = spec_params(spec_name)
+    p = {k: (v.to(dt).requires_grad_(True) if v.is_floating_point() and "running" not in k
+             else (v.to(dt) if v.is_floating_point() else v)) for k, v in p.items()}
+    b = {k: (v.to(dt) if torch.is_tensor(v) and v.is_floating_point() else
+             ([t.to(dt) for t in v] if isinstance(v, list) else v)) for k, v in batch.items()}
+    out = O.train_step_loss(p, version, mind, maxd, b, kind=kind, flip=flip)
+    out["loss"].sum().backward()
+    return out, [(k, v.grad) for k, v in p.items() if getattr(v, "grad", None) is not None]
+
+
+def _grad_pin(fixture, g32, g64, floor=2e-5, frac=0.1):
+    """Per tensor, over the fixture's stored elements: the fp32 oracle within
+    max(floor, frac x the reference fp32 gradient's own max-rel distance to
+    the fp64 oracle) of the reference.  The reference is itself that far from
+    the exact gradient (BatchNorm parameter gradients are sums with heavy
+    cancellation, the recurrent loop amplifies rounding); a restatement
+    error would show up as a fixed fraction of the gradient, not below it."""
+    e32, e64 = grad_errors(g32, fixture), grad_errors(g64, fixture)
+    assert e32.keys() == e64.keys() and len(e32) > 100
+    bad = [(k, e32[k], e64[k]) for k in e32 if e32[k] > max(floor, frac * e64[k])]
+    return bad, max(e32.values())
+
+
+@pytest.mark.parametrize("flip", [False, True])
+@pytest.mark.parametrize("tag,version,kind", [("it8", "it8-seq4-inter-out", "selfsup"),
+                                              ("it12h", "it12-h-out", "sup")])
+def test_train_step_gradients_per_element(tag, version, kind, flip):
+    """Training step (SelfSupModelMF it8 / SupModelMF it12-h) without and with
+    the left-right flip forced (SfmModelMF.py:110-119: K flipped in place,
+    the loss sees it): loss 1e-5 and every parameter gradient per element
+    (it8: update blocks and heads whole; encoders at a fixed sample of 2048
+    entries per tensor) against the reference's own fixtures."""
+    d = fx(f"train_step_{tag}")
+    dn = fx(f"depthposenet_{tag}")
+    f = fx(f"train_step_{tag}_{'flip' if flip else 'grads'}")
+    mind, maxd = fval(dn["min_depth"]), fval(dn["max_depth"])
+    N = d["refs"].shape[0]
+    batch = {"rgb": d["image"], "rgb_context": list(d["refs"]), "rgb_original": d["image"],
+             "rgb_context_original": list(d["refs"]), "intrinsics": d["K"], "depth": d["gt_depth"],
+             "pose_context": [d["gt_poses"][:, j] for j in range(N)]}
+    out, g32 = _train_step_oracle(f"depthposenet_{tag}", version, mind, maxd, batch, kind, torch.float32, flip)
+    assert O.rel_err(out["loss"], f["loss"]) < 1e-5
+    if flip:
+        assert torch.equal(O.flip_lr_intr(d["K"], d["image"].shape[3]), f["K_after"])
+    _, g64 = _train_step_oracle(f"depthposenet_{tag}", version, mind, maxd, batch, kind, torch.float64, flip)
+    bad, worst = _grad_pin(f, g32, g64)
+    assert not bad, bad[:5]
+
+
+def test_train_step_selfsup_view5_n4():
+    """configs[4] model: SelfSupModelMF it12-h-out with N=4 refs (ScanNet view5,
+    depth 0.2-10) -- loss and per-element gradients vs the reference."""
+    f = fx("train_step_it12h_selfsup_n4")
+    N = f["refs"].shape[0]
+    batch = {"rgb": f["image"], "rgb_context": list(f["refs"]), "rgb_original": f["image"],
+             "rgb_context_original": list(f["refs"]), "intrinsics": f["K"]}
+    mind, maxd = fval(f["min_depth"]), fval(f["max_depth"])
+    assert N == 4
+    out, g32 = _train_step_oracle("depthposenet_it12h", "it12-h-out", mind, maxd, batch, "selfsup", torch.float32)
+    assert O.rel_err(out["loss"], f["loss"]) < 1e-5
+    _, g64 = _train_step_oracle("depthposenet_it12h", "it12-h-out", mind, maxd, batch, "selfsup", torch.float64)
+    bad, worst = _grad_pin(f, g32, g64)
+    assert not bad, bad[:5]

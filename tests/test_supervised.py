@@ -13,7 +13,7 @@ import os
 import pytest
 import torch
 
-from common import SCANNET_K_320, kitti_K, load_fixture
+from common import SCANNET_K_320, fval, kitti_K, load_fixture
 from oracle import dro_oracle as O
 
 G = os.path.join(os.path.dirname(__file__), "golden")
@@ -69,7 +69,7 @@ def test_supervised_golden(hip):
     gt_inv = _gt_inv(d["gt_depth"])
     loss, metrics, g_inv, g_pose = _run(hip, d["inv_depths"], gt_inv,
                                         [d["gt_poses"][:, j] for j in range(N)], d["poses"], d["K"],
-                                        float(d["min_depth"]), float(d["max_depth"]))
+                                        fval(d["min_depth"]), fval(d["max_depth"]))
     assert rel(loss, d["loss"]) < TOL
     assert rel(metrics[0], d["depth_loss"]) < TOL
     assert rel(metrics[1], d["pose_loss"]) < TOL
