@@ -39,6 +39,10 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
 
 #include "conv_common.hpp"
 #include "dro_common.hpp"
@@ -932,6 +936,219 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
   stamp(14);
 }
 
+// ------------------------------------------------------------------ weight gradient v2
+// dW[o, c, tap] = sum_p G[o, p] X[c, p + d(tap)]: block = 64 output x 64 input
+// channels x all taps, 8 waves (2 per SIMD), K = the pixels of a run of TH x TW
+// tiles.  Against wgrad_halo_kernel (64 x 32 channels, 4 waves): G is staged
+// once per 64 input channels instead of per 32 (half the G / y re-reads) and
+// two waves per SIMD hide the LDS -> MFMA latency the single wave left
+// exposed (profiles/r3_conv_roofline.json: 25 % of the f32 MFMA peak, 195 MB
+// fetched per 4.5 GFLOP launch).  Wave w: o half w & 1, c half (w >> 1) & 1,
+// group w >> 2 = tap group (3x3: taps 0-4 / 5-8) or pixel half (T <= 5:
+// summed through LDS at the end).  Same partials as wgrad_halo_kernel
+// ([split][Cout][Cin][T], bias [split][Cout]) and the same finish kernel.
+template <int KH, int KW>
+struct HaloShapeW2 {
+  static constexpr int T = KH * KW;
+  static constexpr bool TAPSPLIT = T == 9;
+  static constexpr int TPW = TAPSPLIT ? 5 : T;
+  static constexpr int TH = HaloShape<32, KH, KW>::TH, TW = 64 / TH;
+  static constexpr int HWd = TW + KW - 1;
+  static constexpr int HALO = (TH + KH - 1) * HWd;
+  static constexpr int HPAD = HALO | 1;
+  static constexpr int NJ = (HALO + 63) / 64;
+  static constexpr int BC = 64, GPAD = 65;
+  static constexpr int STAGE = 64 * GPAD + BC * HPAD;
+  static constexpr int RED = TAPSPLIT ? 0 : 4 * 16 * 64;        // pixel-half reduction (one tap)
+  static constexpr int LDS = 2 * STAGE > RED ? 2 * STAGE : RED;
+  static_assert(NJ <= 2 && TW % 2 == 0, "halo shape");
+};
+
+template <int KH, int KW, int GACT, bool MULTI>
+__global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T P) {
+  const IgArgs& a = WgParam<MULTI>::ig(P);
+  using S = HaloShapeW2<KH, KW>;
+  constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
+  constexpr int NJ = S::NJ, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE, TPW = S::TPW;
+  constexpr bool TAPSPLIT = S::TAPSPLIT;
+  constexpr int PH = KH / 2, PW = KW / 2;
+  __shared__ float smem[S::LDS];
+  const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
+  const int H = a.g.H, W = a.g.W, Cin = a.g.Cin, Cout = a.g.Cout;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..7
+  const int t = blockIdx.x;
+  const int ot = t % a.otiles, ct = t / a.otiles;
+  const int o0 = ot * 64, c0 = ct * BC;
+  const size_t HW = (size_t)H * W;
+  const unsigned HWu = (unsigned)HW;
+  int ntiles = a.g.B * a.tiles_img;
+  if constexpr (MULTI) ntiles = P.use_tiles * P.nuse;
+  const int tbeg = blockIdx.y * a.chunks_per_split;
+  const int tend = min(ntiles, tbeg + a.chunks_per_split);
+  const bool do_bias = a.gbias && ct == 0;
+  const float galpha = a.galpha;
+  float gr[8], yr[GACT ? 8 : 1], xr[8 * NJ], bsum[8];
+  unsigned gmask = 0, xmask = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  auto load = [&](int tile) {
+    const float* __restrict__ Gp = a.G;
+    const float* __restrict__ Yp = a.gy;
+    KSlice sbase = kernarg_srcs();
+    if constexpr (MULTI) {
+      const int u = tile / P.use_tiles;
+      tile -= u * P.use_tiles;
+      Gp = *(KFPtr)(kernarg_base() + offsetof(WgMulti, uG) + u * sizeof(FPtr));
+      if (GACT) Yp = *(KFPtr)(kernarg_base() + offsetof(WgMulti, uy) + u * sizeof(FPtr));
+      sbase = (KSlice)(kernarg_base() + offsetof(WgMulti, usrc)) + u * kMaxSrc;
+    }
+    const int b = tile / a.tiles_img, trem = tile - b * a.tiles_img;
+    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+    // G tile: lane = pixel of the tile, wave w -> output channels o0 + 8w + j
+    const int qy = lane / TW, qx = lane - qy * TW;
+    const int oy = ty0 + qy, ox = tx0 + qx;
+    const bool pin = oy < H && ox < W;
+    const unsigned pix = pin ? (unsigned)(oy * W + ox) : 0u;
+    gmask = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = o0 + wave * 8 + j;          // scalar
+      const bool ok = pin && o < Cout;
+      gmask |= ok ? (1u << j) : 0u;
+      const unsigned off = ok ? ((unsigned)b * Cout + o) * HWu + pix : 0u;
+      gr[j] = Gp[off];
+      if (GACT) yr[j] = Yp[off];
+    }
+    // X patch: wave w -> channels c0 + w + 8i, lanes over the halo
+    RowDesc ds[8];
+    bool real[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = c0 + wave + 8 * i;         // scalar
+      real[i] = ch < Cin;
+      ds[i] = row_desc_at(sbase, cb1, cb2, cb3, real[i] ? ch : 0, HWu);
+    }
+    xmask = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned xbase = (unsigned)b * ds[i].A + ds[i].Bc;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        const int hy = e / HWd, hx = e - hy * HWd;
+        const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
+        const bool ok = real[i] && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        xmask |= ok ? (1u << (i * NJ + j)) : 0u;
+        xr[i * NJ + j] = ds[i].p[ok ? xbase + (ds[i].M ? (unsigned)(yy * W + xx) : 0u) : 0u];
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    float* Gs = smem + buf * STAGE;
+    float* Xs = Gs + 64 * GPAD;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float g = (gmask >> j) & 1u ? galpha * gr[j] : 0.f;
+      if (GACT) g *= act_bwd(yr[j], GACT);
+      Gs[lane * GPAD + wave * 8 + j] = g;
+      if (do_bias) bsum[j] += g;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        if (e < HPAD) Xs[(wave + 8 * i) * HPAD + e] = (xmask >> (i * NJ + j)) & 1u ? xr[i * NJ + j] : 0.f;
+      }
+    }
+  };
+
+  const int wo = wave & 1, wc = (wave >> 1) & 1, wg = wave >> 2;
+  const int hi = lane >> 5;
+  const int tap0 = TAPSPLIT ? wg * 5 : 0;
+  const int ntap = TAPSPLIT ? (wg == 0 ? 5 : 4) : T;
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int tp = 0; tp < TPW; ++tp)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[tp][r] = 0.f;
+
+  if (tbeg < tend) {
+    load(tbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int tl = tbeg; tl < tend; ++tl) {
+    const int buf = (tl - tbeg) & 1;
+    const bool more = tl + 1 < tend;
+    if (more) load(tl + 1);
+    const float* Gs = smem + buf * STAGE;
+    const float* Xs = Gs + 64 * GPAD;
+    const float* ga = Gs + hi * GPAD + wo * 32 + (lane & 31);
+    const float* xb = Xs + (wc * 32 + (lane & 31)) * HPAD + hi;
+    constexpr int KS = TAPSPLIT ? 32 : 16;        // k-steps (pixel pairs) per wave
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int pp = 2 * ((TAPSPLIT ? 0 : wg * 16) + s);   // even pixel of this k-step
+      const float av = ga[pp * GPAD];
+      const int poff = (pp / TW) * HWd + (pp % TW);
+#pragma unroll
+      for (int k = 0; k < TPW; ++k) {
+        if (k < ntap) {
+          const int tap = tap0 + k;
+          const int ty = tap / KW, tx = tap - ty * KW;
+          acc[k] = mfma32(av, xb[poff + ty * HWd + tx], acc[k]);
+        }
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* wpart = a.part + (size_t)blockIdx.y * Cout * Cin * T;
+  const int c = c0 + wc * 32 + (lane & 31);
+  if (TAPSPLIT) {
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      if (k < ntap) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (o < Cout && c < Cin) wpart[((size_t)o * Cin + c) * T + tap0 + k] = acc[k][r];
+        }
+      }
+    }
+  } else {   // sum the pixel halves one tap at a time
+    float* red = smem;   // [4 (o half, c half)][16][64]
+    const int q4 = wo + 2 * wc;
+#pragma unroll
+    for (int tp = 0; tp < T; ++tp) {
+      if (wg == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(q4 * 16 + r) * 64 + lane] = acc[tp][r];
+      }
+      __syncthreads();
+      if (wg == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (o < Cout && c < Cin)
+            wpart[((size_t)o * Cin + c) * T + tp] = acc[tp][r] + red[(q4 * 16 + r) * 64 + lane];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = wave_sum(bsum[j]);
+      const int o = o0 + wave * 8 + j;
+      if (lane == 0 && o < Cout) a.bpart[(size_t)blockIdx.y * Cout + o] = v;
+    }
+  }
+}
+
 // dW[o][c][tap] = sum_s part[s][o][c][tap]; db[o] = sum_s bpart[s][o]
 __global__ __launch_bounds__(256) void wgrad_halo_finish_kernel(IgArgs a, int splits) {
   const int Cout = a.g.Cout;
@@ -1171,6 +1388,41 @@ WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
   return pl;
 }
 
+// weight gradient v2 (wgrad2_kernel): 64 x 64 channel tiles, one block of 8
+// waves per CU (85 KB LDS); splits fill ~`target` blocks with >= 2 pixel tiles
+// per split.  DRO_WGRAD_V1=1 keeps the wgrad_halo_kernel path (A/B).
+bool wgrad_v1() {
+  static const bool v1 = getenv("DRO_WGRAD_V1") != nullptr;
+  return v1;
+}
+
+WhPlan plan_wgrad2(int Cin, int Cout, int KH, int KW, int ntiles_total, int B, int H, int W) {
+  WhPlan pl = {};
+  pl.ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3) || (KH == 1 && KW == 1);
+  if (!pl.ok) return pl;
+  const int TH = (KW == 1 || (KH == 3 && KW == 3)) ? 8 : 4, TW = 64 / TH;
+  pl.tiles_x = (W + TW - 1) / TW;
+  pl.tiles_img = ((H + TH - 1) / TH) * pl.tiles_x;
+  const int ntiles = ntiles_total > 0 ? ntiles_total : B * pl.tiles_img;
+  pl.otiles = (Cout + 63) / 64;
+  pl.ctiles = (Cin + 63) / 64;
+  const int blocks = pl.otiles * pl.ctiles;
+  static const int target = [] {   // tuning override: DRO_WG2_TARGET_BLOCKS (default 256)
+    const char* e = getenv("DRO_WG2_TARGET_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 256;
+  }();
+  int sp = (target + blocks - 1) / blocks;
+  if (sp > 256) sp = 256;
+  if (sp > ntiles / 2) sp = ntiles / 2;
+  if (sp < 1) sp = 1;
+  pl.tiles_per_split = (ntiles + sp - 1) / sp;
+  pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
+  pl.part_bytes = align256((size_t)pl.splits * Cout * Cin * KH * KW * sizeof(float)) +
+                  align256((size_t)pl.splits * Cout * sizeof(float));
+  return pl;
+}
+
 size_t fwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   return std::max(plan_igemm(Cout, Cin, KH, KW, B, H, W).part_bytes,
                   xconv_part_bytes(Cout, Cin, KH, KW, B, H, W));
@@ -1182,8 +1434,9 @@ size_t bwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   return align256((size_t)Cout * P * sizeof(float)) +              // pre-activation gradient
          std::max(plan_igemm(Cin, Cout, KH, KW, B, H, W).part_bytes,  // data-gradient split-K
                   xconv_part_bytes(Cin, Cout, KH, KW, B, H, W)) +
-         std::max(plan_wgrad(Cin, Cout, T, P).part_bytes,           // weight-gradient partials
-                  plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).part_bytes);
+         std::max(std::max(plan_wgrad(Cin, Cout, T, P).part_bytes,  // weight-gradient partials
+                           plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).part_bytes),
+                  plan_wgrad2(Cin, Cout, KH, KW, 0, B, H, W).part_bytes);
 }
 
 bool too_big(long long B, long long C, long long HW) { return B * C * HW >= (1LL << 30); }
@@ -1414,6 +1667,28 @@ __global__ __launch_bounds__(256) void thin_dgrad_kernel(IgArgs a, int tiles_x, 
 }
 
 // thin path eligibility: 7x7, a single source of <= 8 channels, plain epilogue
+// ---- launch log (dro_conv_log_*): algorithmic FLOPs per kernel instantiation,
+// for the per-kernel roofline table (tools/conv_roofline.py).  Host side only.
+bool g_conv_log = false;
+std::mutex g_conv_log_mu;
+std::map<std::string, std::pair<long long, double>> g_conv_log_map;
+
+void conv_log(const char* name, double flops) {
+  if (!g_conv_log) return;
+  std::lock_guard<std::mutex> lk(g_conv_log_mu);
+  auto& e = g_conv_log_map[name];
+  e.first += 1;
+  e.second += flops;
+}
+
+template <typename... Ts>
+void conv_logf(double flops, const char* fmt, Ts... args) {
+  if (!g_conv_log) return;
+  char buf[160];
+  snprintf(buf, sizeof(buf), fmt, args...);
+  conv_log(buf, flops);
+}
+
 template <int MODE, int EPI>
 bool thin_ok(const IgArgs& a) {
   if (EPI != 0 || a.g.KH != kThinK || a.g.KW != kThinK || a.g.B > 65535) return false;
@@ -1426,7 +1701,9 @@ bool thin_ok(const IgArgs& a) {
 template <int MODE, int ACT>
 int launch_thin(IgArgs& a, int max_splits, hipStream_t s) {
   const int tiles_x = (a.g.W + 7) / 8, tiles = tiles_x * ((a.g.H + 7) / 8);
+  const double flops = 2.0 * a.rows * a.kch * a.g.KH * a.g.KW * (double)a.g.B * a.g.H * a.g.W;
   if (MODE == 0) {
+    conv_logf(flops, "thin_fwd_kernel<%d>", ACT);
     hipLaunchKernelGGL((thin_fwd_kernel<ACT>), dim3(tiles, (a.g.Cout + 15) / 16, a.g.B), dim3(256), 0,
                        s, a, tiles_x);
     return launch_status("thin_fwd_kernel launch failed");
@@ -1437,6 +1714,7 @@ int launch_thin(IgArgs& a, int max_splits, hipStream_t s) {
   const int cps = (a.g.Cout + splits - 1) / splits;
   if (splits == 1) a.part = nullptr;
   const dim3 grid(tiles, splits, a.g.B);
+  conv_logf(flops, "thin_dgrad_kernel<%d, %d>", ACT, a.rows == 1 ? 1 : a.rows == 2 ? 2 : a.rows <= 4 ? 4 : 8);
   if (a.rows == 1)
     hipLaunchKernelGGL((thin_dgrad_kernel<ACT, 1>), grid, dim3(256), 0, s, a, tiles_x, cps);
   else if (a.rows == 2)
@@ -1478,6 +1756,11 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   a.chunks_per_split = pl.chunks_per_split;
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
   const dim3 grid(pl.row_tiles * pl.ptiles, pl.ksplit);
+  const double flops = 2.0 * a.rows * a.kch * a.g.KH * a.g.KW * (double)P;
+  if (pl.halo)
+    conv_logf(flops, "dconv_kernel<%d, %d, %d, %d, %d, %d, %d>", pl.bm, a.g.KH, a.g.KW, MODE, ACT, EPI, pl.kin);
+  else
+    conv_logf(flops, "igemm_kernel<%d, %d, %d, %d>", pl.bm, MODE, ACT, EPI);
   if (pl.halo) {
     a.TH = pl.TH;
     a.TW = pl.TW;
@@ -1575,6 +1858,30 @@ extern "C" int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, 
                            (long long)pl.lds_bytes, (long long)pl.part_bytes, pl.kin};
   for (int i = 0; i < 16; ++i) info[i] = v[i];
   return DRO_OK;
+}
+
+extern "C" int dro_conv_log(int enable) {
+  std::lock_guard<std::mutex> lk(g_conv_log_mu);
+  g_conv_log = enable != 0;
+  if (enable) g_conv_log_map.clear();
+  return DRO_OK;
+}
+
+extern "C" long long dro_conv_log_read(char* buf, long long cap) {
+  std::lock_guard<std::mutex> lk(g_conv_log_mu);
+  std::string out;
+  for (const auto& kv : g_conv_log_map) {
+    char line[256];
+    snprintf(line, sizeof(line), "%s\t%lld\t%.17g\n", kv.first.c_str(), kv.second.first, kv.second.second);
+    out += line;
+  }
+  const long long n = (long long)out.size();
+  if (buf && cap > 0) {
+    const long long m = n < cap - 1 ? n : cap - 1;
+    memcpy(buf, out.data(), (size_t)m);
+    buf[m] = 0;
+  }
+  return n;
 }
 
 extern "C" int dro_debug_conv_stamps(void* buffer) {
@@ -1766,7 +2073,30 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     DRO_ACT_SWITCH(gact, st = (launch_igemm<1, A_, 0>(a, P, ws_ig, s)));
     if (st) return st;
   }
-  if (grad_weight && wh.ok) {
+  if (grad_weight && wh.ok && !wgrad_v1()) {
+    const WhPlan w2 = plan_wgrad2(a.g.Cin, Cout, KH, KW, 0, B, H, W);
+    a.otiles = w2.otiles;
+    a.tiles_x = w2.tiles_x;
+    a.tiles_img = w2.tiles_img;
+    a.chunks_per_split = w2.tiles_per_split;
+    a.part = reinterpret_cast<float*>(ws_wg);
+    a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)w2.splits * Cout * a.g.Cin * T * sizeof(float)));
+    const dim3 grid((unsigned)(w2.otiles * w2.ctiles), (unsigned)w2.splits);
+    const int gact = fold ? act : 0;
+    conv_logf(2.0 * Cout * a.g.Cin * T * (double)P, "wgrad2_kernel<%d, %d, %d, false>", KH, KW, gact);
+#define DRO_WG2(KH_, KW_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad2_kernel<KH_, KW_, A_, false>), grid, dim3(512), 0, s, a))
+    if (KH == 1 && KW == 1) { DRO_WG2(1, 1); }
+    else if (KH == 1) { DRO_WG2(1, 5); }
+    else if (KW == 1) { DRO_WG2(5, 1); }
+    else { DRO_WG2(3, 3); }
+#undef DRO_WG2
+    if ((st = launch_status("wgrad2_kernel launch failed"))) return st;
+    const long long total = (long long)Cout * a.g.Cin * T;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, w2.splits);
+    if ((st = launch_status("wgrad_halo_finish_kernel launch failed"))) return st;
+  } else if (grad_weight && wh.ok) {
     a.otiles = wh.otiles;
     a.tiles_x = wh.tiles_x;
     a.tiles_img = wh.tiles_img;
@@ -1775,6 +2105,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)wh.splits * Cout * a.g.Cin * T * sizeof(float)));
     const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
     const int gact = fold ? act : 0;
+    conv_logf(2.0 * Cout * a.g.Cin * T * (double)P, "wgrad_halo_kernel<%d, %d, %d, false>", KH, KW, gact);
 #define DRO_WH(KH_, KW_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_, false>), grid, dim3(256), 0, s, a))
     if (KH == 1 && KW == 1) { DRO_WH(1, 1); }
     else if (KH == 1) { DRO_WH(1, 5); }
@@ -1793,6 +2124,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.otiles = pl.otiles;
     a.pchunk = pl.pchunk;
     a.part = reinterpret_cast<float*>(ws_wg);
+    conv_log("wgrad_kernel(", 2.0 * Cout * a.g.Cin * T * (double)P);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits),
                        dim3(256), 0, s, a);
     if ((st = launch_status("wgrad_kernel launch failed"))) return st;
@@ -1837,6 +2169,10 @@ static WhPlan plan_wgrad_multi(int Cin, int Cout, int KH, int KW, int nuse, int 
 extern "C" size_t dro_conv2d_weight_grad_multi_workspace_bytes(int nuse, int B, int H, int W, int Cin,
                                                               int Cout, int KH, int KW) {
   if (nuse < 1) nuse = 1;
+  if (!wgrad_v1()) {
+    const WhPlan t = plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W);
+    return plan_wgrad2(Cin, Cout, KH, KW, nuse * B * t.tiles_img, B, H, W).part_bytes;
+  }
   return plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W).part_bytes;
 }
 
@@ -1879,7 +2215,10 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
     m.uy[u] = act ? uses[u].y : nullptr;
   }
   const int Cin = m.a.g.Cin, T = KH * KW;
-  const WhPlan wh = plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W);
+  const bool v2 = !wgrad_v1();
+  const WhPlan wh = v2 ? plan_wgrad2(Cin, Cout, KH, KW,
+                                     nuse * B * plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).tiles_img, B, H, W)
+                       : plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W);
   if (!wh.ok) {
     set_error("conv2d_weight_grad_multi: kernel shape not supported (1x1, 1x5, 5x1, 3x3)");
     return DRO_E_SHAPE;
@@ -1909,12 +2248,23 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
   }
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
+  conv_logf(2.0 * Cout * Cin * T * (double)B * H * W * nuse, v2 ? "wgrad2_kernel<%d, %d, %d, true>"
+            : "wgrad_halo_kernel<%d, %d, %d, true>", KH, KW, act);
+  if (v2) {
+#define DRO_WG2M(KH_, KW_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad2_kernel<KH_, KW_, A_, true>), grid, dim3(512), 0, s, m))
+    if (KH == 1 && KW == 1) { DRO_WG2M(1, 1); }
+    else if (KH == 1) { DRO_WG2M(1, 5); }
+    else if (KW == 1) { DRO_WG2M(5, 1); }
+    else { DRO_WG2M(3, 3); }
+#undef DRO_WG2M
+  } else {
 #define DRO_WHM(KH_, KW_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_, true>), grid, dim3(256), 0, s, m))
-  if (KH == 1 && KW == 1) { DRO_WHM(1, 1); }
-  else if (KH == 1) { DRO_WHM(1, 5); }
-  else if (KW == 1) { DRO_WHM(5, 1); }
-  else { DRO_WHM(3, 3); }
+    if (KH == 1 && KW == 1) { DRO_WHM(1, 1); }
+    else if (KH == 1) { DRO_WHM(1, 5); }
+    else if (KW == 1) { DRO_WHM(5, 1); }
+    else { DRO_WHM(3, 3); }
 #undef DRO_WHM
+  }
   if ((st = launch_status("wgrad_halo_kernel<multi> launch failed"))) return st;
   const long long total = (long long)Cout * Cin * T;
   long long blocks = (total + 255) / 256;

@@ -19,7 +19,7 @@ int launch_status(const char* what);
 int launch_zero(float* p, size_t n, hipStream_t s);
 // Sums per-workgroup pose partials [npose, nblk, 12] (dL/dR row-major, dL/dt)
 // in a fixed order and writes the pose gradient in its own encoding.
-int launch_pose_finalize(const float* partial, int nblk, int npose, const float* pose,
+int launch_pose_finalize(const double* partial, int nblk, int npose, const float* pose,
                          int pose_mode, float* gpose, hipStream_t s);
 
 // ---------------------------------------------------------------- intrinsics
@@ -86,7 +86,8 @@ __device__ __forceinline__ void load_pose(const float* __restrict__ p, int mode,
   }
 }
 
-__device__ __forceinline__ void mat3_mul(const float A[9], const float B[9], float C[9]) {
+template <typename T>
+__device__ __forceinline__ void mat3_mul(const T A[9], const T B[9], T C[9]) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -139,6 +140,55 @@ __device__ __forceinline__ void store_pose_grad(const float* __restrict__ p, int
       out[4 * r + 1] = gR[3 * r + 1];
       out[4 * r + 2] = gR[3 * r + 2];
       out[4 * r + 3] = gt[r];
+    }
+  }
+}
+
+// fp64 variant: the contraction of the summed R-gradient with dR/d(euler)
+// cancels (see block_sum_d); sums and chain in double, stored as float.
+__device__ __forceinline__ void store_pose_grad_d(const float* __restrict__ p, int mode,
+                                                  const double gR[9], const double gt[3],
+                                                float* __restrict__ out) {
+  if (mode == DRO_POSE_EULER) {
+    out[0] = (float)gt[0];
+    out[1] = (float)gt[1];
+    out[2] = (float)gt[2];
+    double sx, cx, sy, cy, sz, cz;
+    sincos((double)p[3], &sx, &cx);
+    sincos((double)p[4], &sy, &cy);
+    sincos((double)p[5], &sz, &cz);
+    const double Rx[9] = {1, 0, 0, 0, cx, -sx, 0, sx, cx};
+    const double Ry[9] = {cy, 0, sy, 0, 1, 0, -sy, 0, cy};
+    const double Rz[9] = {cz, -sz, 0, sz, cz, 0, 0, 0, 1};
+    const double dRx[9] = {0, 0, 0, 0, -sx, -cx, 0, cx, -sx};
+    const double dRy[9] = {-sy, 0, cy, 0, 0, 0, -cy, 0, -sy};
+    const double dRz[9] = {-sz, -cz, 0, cz, -sz, 0, 0, 0, 0};
+    double T0[9], T1[9], D[9];
+    mat3_mul(dRx, Ry, T0);
+    mat3_mul(T0, Rz, D);
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s += gR[i] * D[i];
+    out[3] = (float)s;
+    mat3_mul(Rx, dRy, T0);
+    mat3_mul(T0, Rz, D);
+    s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s += gR[i] * D[i];
+    out[4] = (float)s;
+    mat3_mul(Rx, Ry, T1);
+    mat3_mul(T1, dRz, D);
+    s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s += gR[i] * D[i];
+    out[5] = (float)s;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      out[4 * r + 0] = (float)gR[3 * r + 0];
+      out[4 * r + 1] = (float)gR[3 * r + 1];
+      out[4 * r + 2] = (float)gR[3 * r + 2];
+      out[4 * r + 3] = (float)gt[r];
     }
   }
 }
@@ -294,6 +344,39 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* scratch) {
       float s = 0.f;
       for (int i = 0; i < nw; ++i) s += scratch[k * nw + i];
       v[k] = s;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Block-wide sum of NV per-thread values accumulated in fp64 (pose-gradient
+// partials: the per-pixel terms R-gradient = sum_p gP X^T cancel heavily, and
+// the euler chain contracts them again -- fp32 sums of ~10^4 terms put
+// errors of ~1e-3 of the largest component on the small ones).  Result in
+// `out` of thread 0.  `scratch` holds NV * (blockDim.x / 64) doubles.
+template <int NV>
+__device__ __forceinline__ void block_sum_d(const float (&v)[NV], double (&out)[NV], double* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) out[k] = wave_sum_d((double)v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) scratch[k * nw + wid] = out[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double s = 0.0;
+      for (int i = 0; i < nw; ++i) s += scratch[k * nw + i];
+      out[k] = s;
     }
   }
   __syncthreads();

@@ -58,7 +58,7 @@ struct PhotoArgs {
   float* U;         // [n,B,2]
   float* part_ph;   // [n,B,tiles]
   float* part_sm;   // [n,B,tiles,2]
-  float* part_pose; // [N,n,B,tiles,12]
+  double* part_pose; // [N,n,B,tiles,12] fp64 (block_sum_d)
 };
 
 __device__ __forceinline__ int reflect_idx(int y, int H) {
@@ -390,11 +390,6 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
 // Per (i,b) one wave sums the tile partials (strided lanes, then a fixed
 // shuffle tree: deterministic); the inverse-depth mean (inv_depths_normalize,
 // utils/depth.py:147-163: clamp 1e-6) normalises the smoothness sums.
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 __global__ __launch_bounds__(1024) void photo_finalize_kernel(PhotoArgs a, float* __restrict__ out) {
   __shared__ double ph[64], sx[64], sy[64];
@@ -451,16 +446,16 @@ __global__ __launch_bounds__(1024) void photo_finalize_kernel(PhotoArgs a, float
 }
 
 // ------------------------------------------------------------------ backward tile kernel
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
                                                              float* __restrict__ ginv) {
   constexpr int PL2 = H2 * W2;  // est / tgt with 2-px halo
   constexpr int PL1 = H1 * W1;  // adjoint image with 1-px halo
   __shared__ float tgt[3 * PL2];
   __shared__ float est[3 * PL2];
-  __shared__ float adj[9 * PL1];  // per channel: dL/dmu_x, dL/dE[x^2], dL/dE[xy]
+  __shared__ float adj[3 * PL1];  // one channel: dL/dmu_x, dL/dE[x^2], dL/dE[xy]
   __shared__ unsigned char selt[PL1];
   __shared__ float invt[PL2];
-  __shared__ float scratch[12 * (kThreads / kWave)];
+  __shared__ double dscratch[12 * (kThreads / kWave)];
 
   int tile, ib;
   block_tile(a, tile, ib);
@@ -504,46 +499,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
     if (j) __syncthreads();
     stage_warp<PL2, W2, 2>(a, ctx, invt, ki, kr, R, t, x0, y0, est);
     __syncthreads();
-    // adjoint of the SSIM term at every real pixel of the tile + 1-px ring
-    for (int k = threadIdx.x; k < PL1; k += kThreads) {
-      const int ly = k / W1, lx = k % W1;
-      const bool on = a.reduce_min ? (selt[k] == kw) : (y0 + ly - 1 >= 0 && y0 + ly - 1 < H &&
-                                                        x0 + lx - 1 >= 0 && x0 + lx - 1 < W);
-      const int o2 = (ly + 1) * W2 + (lx + 1);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        float A = 0.f, Bv = 0.f, Cv = 0.f;
-        if (on) {
-          const SsimStats s = pool3(est + c * PL2, tgt + c * PL2, o2, W2);
-          const float mxy = s.mx * s.my, mxx = s.mx * s.mx, myy = s.my * s.my;
-          const float v1 = 2.f * (s.sxy - mxy) + a.C2;
-          const float v2 = (s.sxx - mxx) + (s.syy - myy) + a.C2;
-          const float num = (2.f * mxy + a.C1) * v1, den = (mxx + myy + a.C1) * v2;
-          const float ssim = num / den;
-          const float lval = (1.f - ssim) / 2.f;
-          const float S = (lval >= 0.f && lval <= 1.f) ? gsel * (a.ssim_w / 3.f) * -0.5f : 0.f;
-          const float dn = S / den, dd = -S * ssim / den;
-          const float g_v1 = dn * (2.f * mxy + a.C1);
-          const float g_v2 = dd * (mxx + myy + a.C1);
-          const float g_mxy = dn * 2.f * v1 - g_v1 * 2.f;
-          const float g_mxx = dd * v2 - g_v2;
-          A = 2.f * s.mx * g_mxx + s.my * g_mxy;
-          Bv = g_v2;
-          Cv = 2.f * g_v1;
-        }
-        adj[(3 * c + 0) * PL1 + k] = A;
-        adj[(3 * c + 1) * PL1 + k] = Bv;
-        adj[(3 * c + 2) * PL1 + k] = Cv;
-      }
-    }
-    __syncthreads();
-    float acc[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) acc[k] = 0.f;
-    // (1) projections and bilinear taps of the thread's pixels, all their
-    // context gathers issued before the LDS adjoint sums below consume time
-    // Only the bilinear derivative terms stay live (6 floats per pixel); the
-    // projection is recomputed for the chain rule in (3).
+    // (1) projections and bilinear taps of the thread's pixels: only the
+    // bilinear derivative terms stay live (6 floats per pixel); the projection
+    // is recomputed for the chain rule in (3).  Their context gathers are in
+    // flight while the first adjoint plane is formed.
     float dxc[kPxPerThread][3], dyc[kPxPerThread][3];
 #pragma unroll
     for (int r = 0; r < kPxPerThread; ++r) {
@@ -568,92 +527,120 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
         dyc[r][c] = (v[2] - v[0]) * omx + (v[3] - v[1]) * T.tx;
       }
     }
+    float gix[kPxPerThread], giy[kPxPerThread];
 #pragma unroll
-    for (int r = 0; r < kPxPerThread; ++r) {
-      const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
-      const int gy = y0 + ly, gx = x0 + lx;
-      if (gy >= H || gx >= W) continue;
-      const int o2 = (ly + 2) * W2 + (lx + 2);
-      const int o1 = (ly + 1) * W1 + (lx + 1);
-      const bool self_on = a.reduce_min ? (selt[o1] == kw) : true;
-      // (2) adjoint of the 3x3 average pools: sum over the real pixels whose
-      // (reflected) windows tap this pixel.  Pixels >= 2 from every border
-      // see exactly the 3x3 neighbourhood (same summation order as the
-      // general path, which handles the reflected taps explicitly).
-      float sA[3], sB[3], sC[3];
-      if (gy >= 2 && gy <= H - 3 && gx >= 2 && gx <= W - 3) {
+    for (int r = 0; r < kPxPerThread; ++r) gix[r] = giy[r] = 0.f;
+    // one channel at a time: its adjoint plane (3 x PL1 floats of LDS instead
+    // of 9 x PL1 for all three: 4 blocks per CU instead of 3), then the
+    // gather of every real pixel's d(loss)/d(warped value) of that channel
+#pragma unroll 1
+    for (int c = 0; c < 3; ++c) {
+      if (c) __syncthreads();                  // the previous channel's gathers are done
+      // adjoint of the SSIM term of channel c at every real pixel of the tile + 1-px ring
+      for (int k = threadIdx.x; k < PL1; k += kThreads) {
+        const int ly = k / W1, lx = k % W1;
+        const bool on = a.reduce_min ? (selt[k] == kw) : (y0 + ly - 1 >= 0 && y0 + ly - 1 < H &&
+                                                          x0 + lx - 1 >= 0 && x0 + lx - 1 < W);
+        const int o2 = (ly + 1) * W2 + (lx + 1);
+        float A = 0.f, Bv = 0.f, Cv = 0.f;
+        if (on) {
+          const SsimStats s = pool3(est + c * PL2, tgt + c * PL2, o2, W2);
+          const float mxy = s.mx * s.my, mxx = s.mx * s.mx, myy = s.my * s.my;
+          const float v1 = 2.f * (s.sxy - mxy) + a.C2;
+          const float v2 = (s.sxx - mxx) + (s.syy - myy) + a.C2;
+          const float num = (2.f * mxy + a.C1) * v1, den = (mxx + myy + a.C1) * v2;
+          const float rden = 1.f / den;
+          const float ssim = num * rden;
+          const float lval = (1.f - ssim) / 2.f;
+          const float S = (lval >= 0.f && lval <= 1.f) ? gsel * (a.ssim_w / 3.f) * -0.5f : 0.f;
+          const float dn = S * rden, dd = -S * ssim * rden;
+          const float g_v1 = dn * (2.f * mxy + a.C1);
+          const float g_v2 = dd * (mxx + myy + a.C1);
+          const float g_mxy = dn * 2.f * v1 - g_v1 * 2.f;
+          const float g_mxx = dd * v2 - g_v2;
+          A = 2.f * s.mx * g_mxx + s.my * g_mxy;
+          Bv = g_v2;
+          Cv = 2.f * g_v1;
+        }
+        adj[0 * PL1 + k] = A;
+        adj[1 * PL1 + k] = Bv;
+        adj[2 * PL1 + k] = Cv;
+      }
+      __syncthreads();
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+      for (int r = 0; r < kPxPerThread; ++r) {
+        const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
+        const int gy = y0 + ly, gx = x0 + lx;
+        if (gy >= H || gx >= W) continue;
+        const int o2 = (ly + 2) * W2 + (lx + 2);
+        const int o1 = (ly + 1) * W1 + (lx + 1);
+        // (2) adjoint of the 3x3 average pools: sum over the real pixels whose
+        // (reflected) windows tap this pixel.  Pixels >= 2 from every border
+        // see exactly the 3x3 neighbourhood (same summation order as the
+        // general path, which handles the reflected taps explicitly).
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        if (gy >= 2 && gy <= H - 3 && gx >= 2 && gx <= W - 3) {
 #pragma unroll
           for (int u = 0; u < 3; ++u)
 #pragma unroll
             for (int v = 0; v < 3; ++v) {
               const int kk = (ly + u) * W1 + (lx + v);
-              s0 += adj[(3 * c + 0) * PL1 + kk];
-              s1 += adj[(3 * c + 1) * PL1 + kk];
-              s2 += adj[(3 * c + 2) * PL1 + kk];
+              s0 += adj[0 * PL1 + kk];
+              s1 += adj[1 * PL1 + kk];
+              s2 += adj[2 * PL1 + kk];
             }
-          sA[c] = s0;
-          sB[c] = s1;
-          sC[c] = s2;
-        }
-      } else {
-        int rows[4], nr = 0, cols[4], nc = 0;
-        for (int d = -1; d <= 1; ++d) {
-          if (gy + d >= 0 && gy + d < H) rows[nr++] = ly + 1 + d;
-          if (gx + d >= 0 && gx + d < W) cols[nc++] = lx + 1 + d;
-        }
-        if (gy == 1) rows[nr++] = ly;              // row 0's tap at -1 reflects to 1
-        if (gy == H - 2) rows[nr++] = ly + 2;      // row H-1's tap at H reflects to H-2
-        if (gx == 1) cols[nc++] = lx;
-        if (gx == W - 2) cols[nc++] = lx + 2;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        } else {
+          int rows[4], nr = 0, cols[4], nc = 0;
+          for (int d = -1; d <= 1; ++d) {
+            if (gy + d >= 0 && gy + d < H) rows[nr++] = ly + 1 + d;
+            if (gx + d >= 0 && gx + d < W) cols[nc++] = lx + 1 + d;
+          }
+          if (gy == 1) rows[nr++] = ly;              // row 0's tap at -1 reflects to 1
+          if (gy == H - 2) rows[nr++] = ly + 2;      // row H-1's tap at H reflects to H-2
+          if (gx == 1) cols[nc++] = lx;
+          if (gx == W - 2) cols[nc++] = lx + 2;
           for (int u = 0; u < nr; ++u)
             for (int v = 0; v < nc; ++v) {
               const int kk = rows[u] * W1 + cols[v];
-              s0 += adj[(3 * c + 0) * PL1 + kk];
-              s1 += adj[(3 * c + 1) * PL1 + kk];
-              s2 += adj[(3 * c + 2) * PL1 + kk];
+              s0 += adj[0 * PL1 + kk];
+              s1 += adj[1 * PL1 + kk];
+              s2 += adj[2 * PL1 + kk];
             }
-          sA[c] = s0;
-          sB[c] = s1;
-          sC[c] = s2;
         }
-      }
-      float gest[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
         const float xv = est[c * PL2 + o2], yv = tgt[c * PL2 + o2];
-        float ge = (sA[c] + 2.f * xv * sB[c] + yv * sC[c]) / 9.f;
-        if (self_on) {
+        float ge = (s0 + 2.f * xv * s1 + yv * s2) * (1.f / 9.f);
+        if (a.reduce_min ? (selt[o1] == kw) : true) {
           const float df = xv - yv;
           const float sg = df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f);
           ge += gsel * (a.l1_w / 3.f) * sg;
         }
-        gest[c] = ge;
+        // (3a) chain through the bilinear sample, channel by channel
+        gix[r] += ge * dxc[r][c];
+        giy[r] += ge * dyc[r][c];
       }
-      // (3) chain through the bilinear sample and the projection
-      float gix = 0.f, giy = 0.f;
+    }
+    // (3b) chain through the projection
+    float acc[12];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        gix += gest[c] * dxc[r][c];
-        giy += gest[c] * dyc[r][c];
-      }
+    for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < kPxPerThread; ++r) {
+      const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
+      const int gy = y0 + ly, gx = x0 + lx;
+      if (gy >= H || gx >= W) continue;
       float dd;
-      const float depth = decode_depth(invt[o2], DRO_DEPTH_INV, 0.f, 0.f, &dd);
+      const float depth = decode_depth(invt[(ly + 2) * W2 + (lx + 2)], DRO_DEPTH_INV, 0.f, 0.f, &dd);
       Proj q;
       project(ki, kr, R, t, (float)gx, (float)gy, depth, H, W, q);
-      gdep[r] += project_backward(q, kr, R, gix, giy, acc, acc + 9);
+      gdep[r] += project_backward(q, kr, R, gix[r], giy[r], acc, acc + 9);
     }
     if (a.part_pose) {
-      block_sum<12>(acc, scratch);
+      double sum[12];
+      block_sum_d<12>(acc, sum, dscratch);
       if (threadIdx.x == 0) {
-        float* dst = a.part_pose + (((size_t)(j * a.n + i) * a.B + b) * tiles + tile) * 12;
+        double* dst = a.part_pose + (((size_t)(j * a.n + i) * a.B + b) * tiles + tile) * 12;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) dst[k] = acc[k];
+        for (int k = 0; k < 12; ++k) dst[k] = sum[k];
       }
     }
   }
@@ -723,7 +710,7 @@ PhotoLayout photo_layout(int B, int N, int n, int H, int W) {
   L.part_sm = off;
   off = al(off + sizeof(float) * n * B * tiles * 2);
   L.part_pose = off;
-  off = al(off + sizeof(float) * N * n * B * tiles * 12);
+  off = al(off + sizeof(double) * N * n * B * tiles * 12);
   L.total = off;
   return L;
 }
@@ -778,7 +765,7 @@ int photo_setup(PhotoArgs& a, const float* image, const float* context, const fl
   a.U = (float*)(ws + L.U);
   a.part_ph = (float*)(ws + L.part_ph);
   a.part_sm = (float*)(ws + L.part_sm);
-  a.part_pose = (float*)(ws + L.part_pose);
+  a.part_pose = (double*)(ws + L.part_pose);
   return DRO_OK;
 }
 }  // namespace

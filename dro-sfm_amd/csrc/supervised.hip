@@ -44,7 +44,7 @@ struct SupArgs {
   float lo_disp, hi_disp;   // 1/max_depth, 1/min_depth (depth term validity)
   float min_d, max_d4;      // min_depth, max_depth/4   (pose term validity)
   int nblk;                 // pixel blocks per image
-  float* part;              // forward: [n][B][nblk][2]; backward: [N][n][B][nblk][12]
+  float* part;              // forward: float [n][B][nblk][2]; backward: double [N][n][B][nblk][12]
 };
 
 // normalised projection of one reconstructed pixel (camera.py:178-184)
@@ -73,6 +73,7 @@ template <bool BACKWARD>
 __global__ __launch_bounds__(kSupThreads) void sup_loss_kernel(SupArgs a, const float* __restrict__ gout,
                                                                float* __restrict__ ginv) {
   __shared__ float scratch[12 * (kSupThreads / kWave)];
+  __shared__ double dscratch[12 * (kSupThreads / kWave)];
   const int b = blockIdx.y, i = blockIdx.z;
   const int HW = a.H * a.W;
   const float wm1 = (float)(a.W - 1), hm1 = (float)(a.H - 1);
@@ -152,11 +153,12 @@ __global__ __launch_bounds__(kSupThreads) void sup_loss_kernel(SupArgs a, const 
       }
     }
     if (BACKWARD) {
-      block_sum<12>(acc, scratch);
+      double sum[12];
+      block_sum_d<12>(acc, sum, dscratch);
       if (threadIdx.x == 0) {
-        float* dst = a.part + ((((size_t)j * a.n + i) * a.B + b) * a.nblk + blockIdx.x) * 12;
+        double* dst = (double*)a.part + ((((size_t)j * a.n + i) * a.B + b) * a.nblk + blockIdx.x) * 12;
 #pragma unroll
-        for (int e = 0; e < 12; ++e) dst[e] = acc[e];
+        for (int e = 0; e < 12; ++e) dst[e] = sum[e];
       }
     }
   }
@@ -247,8 +249,10 @@ using namespace dro;
 
 extern "C" size_t dro_supervised_workspace_bytes(int B, int N, int n, int H, int W) {
   const size_t nblk = ((size_t)H * W + kPxBlock - 1) / kPxBlock;
-  const size_t fwd = (size_t)n * B * nblk * 2, bwd = (size_t)N * n * B * nblk * 12;
-  return (fwd > bwd ? fwd : bwd) * sizeof(float);
+  // forward: float partials; backward: fp64 pose partials
+  const size_t fwd = (size_t)n * B * nblk * 2 * sizeof(float);
+  const size_t bwd = (size_t)N * n * B * nblk * 12 * sizeof(double);
+  return fwd > bwd ? fwd : bwd;
 }
 
 extern "C" int dro_supervised_forward(const float* gt_inv, const float* inv_depths, const float* K,
@@ -290,5 +294,5 @@ extern "C" int dro_supervised_backward(const float* gt_inv, const float* inv_dep
   hipLaunchKernelGGL(sup_loss_kernel<true>, dim3(a.nblk, B, n), dim3(kSupThreads), 0, s, a,
                      grad_out, grad_inv_depths);
   if ((st = launch_status("sup_loss_kernel<bwd> launch failed"))) return st;
-  return launch_pose_finalize(a.part, a.nblk, N * n * B, pose, pose_mode, grad_pose, s);
+  return launch_pose_finalize((const double*)a.part, a.nblk, N * n * B, pose, pose_mode, grad_pose, s);
 }

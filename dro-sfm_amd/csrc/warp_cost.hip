@@ -219,8 +219,8 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
 // input (summed over refs, no atomics) and to per-workgroup pose partials.
 __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
     WarpArgs a, const float* __restrict__ gxy, float* __restrict__ gdepth,
-    float* __restrict__ partial) {
-  __shared__ float scratch[12 * (kGeoThreads / kWave)];
+    double* __restrict__ partial) {
+  __shared__ double scratch[12 * (kGeoThreads / kWave)];
   const int P = a.h * a.w;
   const int p = blockIdx.x * kGeoThreads + threadIdx.x;
   const int b = blockIdx.y;
@@ -245,11 +245,12 @@ __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
       gd_total += project_backward(q, kr, R, g[0], g[1], acc, acc + 9);
     }
     if (partial) {
-      block_sum<12>(acc, scratch);
+      double sum[12];
+      block_sum_d<12>(acc, sum, scratch);
       if (threadIdx.x == 0) {
-        float* dst = partial + (((size_t)n * a.B + b) * gridDim.x + blockIdx.x) * 12;
+        double* dst = partial + (((size_t)n * a.B + b) * gridDim.x + blockIdx.x) * 12;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) dst[k] = acc[k];
+        for (int k = 0; k < 12; ++k) dst[k] = sum[k];
       }
     }
   }
@@ -260,35 +261,35 @@ __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
 // stride over the pose's [nblk][12] partials (coalesced), then the 5 group
 // sums are added in a fixed order (deterministic).  The photometric loss hands
 // in 240 tile partials per pose: one serial thread per pose took 51 us there.
-__global__ __launch_bounds__(64) void pose_finalize_kernel(const float* __restrict__ partial, int nblk,
+__global__ __launch_bounds__(64) void pose_finalize_kernel(const double* __restrict__ partial, int nblk,
                                                            int npose, const float* __restrict__ pose,
                                                            int pose_mode, float* __restrict__ gpose) {
   constexpr int G = 5;   // row groups
-  __shared__ float sh[G * 12];
-  __shared__ float s[12];
+  __shared__ double sh[G * 12];
+  __shared__ double s[12];
   const int i = blockIdx.x, lane = threadIdx.x;
   if (i >= npose) return;
   if (lane < G * 12) {
     const int comp = lane % 12, g = lane / 12;
-    const float* src = partial + (size_t)i * nblk * 12 + comp;
-    float v = 0.f;
+    const double* src = partial + (size_t)i * nblk * 12 + comp;
+    double v = 0.0;
     for (int j = g; j < nblk; j += G) v += src[(size_t)j * 12];
     sh[lane] = v;
   }
   __syncthreads();
   if (lane < 12) {
-    float v = 0.f;
+    double v = 0.0;
 #pragma unroll
     for (int g = 0; g < G; ++g) v += sh[g * 12 + lane];
     s[lane] = v;
   }
   __syncthreads();
   if (lane == 0) {
-    float r[12];
+    double r[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) r[k] = s[k];
     const int ps = pose_stride(pose_mode);
-    store_pose_grad(pose + (size_t)i * ps, pose_mode, r, r + 9, gpose + (size_t)i * ps);
+    store_pose_grad_d(pose + (size_t)i * ps, pose_mode, r, r + 9, gpose + (size_t)i * ps);
   }
 }
 
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(256) void plane_sweep_wide_kernel(WarpArgs a, const
   }
 }
 
-int launch_pose_finalize(const float* partial, int nblk, int npose, const float* pose,
+int launch_pose_finalize(const double* partial, int nblk, int npose, const float* pose,
                          int pose_mode, float* gpose, hipStream_t s) {
   if (npose <= 0) return 0;
   hipLaunchKernelGGL(pose_finalize_kernel, dim3(npose), dim3(64), 0, s, partial, nblk,
@@ -415,7 +416,8 @@ using namespace dro;
 extern "C" size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w) {
   const size_t P = (size_t)h * w;
   const size_t nblk = (P + kGeoThreads - 1) / kGeoThreads;
-  return ((size_t)N * B * P * 2 + (size_t)N * B * nblk * 12) * sizeof(float);
+  // gxy (float), then the fp64 pose partials (8-byte aligned: N*B*P*2 floats is even)
+  return (size_t)N * B * P * 2 * sizeof(float) + (size_t)N * B * nblk * 12 * sizeof(double);
 }
 
 extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, const float* depth,
@@ -471,7 +473,7 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
   const int P = h * w;
   float* gxy = geo ? (float*)workspace : nullptr;
   const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
-  float* partial = (geo && grad_pose) ? gxy + (size_t)N * B * P * 2 : nullptr;
+  double* partial = (geo && grad_pose) ? (double*)(gxy + (size_t)N * B * P * 2) : nullptr;
   if (grad_fmap_ref && !(accumulate & 2) &&
       (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s)))
     return st;

@@ -70,6 +70,8 @@ def load():
     _sig(lib.dro_conv2d_workspace_bytes, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_plan, I, I, I, I, I, I, I, P)
     _sig(lib.dro_debug_conv_stamps, P)
+    _sig(lib.dro_conv_log, I)
+    _sig(lib.dro_conv_log_read, ctypes.c_char_p, ctypes.c_longlong, restype=ctypes.c_longlong)
     _sig(lib.dro_weight_split_bytes, I, I, I, I, I, restype=Z)
     _sig(lib.dro_weight_split, P, I, I, I, I, P, P, S)
     _sig(lib.dro_conv2d_forward, P, I, P, P, I, I, I, I, I, I, I, F, P, I, I, P, P, Z, S)
@@ -99,7 +101,7 @@ EXPORTED = (
     "dro_resize_rgb8_to_tensor", "dro_color_jitter_rgb8", "dro_resize_rgb8", "dro_rgb8_to_tensor",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",
-    "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv2d_forward", "dro_convgru_gates_forward",
+    "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv_log", "dro_conv_log_read", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",
     "dro_gru_backward_elem", "dro_adam_step",

@@ -331,6 +331,16 @@ int dro_conv2d_plan(int rows, int kch, int KH, int KW, int B, int H, int W, long
  * production launches. */
 int dro_debug_conv_stamps(void* buffer);
 
+/* Diagnostics: with dro_conv_log(1) every following conv-engine launch records
+ * (kernel instantiation name as rocprof prints it, e.g. "dconv_kernel<32, 1,
+ * 5, 0, 2, 2, 4>", launch count, algorithmic FLOPs 2*Cout*Cin*KH*KW*B*H*W
+ * [* uses]) in a host-side table (cleared on enable); dro_conv_log_read copies
+ * it as "name\tlaunches\tflops\n" lines into buf (NUL-terminated, truncated
+ * at cap) and returns the full length.  Feeds the per-kernel roofline table
+ * (tools/conv_roofline.py). */
+int dro_conv_log(int enable);
+long long dro_conv_log_read(char* buf, long long cap);
+
 int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* weight, const float* bias,
                        int B, int H, int W, int Cout, int KH, int KW, int act, float alpha,
                        float* out, int out_ctot, int out_coff, const void* wsplit,

@@ -5,7 +5,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-for p in (ROOT, GOLDEN):
+TESTS = os.path.join(ROOT, "tests")
+for p in (ROOT, GOLDEN, TESTS):
     if p not in sys.path:
         sys.path.insert(0, p)
 

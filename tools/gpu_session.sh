@@ -53,6 +53,14 @@ for step in "$@"; do
     stampdbg) run conv_stamps_dbg 300 env STAMP_DBG=${STAMP_DBG:-0,1,2,4,3,5} python tools/conv_stamps.py ;;
     tprof) run torch_prof 600 python tools/torch_prof.py ;;
     pmcsq) run pmc_sq 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python bench.py --roofline-only ;;
+    croof) run croof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/croof" -o run -- python tools/conv_roofline.py run "$OUT/croof" &&
+         run croof_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/croof_fetch" -o run -- python tools/conv_roofline.py run "$OUT/croof_fetch" &&
+         run croof_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/croof_write" -o run -- python tools/conv_roofline.py run "$OUT/croof_write" &&
+         run croof_mfma 300 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/croof_mfma" -o run -- python tools/conv_roofline.py run "$OUT/croof_mfma" &&
+         run croof_table 60 python tools/conv_roofline.py table "$OUT/croof" --pmc-dirs "$OUT/croof_fetch" "$OUT/croof_write" "$OUT/croof_mfma" ;;
+    v5iso) run py_view5iso 600 python tools/diag_train_steps.py view5iso ;;
+    envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
+    benchab20) run bench_ab 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
