@@ -1105,8 +1105,12 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
     if (more) store(buf ^ 1);
     __syncthreads();
   }
+  // partials [split][tap][o][c]: lanes run along c, so each store is a
+  // 128-B row segment (the [o][c][tap] order of wgrad_halo_kernel scattered
+  // them 36 B apart -- 7x write amplification measured at this split count)
   float* wpart = a.part + (size_t)blockIdx.y * Cout * Cin * T;
   const int c = c0 + wc * 32 + (lane & 31);
+  const size_t tstride = (size_t)Cout * Cin;
   if (TAPSPLIT) {
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
@@ -1114,7 +1118,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (o < Cout && c < Cin) wpart[((size_t)o * Cin + c) * T + tap0 + k] = acc[k][r];
+          if (o < Cout && c < Cin) wpart[(tap0 + k) * tstride + (size_t)o * Cin + c] = acc[k][r];
         }
       }
     }
@@ -1133,7 +1137,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
         for (int r = 0; r < 16; ++r) {
           const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (o < Cout && c < Cin)
-            wpart[((size_t)o * Cin + c) * T + tp] = acc[tp][r] + red[(q4 * 16 + r) * 64 + lane];
+            wpart[tp * tstride + (size_t)o * Cin + c] = acc[tp][r] + red[(q4 * 16 + r) * 64 + lane];
         }
       }
       __syncthreads();
@@ -1145,6 +1149,25 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
       const float v = wave_sum(bsum[j]);
       const int o = o0 + wave * 8 + j;
       if (lane == 0 && o < Cout) a.bpart[(size_t)blockIdx.y * Cout + o] = v;
+    }
+  }
+}
+
+// wgrad2 partials: dW[o][c][tap] = sum_s part[s][tap][o][c] (threads walk the
+// partials' coalesced (tap, o, c) order); db[o] = sum_s bpart[s][o]
+__global__ __launch_bounds__(256) void wgrad2_finish_kernel(IgArgs a, int splits) {
+  const int Cout = a.g.Cout, Cin = a.g.Cin, T = a.g.KH * a.g.KW;
+  const long long oc = (long long)Cout * Cin, total = oc * T;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const float v = split_sum(a.part + e, (size_t)total, splits);
+    const int tap = (int)(e / oc);
+    const long long r = e - (long long)tap * oc;        // o * Cin + c
+    const size_t dst = (size_t)r * T + tap;
+    a.gweight[dst] = a.wacc ? a.gweight[dst] + v : v;
+    if (a.gbias && e < Cout) {
+      const float bv = split_sum(a.bpart + e, (size_t)Cout, splits);
+      a.gbias[e] = a.wacc ? a.gbias[e] + bv : bv;
     }
   }
 }
@@ -1389,8 +1412,8 @@ WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
 }
 
 // weight gradient v2 (wgrad2_kernel): 64 x 64 channel tiles, one block of 8
-// waves per CU (85 KB LDS); splits fill ~`target` blocks with >= 2 pixel tiles
-// per split.  DRO_WGRAD_V1=1 keeps the wgrad_halo_kernel path (A/B).
+// waves per CU (85 KB LDS); splits fill ~`target` blocks with >= `min_tiles`
+// pixel tiles per split (each split writes a full Cout x Cin x T partial).  DRO_WGRAD_V1=1 keeps the wgrad_halo_kernel path (A/B).
 bool wgrad_v1() {
   static const bool v1 = getenv("DRO_WGRAD_V1") != nullptr;
   return v1;
@@ -1412,9 +1435,14 @@ WhPlan plan_wgrad2(int Cin, int Cout, int KH, int KW, int ntiles_total, int B, i
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 256;
   }();
+  static const int min_tiles = [] {   // tuning override: DRO_WG2_MIN_TILES (default 4)
+    const char* e = getenv("DRO_WG2_MIN_TILES");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 4;
+  }();
   int sp = (target + blocks - 1) / blocks;
   if (sp > 256) sp = 256;
-  if (sp > ntiles / 2) sp = ntiles / 2;
+  if (sp > ntiles / min_tiles) sp = ntiles / min_tiles;
   if (sp < 1) sp = 1;
   pl.tiles_per_split = (ntiles + sp - 1) / sp;
   pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
@@ -2094,7 +2122,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     const long long total = (long long)Cout * a.g.Cin * T;
     long long blocks = (total + 255) / 256;
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, w2.splits);
+    hipLaunchKernelGGL(wgrad2_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, w2.splits);
     if ((st = launch_status("wgrad_halo_finish_kernel launch failed"))) return st;
   } else if (grad_weight && wh.ok) {
     a.otiles = wh.otiles;
@@ -2269,7 +2297,10 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
   const long long total = (long long)Cout * Cin * T;
   long long blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
+  if (v2)
+    hipLaunchKernelGGL(wgrad2_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
+  else
+    hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
   return launch_status("wgrad_halo_finish_kernel launch failed");
 }
 

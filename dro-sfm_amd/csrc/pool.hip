@@ -88,7 +88,7 @@ static int pool_check(const void* a, const void* b, const void* c, long long pla
     set_error("maxpool3x3s2: NULL pointer");
     return DRO_E_NULL;
   }
-  if (planes < 1 || planes > 65535 || H < 1 || W < 1 || (long long)H * W >= (1LL << 30)) {
+  if (planes < 1 || planes >= (1LL << 40) || H < 1 || W < 1 || (long long)H * W >= (1LL << 30)) {
     set_error("maxpool3x3s2: sizes out of range");
     return DRO_E_SHAPE;
   }
@@ -100,9 +100,15 @@ extern "C" int dro_maxpool3x3s2_forward(const float* x, long long planes, int H,
   int st = pool_check(x, y, argmax, planes, H, W);
   if (st) return st;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((Ho * Wo + kPoolThreads - 1) / kPoolThreads, (unsigned)planes),
-                     dim3(kPoolThreads), 0, (hipStream_t)stream, x, H, W, Ho, Wo, y, argmax);
-  return launch_status("maxpool3s2_fwd_kernel launch failed");
+  // planes ride grid.y (<= 65535 per launch): larger batches go in chunks
+  for (long long p0 = 0; p0 < planes; p0 += 65535) {
+    const long long np = planes - p0 < 65535 ? planes - p0 : 65535;
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((Ho * Wo + kPoolThreads - 1) / kPoolThreads, (unsigned)np),
+                       dim3(kPoolThreads), 0, (hipStream_t)stream, x + p0 * H * W, H, W, Ho, Wo,
+                       y + p0 * Ho * Wo, argmax + p0 * Ho * Wo);
+    if ((st = launch_status("maxpool3s2_fwd_kernel launch failed"))) return st;
+  }
+  return DRO_OK;
 }
 
 extern "C" int dro_maxpool3x3s2_backward(const float* grad_y, const unsigned char* argmax,
@@ -111,7 +117,12 @@ extern "C" int dro_maxpool3x3s2_backward(const float* grad_y, const unsigned cha
   int st = pool_check(grad_y, argmax, grad_x, planes, H, W);
   if (st) return st;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((H * W + kPoolThreads - 1) / kPoolThreads, (unsigned)planes),
-                     dim3(kPoolThreads), 0, (hipStream_t)stream, grad_y, argmax, H, W, Ho, Wo, grad_x);
-  return launch_status("maxpool3s2_bwd_kernel launch failed");
+  for (long long p0 = 0; p0 < planes; p0 += 65535) {
+    const long long np = planes - p0 < 65535 ? planes - p0 : 65535;
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((H * W + kPoolThreads - 1) / kPoolThreads, (unsigned)np),
+                       dim3(kPoolThreads), 0, (hipStream_t)stream, grad_y + p0 * Ho * Wo, argmax + p0 * Ho * Wo,
+                       H, W, Ho, Wo, grad_x + p0 * H * W);
+    if ((st = launch_status("maxpool3s2_bwd_kernel launch failed"))) return st;
+  }
+  return DRO_OK;
 }

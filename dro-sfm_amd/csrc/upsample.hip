@@ -429,7 +429,7 @@ static int bl2_check(const float* a, const float* b, long long planes, int h, in
     set_error("bilinear_upsample2x: NULL pointer");
     return DRO_E_NULL;
   }
-  if (planes < 1 || planes > 65535 || h < 1 || w < 1 || 4LL * h * w >= (1LL << 30)) {
+  if (planes < 1 || planes >= (1LL << 40) || h < 1 || w < 1 || 4LL * h * w >= (1LL << 30)) {
     set_error("bilinear_upsample2x: sizes out of range");
     return DRO_E_SHAPE;
   }
@@ -440,16 +440,25 @@ extern "C" int dro_bilinear_upsample2x_forward(const float* x, long long planes,
                                                float* out, void* stream) {
   int st = bl2_check(x, out, planes, h, w);
   if (st) return st;
-  hipLaunchKernelGGL(bilinear2x_fwd_kernel, dim3((4 * h * w + 255) / 256, (unsigned)planes), dim3(256), 0,
-                     (hipStream_t)stream, x, h, w, out);
-  return launch_status("bilinear2x_fwd_kernel launch failed");
+  // planes ride grid.y (<= 65535 per launch): larger batches go in chunks
+  for (long long p0 = 0; p0 < planes; p0 += 65535) {
+    const long long np = planes - p0 < 65535 ? planes - p0 : 65535;
+    hipLaunchKernelGGL(bilinear2x_fwd_kernel, dim3((4 * h * w + 255) / 256, (unsigned)np), dim3(256), 0,
+                       (hipStream_t)stream, x + p0 * h * w, h, w, out + p0 * 4 * h * w);
+    if ((st = launch_status("bilinear2x_fwd_kernel launch failed"))) return st;
+  }
+  return DRO_OK;
 }
 
 extern "C" int dro_bilinear_upsample2x_backward(const float* grad_out, long long planes, int h,
                                                 int w, float* grad_x, void* stream) {
   int st = bl2_check(grad_out, grad_x, planes, h, w);
   if (st) return st;
-  hipLaunchKernelGGL(bilinear2x_bwd_kernel, dim3((h * w + 255) / 256, (unsigned)planes), dim3(256), 0,
-                     (hipStream_t)stream, grad_out, h, w, grad_x);
-  return launch_status("bilinear2x_bwd_kernel launch failed");
+  for (long long p0 = 0; p0 < planes; p0 += 65535) {
+    const long long np = planes - p0 < 65535 ? planes - p0 : 65535;
+    hipLaunchKernelGGL(bilinear2x_bwd_kernel, dim3((h * w + 255) / 256, (unsigned)np), dim3(256), 0,
+                       (hipStream_t)stream, grad_out + p0 * 4 * h * w, h, w, grad_x + p0 * h * w);
+    if ((st = launch_status("bilinear2x_bwd_kernel launch failed"))) return st;
+  }
+  return DRO_OK;
 }

@@ -11,11 +11,16 @@ bytes) and csrc/resize.hip resamples them bit-identically to Pillow, applies
 torchvision's ColorJitter (the reference default jittering = (0.2, 0.2, 0.2,
 0.05), configs/default_config.py:145) bit-identically to Pillow's
 ImageEnhance / HSV arithmetic, and writes the float CHW tensors.  The
-jitter's random order and factors are drawn on the host from torch's global
-generator in torchvision's get_params order, one draw per frame as the
-reference's per-image transform call.  Decoding stays on the host.
+jitter's random order and factors are drawn on the host from torch's
+generator in the reference's exact order per sample (colorjitter_sample,
+augmentations.py:226-256): its Python `random.random()` gate, one get_params
+draw that the reference discards, then one ColorJitter draw per image --
+'rgb', then each 'rgb_context' frame -- so a seeded run reproduces the
+reference's augmentations, not only their distribution.  Decoding stays on
+the host.
 """
 import ctypes
+import random
 from functools import lru_cache
 
 import numpy as np
@@ -194,9 +199,17 @@ def train_transforms(sample, image_shape, jittering, generator=None):
     resized = [resize_rgb8(f, image_shape) if len(image_shape) else f.contiguous() for f in frames]
     originals = [rgb8_to_tensor(r) for r in resized]
     if len(jittering) > 0:
-        for r in resized:
-            orders, factors, hues = colorjitter_params(jittering, r.shape[0], generator)
-            color_jitter_(r, orders, factors, hues)
+        # per sample, in colorjitter_sample's order (augmentations.py:226-256)
+        B, F = resized[0].shape[0], len(resized)
+        per = [[None] * B for _ in range(F)]
+        for b in range(B):
+            random.random()                                  # `random.random() < prob` (prob 1.0)
+            colorjitter_params(jittering, 1, generator)      # get_params result the reference discards
+            for f in range(F):                               # 'rgb', then 'rgb_context' in order
+                o, fa, hu = colorjitter_params(jittering, 1, generator)
+                per[f][b] = (o[0], fa[0], hu[0])
+        for f, r in enumerate(resized):
+            color_jitter_(r, [p[0] for p in per[f]], [p[1] for p in per[f]], [p[2] for p in per[f]])
     tensors = [rgb8_to_tensor(r) for r in resized]
     out["rgb"], out["rgb_context"] = tensors[0], tensors[1:]
     out["rgb_original"], out["rgb_context_original"] = originals[0], originals[1:]

@@ -444,12 +444,16 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
     N, n = pvec.shape[1], pvec.shape[2]
     poses = [[pvec[:, j, i] for i in range(n)] for j in range(N)]
     if kind == "selfsup":
-        return photometric_decay_loss(batch["rgb_original"], batch["rgb_context_original"], invs, K,
-                                      K, poses, forced_selection=forced_selection, **loss_kw)
-    gt_inv = torch.where(batch["depth"] <= 0, torch.zeros_like(batch["depth"]),
-                         1.0 / batch["depth"].clamp(min=1e-6))
-    return supervised_depth_pose_loss(invs, gt_inv, batch["pose_context"], poses, K, K, min_depth,
-                                      max_depth)
+        out = photometric_decay_loss(batch["rgb_original"], batch["rgb_context_original"], invs, K,
+                                     K, poses, forced_selection=forced_selection, **loss_kw)
+    else:
+        gt_inv = torch.where(batch["depth"] <= 0, torch.zeros_like(batch["depth"]),
+                             1.0 / batch["depth"].clamp(min=1e-6))
+        out = supervised_depth_pose_loss(invs, gt_inv, batch["pose_context"], poses, K, K, min_depth,
+                                         max_depth)
+    # the net's predictions, for tests measuring forward distances
+    out["preds"] = (torch.stack([d.detach() for d in invs]), pvec.detach())
+    return out
 
 
 # ============================================================================ evaluation

@@ -340,27 +340,69 @@ def test_depth_pose_net_golden(hip, tag, version):
         assert rel(pose_e, d["poses_eval"]) < 1e-3
 
 
-def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=False, perturb=False):
-    """Oracle loss and parameter gradients.  perturb: the images and K moved by
-    ~1 ulp (relative 1e-7 Gaussian, seeded) -- the gradient's change under it
-    measures how far ANY fp32 evaluation of this step may land from another
-    (kinks of the loss: min selection, L1 signs, bilinear cell edges,
-    smoothness signs; amplified by the recurrence)."""
+def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=False, perturb=False,
+                  want_preds=False):
+    """Oracle loss and parameter gradients (and, want_preds, the net's
+    predictions (inv_depths [n,B,1,H,W], poses [B,N,n,6])).  perturb (True =
+    1e-7, or a relative scale): the images and K moved by a seeded relative
+    Gaussian -- the gradient's change under it measures how far an fp32
+    evaluation of this step may land from another at that distance (kinks of
+    the loss: min selection, L1 signs, bilinear cell edges, smoothness signs;
+    amplified by the recurrence)."""
     p = params_from_spec(spec)
     p = {k: (v.to(dt).requires_grad_(True) if v.is_floating_point() and "running" not in k
              else (v.to(dt) if v.is_floating_point() else v)) for k, v in p.items()}
     b = {k: (v.to(dt) if torch.is_tensor(v) and v.is_floating_point() else
              ([t.to(dt) for t in v] if isinstance(v, list) else v)) for k, v in batch.items()}
     if perturb:
+        s = 1e-7 if perturb is True else float(perturb)
         g = torch.Generator().manual_seed(99)
-        jig = lambda t: t * (1 + 1e-7 * torch.randn(t.shape, generator=g, dtype=t.dtype))
+        jig = lambda t: t * (1 + s * torch.randn(t.shape, generator=g, dtype=t.dtype))
         for key in ("rgb", "rgb_original", "intrinsics"):
             b[key] = jig(b[key])
         for key in ("rgb_context", "rgb_context_original"):
             b[key] = [jig(t) for t in b[key]]
     out = O.train_step_loss(p, version, mind, maxd, b, kind=kind, forced_selection=forced, flip=flip)
     out["loss"].sum().backward()
-    return out["loss"].detach(), {k: v.grad for k, v in p.items() if getattr(v, "grad", None) is not None}
+    grads = {k: v.grad for k, v in p.items() if getattr(v, "grad", None) is not None}
+    if want_preds:
+        return out["loss"].detach(), grads, out["preds"]
+    return out["loss"].detach(), grads
+
+
+def _l2(a, b):
+    return float((a.double().cpu() - b.double().cpu()).norm() / b.double().cpu().norm())
+
+
+def _matched_sensitivity(model, out, preds64, oracle_args, cap=1e-5):
+    """The fp64 gradient's change between two points as far apart as THIS
+    evaluation's forward pass is from fp64.
+
+    The photometric loss has derivative jumps (bilinear cell edges where a
+    warped coordinate crosses an integer, L1 and smoothness signs): the
+    gradient is piecewise smooth, and on small images a few pixels crossing a
+    cell edge move a pose gradient by percents (view5 fixture, fp64 oracle:
+    input perturbation 1e-7 -> gradient L2 change 2.3e-5; 1e-6 -> 4.3e-3, dL/dpose
+    of one ref by 11 %).  Where an fp32 forward lands within that band is
+    rounding, not parity.  So: measure the forward distance d_hip of the HIP
+    predictions (inverse depths and poses, relative L2) from the fp64 oracle's,
+    measure the fp64 oracle's own prediction move d0 under a 1e-7 input
+    perturbation, and evaluate the fp64 gradient at a perturbation scaled to
+    1e-7 * d_hip / d0 (capped at `cap`, which also bounds what this allowance
+    can ever absorb).  Returns (gsens, info)."""
+    inv_h = torch.stack([d.detach() for d in out["inv_depths"]]).double().cpu()
+    pv = getattr(out.get("poses"), "vec", None)
+    pose_h = pv.detach().double().cpu() if pv is not None else None
+    args, kw = oracle_args
+    _, _, (inv_p, pose_p) = _oracle_grads(*args, perturb=1e-7, want_preds=True, **kw)
+    d_hip = _l2(inv_h, preds64[0])
+    d0 = _l2(inv_p, preds64[0])
+    if pose_h is not None:
+        d_hip = max(d_hip, _l2(pose_h, preds64[1]))
+        d0 = max(d0, _l2(pose_p, preds64[1]))
+    scale = min(cap, 1e-7 * max(1.0, d_hip / max(d0, 1e-30)))
+    _, gs = _oracle_grads(*args, perturb=scale, **kw)
+    return gs, {"d_hip": d_hip, "d0_1e-7": d0, "scale": scale}
 
 
 def _grad_check(model, g64, g32, floor_mult=16.0, abs_floor=2e-3, gsens=None):
@@ -464,13 +506,16 @@ def test_train_step_golden(hip, tag, version, kind, flip):
     forced = None
     if kind == "selfsup":
         forced = model._photometric_loss.last_selection.cpu().unsqueeze(2)
-    _, g64 = _oracle_grads(spec, version, mind, maxd, cpu_batch, kind, torch.float64, forced, flip)
-    _, g32 = _oracle_grads(spec, version, mind, maxd, cpu_batch, kind, torch.float32, forced, flip)
-    _, gs = _oracle_grads(spec, version, mind, maxd, cpu_batch, kind, torch.float64, forced, flip, perturb=True)
+    args = (spec, version, mind, maxd, cpu_batch, kind, torch.float64, forced, flip)
+    _, g64, p64 = _oracle_grads(*args, want_preds=True)
+    _, g32, p32 = _oracle_grads(*args[:6], torch.float32, forced, flip, want_preds=True)
+    gs, sinfo = _matched_sensitivity(model, out, p64, (args, {}))
+    sinfo["d_o32"] = _l2(p32[0], p64[0])
+    assert sinfo["d_hip"] < 1e-4, sinfo                   # the forward itself: fp32-close
     bad, ok, info = _grad_check(model, g64, g32, gsens=gs)
-    assert not bad and ok, (bad[:5], info)
+    assert not bad and ok, (bad[:5], info, sinfo)
     fbad, _ = _fixture_check(model, {k: v.cpu() for k, v in f.items()}, g64, g32, gsens=gs)
-    assert not fbad, fbad[:5]
+    assert not fbad, (fbad[:5], sinfo)
 
 
 def _scannet_K(B, W=320, H=240):
@@ -496,14 +541,16 @@ def test_train_step_view5_n4_golden(hip):
     assert rel(out["loss"], f["loss"]) < TOL
     out["loss"].sum().backward()
     forced = model._photometric_loss.last_selection.cpu().unsqueeze(2)
-    _, g64 = _oracle_grads(spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float64, forced)
-    _, g32 = _oracle_grads(spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float32, forced)
-    _, gs = _oracle_grads(spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float64, forced,
-                          perturb=True)
+    args = (spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float64, forced)
+    _, g64, p64 = _oracle_grads(*args, want_preds=True)
+    _, g32, p32 = _oracle_grads(*args[:6], torch.float32, forced, want_preds=True)
+    gs, sinfo = _matched_sensitivity(model, out, p64, (args, {}))
+    sinfo["d_o32"] = _l2(p32[0], p64[0])
+    assert sinfo["d_hip"] < 1e-4, sinfo
     bad, ok, info = _grad_check(model, g64, g32, gsens=gs)
-    assert not bad and ok, (bad[:5], info)
+    assert not bad and ok, (bad[:5], info, sinfo)
     fbad, _ = _fixture_check(model, {k: v.cpu() for k, v in f.items()}, g64, g32, gsens=gs)
-    assert not fbad, fbad[:5]
+    assert not fbad, (fbad[:5], sinfo)
 
 
 @pytest.mark.parametrize("kind", ["selfsup_view5", "sup_view3"])

@@ -43,3 +43,19 @@ def test_maxpool3x3s2_rejects_cpu_and_dtype():
         hip.maxpool3x3s2(torch.zeros(1, 1, 4, 4, dtype=torch.float64))
     with pytest.raises(RuntimeError):
         hip.maxpool3x3s2(torch.zeros(1, 1, 4, 4))
+
+
+@pytest.mark.gpu
+def test_maxpool_more_than_65535_planes():
+    """Chunked launches beyond 65535 planes: bit-identical to
+    F.max_pool2d forward and backward."""
+    import dro_sfm_amd.hip as hip
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.rand(2, 35000, 6, 7, device="cuda", generator=g).requires_grad_(True)
+    y = hip.maxpool3x3s2(x)
+    gy = torch.rand(y.shape, device="cuda", generator=g)
+    (y * gy).sum().backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    y2 = torch.nn.functional.max_pool2d(x2, 3, 2, 1)
+    (y2 * gy).sum().backward()
+    assert torch.equal(y, y2) and torch.equal(x.grad, x2.grad)

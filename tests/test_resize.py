@@ -80,16 +80,23 @@ def test_train_transforms_pipeline_matches_pillow():
     ctx = [rng.integers(0, 256, (B, h0, w0, 3), dtype=np.uint8) for _ in range(2)]
     out = train_transforms({"rgb": torch.from_numpy(rgb).cuda(), "rgb_context": [torch.from_numpy(c).cuda() for c in ctx]},
                            (H, W), (0.2, 0.2, 0.2, 0.05), generator=torch.Generator().manual_seed(3))
+    # the reference's draw order (colorjitter_sample, augmentations.py:226-256): per
+    # sample one discarded get_params draw, then rgb, ctx0, ctx1
     g = torch.Generator().manual_seed(3)
     from dro_sfm_amd.datasets.gpu_transforms import colorjitter_params
+    draws = {}
+    for n in range(B):
+        colorjitter_params((0.2, 0.2, 0.2, 0.05), 1, g)
+        for f in range(3):
+            o, fa, hu = colorjitter_params((0.2, 0.2, 0.2, 0.05), 1, g)
+            draws[f, n] = (o[0], fa[0], hu[0])
     cases = [(out["rgb"], out["rgb_original"], rgb)] + \
         [(out["rgb_context"][j], out["rgb_context_original"][j], ctx[j]) for j in range(2)]
-    for got, got_orig, src in cases:
-        orders, factors, hues = colorjitter_params((0.2, 0.2, 0.2, 0.05), B, g)
+    for f, (got, got_orig, src) in enumerate(cases):
         for n in range(B):
             rs = np.asarray(Image.fromarray(src[n]).resize((W, H), Image.BILINEAR))
             want_o = torch.from_numpy(rs.copy()).permute(2, 0, 1).float().div(255)
-            jt = O.color_jitter_pil(rs, orders[n], factors[n], hues[n])
+            jt = O.color_jitter_pil(rs, *draws[f, n])
             want = torch.from_numpy(jt.copy()).permute(2, 0, 1).float().div(255)
             assert torch.equal(got_orig[n].cpu(), want_o)
             assert torch.equal(got[n].cpu(), want)

@@ -33,3 +33,20 @@ def test_bilinear_upsample2x_matches_interpolate(shape):
 def test_bilinear_upsample2x_rejects_cpu():
     with pytest.raises(RuntimeError):
         hip.bilinear_upsample2x(torch.zeros(1, 1, 2, 2))
+
+
+@pytest.mark.gpu
+def test_bilinear_upsample2x_more_than_65535_planes():
+    """Planes ride grid.y (<= 65535 per launch); larger batches are launched in
+    chunks: forward and backward equal to F.interpolate."""
+    import dro_sfm_amd.hip as hip
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.rand(1, 70001, 3, 5, device="cuda", generator=g).requires_grad_(True)
+    y = hip.bilinear_upsample2x(x)
+    gy = torch.rand(y.shape, device="cuda", generator=g)
+    (y * gy).sum().backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    y2 = torch.nn.functional.interpolate(x2, scale_factor=2, mode="bilinear", align_corners=False)
+    (y2 * gy).sum().backward()
+    torch.testing.assert_close(y, y2, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-6)
