@@ -419,6 +419,8 @@ def main():
                     help="autograd's per-use gradient sums instead of in-place gradient sinks (A/B)")
     ap.add_argument("--aten-maxpool", action="store_true",
                     help="A/B: the ResNet stem max pooling through ATen instead of hip.maxpool3x3s2")
+    ap.add_argument("--miopen-encoder-convs", action="store_true",
+                    help="A/B: the encoders' stride-1 3x3 convolutions on MIOpen instead of the HIP engine")
     ap.add_argument("--no-fused-bn", action="store_true",
                     help="encoder BatchNorm+ReLU through PyTorch's kernels (A/B)")
     ap.add_argument("--miopen-find", choices=("on", "off"), default="off",
@@ -452,6 +454,7 @@ def main():
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     _extractor.set_native_maxpool(not args.aten_maxpool)
+    _extractor.set_native_convs(not args.miopen_encoder_convs)
     from dro_sfm_amd.hip import ops as _hops
     _hops.set_grad_sinks(not args.no_grad_sinks)
 
@@ -515,6 +518,7 @@ def main():
                    "grad_sinks": not args.no_grad_sinks,
                    "split_engine": args.split_engine,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",
+                   "encoder_3x3_s1": "miopen" if args.miopen_encoder_convs else "hip",
                    "stem_pool": "aten" if args.aten_maxpool else "hip",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},

@@ -3,9 +3,8 @@
 State-dict compatible with the reference ResNetEncoder
 (dro_sfm/networks/optim/extractor.py:7-107): conv1/bn1, layer1..layer3 of
 BasicBlocks (conv1/bn1/conv2/bn2[/downsample.0,1]), upconv1.0,
-upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  The convolutions run on
-MIOpen (SURVEY.md §8(f) ranks a fused encoder as the next step); pretrained
-ImageNet weights are never downloaded -- load a checkpoint instead.
+upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  Pretrained ImageNet
+weights are never downloaded -- load a checkpoint instead.
 
 Training-mode batch normalisation runs fused with the ReLU / residual add that
 follows it (hip.batchnorm_act, csrc/batchnorm.hip: two launches each way with
@@ -17,6 +16,9 @@ The 2x bilinear upsampling of the fusion head is a HIP kernel
 (hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.  So
 is the stem's 3x3/s2 max pooling (hip.maxpool3x3s2, bit-identical to
 F.max_pool2d forward and backward; ATen's backward took 55 us per call).
+The stride-1 3x3 convolutions (layer1-3 except each stage's first, the fusion
+head, out_conv) run on the HIP conv engine (conv3x3); the 7x7/s2 stem, the
+3x3/s2 stage entries and the 1x1/s2 downsamples stay on MIOpen.
 """
 import torch
 import torch.nn as nn
@@ -27,6 +29,26 @@ from ... import hip
 
 _FUSED_BN = [True]
 _NATIVE_POOL = [True]
+_NATIVE_CONV = [True]
+
+
+def set_native_convs(enabled):
+    """Stride-1 3x3 convolutions on the HIP f32-MFMA engine (default True) or
+    on MIOpen (False, A/B runs)."""
+    _NATIVE_CONV[0] = bool(enabled)
+
+
+def conv3x3(m, srcs, act=None):
+    """act(m(cat(srcs))) for an nn.Conv2d m.  Stride-1 3x3 'same' convolutions
+    on the GPU run on the HIP conv engine (csrc/conv.hip: sources read as a
+    virtual concatenation, bias + ReLU in the epilogue, weight gradient in
+    place into the trainer's flat buffer); everything else through m."""
+    srcs = list(srcs) if isinstance(srcs, (list, tuple)) else [srcs]
+    if (_NATIVE_CONV[0] and srcs[0].is_cuda and m.kernel_size == (3, 3) and m.stride == (1, 1)
+            and m.padding == (1, 1) and m.dilation == (1, 1) and m.groups == 1):
+        return hip.conv2d(srcs, m.weight, m.bias, act=act)
+    y = m(srcs[0] if len(srcs) == 1 else torch.cat(srcs, 1))
+    return F.relu(y, inplace=True) if act == "relu" else y
 
 
 def set_native_maxpool(enabled):
@@ -71,12 +93,12 @@ class BasicBlock(nn.Module):
                                             BatchNorm2d(cout))
 
     def forward(self, x):
-        y = self.bn1.act(self.conv1(x))
+        y = self.bn1.act(conv3x3(self.conv1, x))
         if self.downsample is None:
             skip = x
         else:
             skip = self.downsample[1].act(self.downsample[0](x), relu=False)
-        return self.bn2.act(self.conv2(y), skip=skip)
+        return self.bn2.act(conv3x3(self.conv2, y), skip=skip)
 
 
 def _stage(cin, cout, stride):
@@ -124,12 +146,12 @@ class ResNetEncoder(nn.Module):
         s4 = self.layer1(x)
         s8 = self.layer2(s4)
         x = self.layer3(s8)
-        x = self.upconv1(hip.bilinear_upsample2x(x))
-        x = self.upconv1_fusion(torch.cat([x, s8], 1))
+        x = conv3x3(self.upconv1[0], hip.bilinear_upsample2x(x), "relu")
+        x = conv3x3(self.upconv1_fusion[0], [x, s8], "relu")      # concat read in place
         if self.stride == 4:
-            x = self.upconv2(hip.bilinear_upsample2x(x))
-            x = self.upconv2_fusion(torch.cat([x, s4], 1))
-        x = self.out_conv(x)
+            x = conv3x3(self.upconv2[0], hip.bilinear_upsample2x(x), "relu")
+            x = conv3x3(self.upconv2_fusion[0], [x, s4], "relu")
+        x = conv3x3(self.out_conv, x)
         if chunks is not None:
             return torch.chunk(x, chunks, 0)
         return x

@@ -423,7 +423,7 @@ def flip_lr_intr(K, width):
 
 
 def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", loss_kw=None,
-                    forced_selection=None, flip=False):
+                    forced_selection=None, flip=False, pred_perturb=None):
     """SelfSupModelMF / SupModelMF .forward in training mode
     (models/SfmModelMF.py:106-189, SelfSupModelMF.py:63-99, SupModelMF.py:78-119).
 
@@ -431,7 +431,14 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
     (SfmModelMF.py:110-119, utils/image.py:61-81, 106-130): the net sees the
     flipped target and refs with K flipped (fx -> -fx, cx -> W - cx), its
     inverse depths are flipped back, and the loss -- on the UNflipped
-    `*_original` images -- uses the flipped K (the in-place mutation)."""
+    `*_original` images -- uses the flipped K (the in-place mutation).
+
+    pred_perturb=(rel_inv, rel_pose, seed) is a test hook: the loss is
+    evaluated at the net's predictions moved by seeded relative Gaussian
+    noise (straight-through: the backward runs through the unmoved net), to
+    measure how far the gradient moves when an fp32 forward lands that far
+    from the exact predictions (the loss's derivative jumps: bilinear cell
+    edges, L1 signs)."""
     loss_kw = loss_kw or {}
     K = batch["intrinsics"]
     img, refs = batch["rgb"], batch["rgb_context"]
@@ -441,6 +448,12 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
     invs, pvec = depth_pose_net(p, version, min_depth, max_depth, img, refs, K, training=True)
     if flip:
         invs = [d.flip(3) for d in invs]
+    if pred_perturb is not None:
+        ri, rp, seed = pred_perturb
+        g = torch.Generator().manual_seed(seed)
+        noise = lambda t, r: (t.detach() * r * torch.randn(t.shape, generator=g, dtype=t.dtype)).to(t.device)
+        invs = [d + noise(d, ri) for d in invs]
+        pvec = pvec + noise(pvec, rp)
     N, n = pvec.shape[1], pvec.shape[2]
     poses = [[pvec[:, j, i] for i in range(n)] for j in range(N)]
     if kind == "selfsup":

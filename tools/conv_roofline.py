@@ -119,9 +119,10 @@ def table(out, pmc_dirs):
             if v:
                 row[label] = round(v[0] / v[1] * scale, 1)
         if "mfma_busy_cycles_per_launch" in row and "gui_active_cycles_per_launch" in row:
-            # busy cycles are summed over the 256 CUs x 4 SIMDs
+            # busy cycles are summed over the 256 CUs x 4 SIMDs; GRBM_GUI_ACTIVE is
+            # the sum over the 8 XCDs (MI355X_MICROARCH.md, DVFS note): /8 = kernel cycles
             row["mfma_busy_frac"] = round(row["mfma_busy_cycles_per_launch"] /
-                                          (row["gui_active_cycles_per_launch"] * 256 * 4), 4)
+                                          (row["gui_active_cycles_per_launch"] / 8 * 256 * 4), 4)
         lines.append(row)
         total_ms += per_step_ms
         total_gf += e["flops"] / 1e9
