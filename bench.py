@@ -255,64 +255,55 @@ def _latest_traffic_file():
 
 
 TRAFFIC_FILE = _latest_traffic_file()
-# the roofline conv: depth SepConvGRU z|r gate forward at the KITTI metric shape
-RF_B, RF_HD, RF_H, RF_W, RF_CIN, RF_KH, RF_KW = 2, 64, 192 // 8, 640 // 8, 160, 1, 5
-
-
-def roofline_kernels():
-    """Names of the kernels one roofline call launches, from the engine's own
-    launch plan (dro_conv2d_plan): the halo conv and, with a K split over
-    blocks, its finish kernel."""
-    import ctypes
-    from dro_sfm_amd.hip import _lib
-    lib = _lib.load()
-    info = (ctypes.c_longlong * 16)()
-    _lib.check(lib.dro_conv2d_plan(2 * RF_HD, RF_CIN, RF_KH, RF_KW, RF_B, RF_H, RF_W, info),
-               "dro_conv2d_plan")
-    bm, ks, kin = int(info[1]), int(info[4]), int(info[15])
-    names = [f"dconv_kernel<{bm}, {RF_KH}, {RF_KW}, 0, 2, 2, {kin}>"]
-    if ks > 1:
-        names.append("igemm_finish_kernel<0, 2, 2>")
-    return names, ks, kin
-
-
+# the roofline conv: the weight gradient of the feature encoder's layer1 3x3
+# convolution at the KITTI metric shape (6 frames of 48x160, 64 -> 64)
+RF_B, RF_C, RF_H, RF_W = 6, 64, 192 // 4, 640 // 4
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_32x32x2_f32)
 
 
+def roofline_kernels():
+    """Names of the kernels one roofline call launches: the weight-gradient
+    kernel and its split-sum finish (rocprof name prefixes)."""
+    return ["wgrad2_kernel<3, 3, 0, true>", "wgrad2_finish_kernel<"], None, None
+
+
 def roofline_conv(device, iters=50, traffic_file=None):
-    """Dominant kernel class of the step: the f32-MFMA direct convolution engine
-    (csrc/conv.hip; dconv + wgrad kernels are ~40% of the step's kernel time).
-    Measured at its busiest shape, the depth SepConvGRU z|r gate conv forward
-    (update.py:59-66 of the reference; 1x5, sigmoid, r*h epilogue):
-    dro_convgru_gates_forward at B=2, 24x80, Cin=160 (h 64 + context 32 + feat
-    63 + inv depth 1), Cout=128 -> dconv_kernel<32,1,5,0,2,2> over 480 blocks
-    (split-K 2) + igemm_finish_kernel<0,2,2> (split sum + sigmoid + r*h).  The
-    HIP events bracket both launches (the rocprof summary lists the two
-    averages; their sum is the event time).
-    Algorithmic flops per call: 2 * Cout * Cin * KH*KW * B*H*W."""
+    """Dominant kernel of the step: the conv engine's weight gradient
+    (csrc/conv.hip wgrad2_kernel; the largest kernel class of the step,
+    profiles/r3_bench_steady_state.txt), measured at its heaviest shape: the
+    fnet layer1 3x3 conv (reference extractor.py:7-107 / torchvision
+    BasicBlock) over the 6 frames of a KITTI metric batch (B=2 targets + 4
+    refs, 48x160, 64 -> 64 channels), through the same entry point the
+    trainer's in-place path uses (dro_conv2d_weight_grad_multi, one use):
+    wgrad2_kernel<3,3,0,true> over 240 pixel splits + wgrad2_finish_kernel
+    (fixed-order split sum into the weight gradient).  HIP events bracket both
+    launches on the launch stream.  Algorithmic flops per call:
+    2 * Cout * Cin * 9 * B*H*W."""
     import ctypes
     from dro_sfm_amd.hip import _lib
-    from dro_sfm_amd.hip.conv import _slices, _workspace
+    from dro_sfm_amd.hip.conv import DroWgradUse, _slices
     lib = _lib.load()
-    B, hd, Hf, Wf, cin, KH, KW = RF_B, RF_HD, RF_H, RF_W, RF_CIN, RF_KH, RF_KW
-    kernels, ks, kin = roofline_kernels()
+    B, C, Hh, Ww = RF_B, RF_C, RF_H, RF_W
+    kernels, _, _ = roofline_kernels()
     g = torch.Generator(device=device)
     g.manual_seed(11)
-    h = torch.randn(B, hd, Hf, Wf, generator=g, device=device).tanh()
-    srcs = [h] + [torch.randn(B, c, Hf, Wf, generator=g, device=device) for c in (32, 63, 1)]
-    wzr = 0.05 * torch.randn(2 * hd, cin, KH, KW, generator=g, device=device)
-    bzr = 0.05 * torch.randn(2 * hd, generator=g, device=device)
-    zr = torch.empty(B, 2 * hd, Hf, Wf, device=device)
-    rh = torch.empty_like(h)
-    ws, nws = _workspace(B, Hf, Wf, cin, 2 * hd, KH, KW, device)
-    sl = _slices(srcs)
+    x = torch.randn(B, C, Hh, Ww, generator=g, device=device)
+    gout = torch.randn(B, C, Hh, Ww, generator=g, device=device)
+    gw = torch.empty(C, C, 3, 3, device=device)
+    sl = _slices([x])
+    use = (DroWgradUse * 1)()
+    use[0].srcs = ctypes.cast(sl, ctypes.c_void_p)
+    use[0].dout = gout.data_ptr()
+    use[0].y = None
+    nb = int(lib.dro_conv2d_weight_grad_multi_workspace_bytes(1, B, Hh, Ww, C, C, 3, 3))
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device)
     st = ctypes.c_void_p(stream.cuda_stream)
 
     def launch():
-        _lib.check(lib.dro_convgru_gates_forward(sl, 4, _lib.ptr(wzr), _lib.ptr(bzr), B, Hf, Wf, hd, KH, KW,
-                                                 _lib.ptr(zr), _lib.ptr(rh), None, _lib.ptr(ws), nws, st),
-                   "dro_convgru_gates_forward")
+        _lib.check(lib.dro_conv2d_weight_grad_multi(use, 1, 1, B, Hh, Ww, C, 3, 3, 0, ctypes.c_float(1.0),
+                                                    _lib.ptr(gw), None, 0, _lib.ptr(ws), nb, st),
+                   "dro_conv2d_weight_grad_multi")
     for _ in range(5):
         launch()
     torch.cuda.synchronize()
@@ -323,7 +314,7 @@ def roofline_conv(device, iters=50, traffic_file=None):
     e1.record(stream)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / iters
-    flops = 2.0 * 2 * hd * cin * KH * KW * B * Hf * Wf
+    flops = 2.0 * C * C * 9 * B * Hh * Ww
     achieved = flops / (us * 1e-6) / 1e12
     traffic = None
     if traffic_file and os.path.exists(traffic_file):
@@ -331,11 +322,11 @@ def roofline_conv(device, iters=50, traffic_file=None):
             tf = json.load(f)
         if tf.get("kernels") == kernels:       # measured on this very launch sequence
             traffic = tf.get("hbm_bytes_per_launch")
-    return {"bound": "mfma", "kernel": " + ".join(kernels) + " (SepConvGRU z|r gates fwd, B=2 24x80 "
-            "Cin 160 Cout 128 1x5)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
+    return {"bound": "mfma", "kernel": kernels[0] + " + " + kernels[1] + "Q> (fnet layer1 3x3 weight gradient, "
+            "B=6 48x160, 64 -> 64)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
             "flops_per_launch": int(flops), "avg_launch_us": round(us, 2), "launches": iters,
-            "split_k_blocks": ks, "split_k_waves": kin}
+            "algorithmic_bytes_per_launch": int(4 * (x.numel() + gout.numel() + gw.numel()))}
 
 
 # ----------------------------------------------------------------------------- CPU baseline

@@ -43,6 +43,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "conv_common.hpp"
 #include "dro_common.hpp"
@@ -947,11 +948,14 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(typename WgParam<MULTI>
 // group w >> 2 = tap group (3x3: taps 0-4 / 5-8) or pixel half (T <= 5:
 // summed through LDS at the end).  Same partials as wgrad_halo_kernel
 // ([split][Cout][Cin][T], bias [split][Cout]) and the same finish kernel.
-template <int KH, int KW>
+template <int KH, int KW, int TG>
 struct HaloShapeW2 {
   static constexpr int T = KH * KW;
-  static constexpr bool TAPSPLIT = T == 9;
-  static constexpr int TPW = TAPSPLIT ? 5 : T;
+  // TG == 3 (3x3 only): a block computes one kernel ROW (3 taps) of its
+  // (o, c) tile; the pixel halves of the block reduce through LDS as for the
+  // 1-D shapes.  TG == 1 for a 3x3: all 9 taps, split 5 | 4 over wave groups.
+  static constexpr bool TAPSPLIT = T == 9 && TG == 1;
+  static constexpr int TPW = TAPSPLIT ? 5 : (TG == 3 ? 3 : T);
   static constexpr int TH = HaloShape<32, KH, KW>::TH, TW = 64 / TH;
   static constexpr int HWd = TW + KW - 1;
   static constexpr int HALO = (TH + KH - 1) * HWd;
@@ -964,10 +968,11 @@ struct HaloShapeW2 {
   static_assert(NJ <= 2 && TW % 2 == 0, "halo shape");
 };
 
-template <int KH, int KW, int GACT, bool MULTI>
+template <int KH, int KW, int GACT, bool MULTI, int TG>
 __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T P) {
+  static_assert(TG == 1 || (TG == 3 && KH == 3 && KW == 3), "tap groups: 3x3 rows");
   const IgArgs& a = WgParam<MULTI>::ig(P);
-  using S = HaloShapeW2<KH, KW>;
+  using S = HaloShapeW2<KH, KW, TG>;
   constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
   constexpr int NJ = S::NJ, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE, TPW = S::TPW;
   constexpr bool TAPSPLIT = S::TAPSPLIT;
@@ -977,7 +982,9 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
   const int H = a.g.H, W = a.g.W, Cin = a.g.Cin, Cout = a.g.Cout;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..7
-  const int t = blockIdx.x;
+  const int noc = a.otiles * ((Cin + BC - 1) / BC);
+  const int tg = TG == 1 ? 0 : (int)blockIdx.x / noc;    // kernel row of this block (TG == 3)
+  const int t = (int)blockIdx.x - tg * noc;
   const int ot = t % a.otiles, ct = t / a.otiles;
   const int o0 = ot * 64, c0 = ct * BC;
   const size_t HW = (size_t)H * W;
@@ -986,7 +993,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
   if constexpr (MULTI) ntiles = P.use_tiles * P.nuse;
   const int tbeg = blockIdx.y * a.chunks_per_split;
   const int tend = min(ntiles, tbeg + a.chunks_per_split);
-  const bool do_bias = a.gbias && ct == 0;
+  const bool do_bias = a.gbias && ct == 0 && tg == 0;
   const float galpha = a.galpha;
   float gr[8], yr[GACT ? 8 : 1], xr[8 * NJ], bsum[8];
   unsigned gmask = 0, xmask = 0;
@@ -1086,17 +1093,18 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
     const float* Gs = smem + buf * STAGE;
     const float* Xs = Gs + 64 * GPAD;
     const float* ga = Gs + hi * GPAD + wo * 32 + (lane & 31);
-    const float* xb = Xs + (wc * 32 + (lane & 31)) * HPAD + hi;
+    const float* xb = Xs + (wc * 32 + (lane & 31)) * HPAD + hi + (TG == 3 ? tg * HWd : 0);
     constexpr int KS = TAPSPLIT ? 32 : 16;        // k-steps (pixel pairs) per wave
+    const int pbase = TAPSPLIT ? 0 : wg * 16;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int pp = 2 * ((TAPSPLIT ? 0 : wg * 16) + s);   // even pixel of this k-step
+      const int pp = 2 * (pbase + s);              // even pixel of this k-step
       const float av = ga[pp * GPAD];
       const int poff = (pp / TW) * HWd + (pp % TW);
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {
-        if (k < ntap) {
-          const int tap = tap0 + k;
+        if (TAPSPLIT ? k < ntap : true) {
+          const int tap = (TAPSPLIT ? tap0 : 0) + k;
           const int ty = tap / KW, tx = tap - ty * KW;
           acc[k] = mfma32(av, xb[poff + ty * HWd + tx], acc[k]);
         }
@@ -1126,7 +1134,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
     float* red = smem;   // [4 (o half, c half)][16][64]
     const int q4 = wo + 2 * wc;
 #pragma unroll
-    for (int tp = 0; tp < T; ++tp) {
+    for (int tp = 0; tp < TPW; ++tp) {
       if (wg == 1) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) red[(q4 * 16 + r) * 64 + lane] = acc[tp][r];
@@ -1137,7 +1145,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
         for (int r = 0; r < 16; ++r) {
           const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (o < Cout && c < Cin)
-            wpart[tp * tstride + (size_t)o * Cin + c] = acc[tp][r] + red[(q4 * 16 + r) * 64 + lane];
+            wpart[(tg * TPW + tp) * tstride + (size_t)o * Cin + c] = acc[tp][r] + red[(q4 * 16 + r) * 64 + lane];
         }
       }
       __syncthreads();
@@ -1153,23 +1161,56 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
   }
 }
 
-// wgrad2 partials: dW[o][c][tap] = sum_s part[s][tap][o][c] (threads walk the
-// partials' coalesced (tap, o, c) order); db[o] = sum_s bpart[s][o]
+// wgrad2 partials: dW[o][c][tap] = sum_s part[s][tap][o][c]; db[o] = sum_s bpart[s][o].
+// Threads walk the partials' coalesced (tap, o, c) order.  The reduction is
+// latency-bound (few output elements, up to 256 partials each), so Q lanes
+// of a wave share one element: lane group q sums the q-th contiguous range of
+// splits (split_sum, 4 chains), and the Q range sums are combined by shuffles
+// in a fixed tree -- the same order on every run.
+template <int Q>
 __global__ __launch_bounds__(256) void wgrad2_finish_kernel(IgArgs a, int splits) {
+  constexpr int EPW = 64 / Q;                     // elements per wave
   const int Cout = a.g.Cout, Cin = a.g.Cin, T = a.g.KH * a.g.KW;
   const long long oc = (long long)Cout * Cin, total = oc * T;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const float v = split_sum(a.part + e, (size_t)total, splits);
-    const int tap = (int)(e / oc);
-    const long long r = e - (long long)tap * oc;        // o * Cin + c
-    const size_t dst = (size_t)r * T + tap;
-    a.gweight[dst] = a.wacc ? a.gweight[dst] + v : v;
-    if (a.gbias && e < Cout) {
+  const int lane = threadIdx.x & 63, q = lane / EPW, le = lane - q * EPW;
+  const int per = (splits + Q - 1) / Q;
+  const int s0 = min(splits, q * per), n = min(splits, s0 + per) - s0;
+  const long long wstride = (long long)gridDim.x * (blockDim.x / 64) * EPW;
+  for (long long eb = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * EPW; eb < total;
+       eb += wstride) {
+    const long long e = eb + le;
+    const bool ok = e < total;
+    float v = ok ? split_sum(a.part + (size_t)s0 * total + e, (size_t)total, n) : 0.f;
+    // every lane shuffles (a shuffle under a lane-dependent branch would read
+    // inactive lanes); a + b == b + a exactly, so each pair's sum is one value
+    if (Q >= 4) v += __shfl_xor(v, 2 * EPW);      // (q0 + q2), (q1 + q3)
+    if (Q >= 2) {
+      const float o = __shfl_xor(v, EPW);
+      v = q & 1 ? o + v : v + o;
+    }
+    if (ok && q == 0) {
+      const int tap = (int)(e / oc);
+      const long long r = e - (long long)tap * oc;        // o * Cin + c
+      const size_t dst = (size_t)r * T + tap;
+      a.gweight[dst] = a.wacc ? a.gweight[dst] + v : v;
+    }
+  }
+  if (a.gbias) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < Cout; e += gridDim.x * blockDim.x) {
       const float bv = split_sum(a.bpart + e, (size_t)Cout, splits);
       a.gbias[e] = a.wacc ? a.gbias[e] + bv : bv;
     }
   }
+}
+
+static void launch_wgrad2_finish(const IgArgs& a, int splits, hipStream_t s) {
+  const long long total = (long long)a.g.Cout * a.g.Cin * a.g.KH * a.g.KW;
+  const int Q = splits >= 32 ? 4 : splits >= 8 ? 2 : 1;
+  long long blocks = (total * Q + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (Q == 4) hipLaunchKernelGGL(wgrad2_finish_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
+  else if (Q == 2) hipLaunchKernelGGL(wgrad2_finish_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
+  else hipLaunchKernelGGL(wgrad2_finish_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
 }
 
 // dW[o][c][tap] = sum_s part[s][o][c][tap]; db[o] = sum_s bpart[s][o]
@@ -1376,6 +1417,7 @@ struct WhPlan {
   bool ok;
   int otiles, ctiles, tiles_x, tiles_img, splits, tiles_per_split;
   size_t part_bytes;
+  int tgroups;   // wgrad2, 3x3: blocks per (o, c) tile along the kernel rows (1 or 3)
 };
 
 WhPlan plan_wgrad_halo(int Cin, int Cout, int KH, int KW, int B, int H, int W) {
@@ -1429,16 +1471,25 @@ WhPlan plan_wgrad2(int Cin, int Cout, int KH, int KW, int ntiles_total, int B, i
   const int ntiles = ntiles_total > 0 ? ntiles_total : B * pl.tiles_img;
   pl.otiles = (Cout + 63) / 64;
   pl.ctiles = (Cin + 63) / 64;
-  const int blocks = pl.otiles * pl.ctiles;
+  // 3x3: one block per kernel row of a tile -- 3x the blocks at the same
+  // split count, so a third of the split partials for the same occupancy
+  // measured (fnet layer1 wgrad, B=6 48x160 64->64): 3 row groups 72 + 5 us
+  // vs all 9 taps per block 51 + 8 us -- staging per MFMA triples; default 1
+  static const int tg3 = [] {   // tuning override: DRO_WG2_TGROUPS=3 (default 1)
+    const char* e = getenv("DRO_WG2_TGROUPS");
+    return e && atoi(e) == 3 ? 3 : 1;
+  }();
+  pl.tgroups = (KH == 3 && KW == 3) ? tg3 : 1;
+  const int blocks = pl.otiles * pl.ctiles * pl.tgroups;
   static const int target = [] {   // tuning override: DRO_WG2_TARGET_BLOCKS (default 256)
     const char* e = getenv("DRO_WG2_TARGET_BLOCKS");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 256;
   }();
-  static const int min_tiles = [] {   // tuning override: DRO_WG2_MIN_TILES (default 4)
+  static const int min_tiles = [] {   // tuning override: DRO_WG2_MIN_TILES (default 1, measured best)
     const char* e = getenv("DRO_WG2_MIN_TILES");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 4;
+    return v > 0 ? v : 1;
   }();
   int sp = (target + blocks - 1) / blocks;
   if (sp > 256) sp = 256;
@@ -2109,20 +2160,19 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.chunks_per_split = w2.tiles_per_split;
     a.part = reinterpret_cast<float*>(ws_wg);
     a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)w2.splits * Cout * a.g.Cin * T * sizeof(float)));
-    const dim3 grid((unsigned)(w2.otiles * w2.ctiles), (unsigned)w2.splits);
+    const dim3 grid((unsigned)(w2.otiles * w2.ctiles * w2.tgroups), (unsigned)w2.splits);
     const int gact = fold ? act : 0;
-    conv_logf(2.0 * Cout * a.g.Cin * T * (double)P, "wgrad2_kernel<%d, %d, %d, false>", KH, KW, gact);
-#define DRO_WG2(KH_, KW_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad2_kernel<KH_, KW_, A_, false>), grid, dim3(512), 0, s, a))
-    if (KH == 1 && KW == 1) { DRO_WG2(1, 1); }
-    else if (KH == 1) { DRO_WG2(1, 5); }
-    else if (KW == 1) { DRO_WG2(5, 1); }
-    else { DRO_WG2(3, 3); }
+    conv_logf(2.0 * Cout * a.g.Cin * T * (double)P, "wgrad2_kernel<%d, %d, %d, false, %d>", KH, KW, gact,
+              w2.tgroups);
+#define DRO_WG2(KH_, KW_, TG_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad2_kernel<KH_, KW_, A_, false, TG_>), grid, dim3(512), 0, s, a))
+    if (KH == 1 && KW == 1) { DRO_WG2(1, 1, 1); }
+    else if (KH == 1) { DRO_WG2(1, 5, 1); }
+    else if (KW == 1) { DRO_WG2(5, 1, 1); }
+    else if (w2.tgroups == 3) { DRO_WG2(3, 3, 3); }
+    else { DRO_WG2(3, 3, 1); }
 #undef DRO_WG2
     if ((st = launch_status("wgrad2_kernel launch failed"))) return st;
-    const long long total = (long long)Cout * a.g.Cin * T;
-    long long blocks = (total + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(wgrad2_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, w2.splits);
+    launch_wgrad2_finish(a, w2.splits, s);
     if ((st = launch_status("wgrad_halo_finish_kernel launch failed"))) return st;
   } else if (grad_weight && wh.ok) {
     a.otiles = wh.otiles;
@@ -2275,15 +2325,21 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
     a.dbg = e ? atoi(e) : 0;
   }
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)(wh.otiles * wh.ctiles), (unsigned)wh.splits);
-  conv_logf(2.0 * Cout * Cin * T * (double)B * H * W * nuse, v2 ? "wgrad2_kernel<%d, %d, %d, true>"
-            : "wgrad_halo_kernel<%d, %d, %d, true>", KH, KW, act);
+  const int tgroups = v2 ? wh.tgroups : 1;
+  const dim3 grid((unsigned)(wh.otiles * wh.ctiles * tgroups), (unsigned)wh.splits);
+  if (v2)
+    conv_logf(2.0 * Cout * Cin * T * (double)B * H * W * nuse, "wgrad2_kernel<%d, %d, %d, true, %d>", KH, KW,
+              act, tgroups);
+  else
+    conv_logf(2.0 * Cout * Cin * T * (double)B * H * W * nuse, "wgrad_halo_kernel<%d, %d, %d, true>", KH, KW,
+              act);
   if (v2) {
-#define DRO_WG2M(KH_, KW_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad2_kernel<KH_, KW_, A_, true>), grid, dim3(512), 0, s, m))
-    if (KH == 1 && KW == 1) { DRO_WG2M(1, 1); }
-    else if (KH == 1) { DRO_WG2M(1, 5); }
-    else if (KW == 1) { DRO_WG2M(5, 1); }
-    else { DRO_WG2M(3, 3); }
+#define DRO_WG2M(KH_, KW_, TG_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad2_kernel<KH_, KW_, A_, true, TG_>), grid, dim3(512), 0, s, m))
+    if (KH == 1 && KW == 1) { DRO_WG2M(1, 1, 1); }
+    else if (KH == 1) { DRO_WG2M(1, 5, 1); }
+    else if (KW == 1) { DRO_WG2M(5, 1, 1); }
+    else if (tgroups == 3) { DRO_WG2M(3, 3, 3); }
+    else { DRO_WG2M(3, 3, 1); }
 #undef DRO_WG2M
   } else {
 #define DRO_WHM(KH_, KW_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad_halo_kernel<KH_, KW_, A_, true>), grid, dim3(256), 0, s, m))
@@ -2298,7 +2354,7 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
   long long blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (v2)
-    hipLaunchKernelGGL(wgrad2_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
+    launch_wgrad2_finish(a, wh.splits, s);
   else
     hipLaunchKernelGGL(wgrad_halo_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, wh.splits);
   return launch_status("wgrad_halo_finish_kernel launch failed");

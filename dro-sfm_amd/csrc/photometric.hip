@@ -28,6 +28,8 @@
 // reduce, 16*HW per prediction for smoothness.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dro_common.hpp"
 
 namespace dro {
@@ -125,6 +127,95 @@ __device__ __forceinline__ void stage_warp(const PhotoArgs& a, const float* __re
         est[c * PL + k] = s;
       }
     }
+  }
+}
+
+// Backward staging: est over the 2-px-halo tile exactly as stage_warp<PL2,
+// W2, 2> computes it, with this thread's own interior pixels (ly = tid / TW +
+// r * (kThreads / TW), lx = tid % TW) among the pixels it stages, so the
+// bilinear derivative terms d est_c / d ix, d est_c / d iy of those pixels
+// come from the same four gathers (a second projection + 12 gathers per pixel
+// otherwise).  Ring pixels (the 2-px halo, 304 of them) are spread over the
+// threads after the interior ones.
+__device__ __forceinline__ void stage_warp_bwd(const PhotoArgs& a, const float* __restrict__ ctx,
+                                               const float* __restrict__ invt, const float ki[9],
+                                               const float kr[9], const float R[9], const float t[3],
+                                               int x0, int y0, float* __restrict__ est,
+                                               float (&dxc)[kPxPerThread][3], float (&dyc)[kPxPerThread][3]) {
+  constexpr int PW = W2, PL = H2 * W2, HALO = 2;
+  constexpr int NRING = PL - TH * TW;
+  constexpr int NR = (NRING + kThreads - 1) / kThreads;
+  static_assert(kPxPerThread == 2 && NR == 2, "two interior + two ring slots per thread");
+  const size_t HW = (size_t)a.H * a.W;
+  auto ring_k = [](int h) {
+    if (h < 2 * PW) return h;                                   // rows 0, 1
+    h -= 2 * PW;
+    if (h < 2 * PW) return (H2 - 2) * PW + h;                   // rows H2-2, H2-1
+    h -= 2 * PW;                                                // rows 2..H2-3, cols 0, 1, PW-2, PW-1
+    const int row = 2 + h / 4, c4 = h % 4;
+    return row * PW + (c4 < 2 ? c4 : PW - 4 + c4);
+  };
+  // one group of U pixels at a time: their gathers are in flight together
+  // (interior pixels one by one -- their derivative terms stay live after)
+  auto group = [&](auto u_c, const int (&kk)[decltype(u_c)::value], const bool (&valid)[decltype(u_c)::value],
+                   int slot0, bool interior) {
+    constexpr int U = decltype(u_c)::value;
+    Taps T[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = kk[u];
+      const int gy = reflect_idx(y0 + k / PW - HALO, a.H), gx = reflect_idx(x0 + k % PW - HALO, a.W);
+      float dd;
+      const float depth = decode_depth(invt[k], DRO_DEPTH_INV, 0.f, 0.f, &dd);
+      Proj q;
+      project(ki, kr, R, t, (float)gx, (float)gy, depth, a.H, a.W, q);
+      bilinear_taps(q.ix, q.iy, a.H, a.W, T[u]);
+    }
+    float v[U][3][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[u][c][q] = ctx[c * HW + (T[u].ok[q] ? T[u].idx[q] : 0)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!valid[u]) continue;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (T[u].ok[q]) s += v[u][c][q] * T[u].wgt[q];
+        est[c * PL + kk[u]] = s;
+        if (interior) {
+          float z[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z[q] = T[u].ok[q] ? v[u][c][q] : 0.f;
+          const float omy = 1.f - T[u].ty, omx = 1.f - T[u].tx;
+          dxc[slot0 + u][c] = (z[1] - z[0]) * omy + (z[3] - z[2]) * T[u].ty;
+          dyc[slot0 + u][c] = (z[2] - z[0]) * omx + (z[3] - z[1]) * T[u].tx;
+        }
+      }
+    }
+  };
+#pragma unroll
+  for (int r = 0; r < kPxPerThread; ++r) {
+    const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
+    const int kk[1] = {(ly + HALO) * PW + lx + HALO};
+    const bool valid[1] = {true};
+    group(std::integral_constant<int, 1>{}, kk, valid, r, true);
+  }
+  {
+    int kk[2];
+    bool valid[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int h = threadIdx.x + u * kThreads;
+      valid[u] = h < NRING;
+      kk[u] = ring_k(valid[u] ? h : 0);
+    }
+    group(std::integral_constant<int, 2>{}, kk, valid, 0, false);
   }
 }
 
@@ -496,37 +587,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     load_pose(a.pose + ((size_t)(j * a.n + i) * a.B + b) * ps, a.pose_mode, R, t);
     const float* ctx = a.context + ((size_t)j * a.B + b) * 3 * HW;
     const int kw = a.automask ? 2 * j : j;
-    if (j) __syncthreads();
-    stage_warp<PL2, W2, 2>(a, ctx, invt, ki, kr, R, t, x0, y0, est);
-    __syncthreads();
-    // (1) projections and bilinear taps of the thread's pixels: only the
-    // bilinear derivative terms stay live (6 floats per pixel); the projection
-    // is recomputed for the chain rule in (3).  Their context gathers are in
-    // flight while the first adjoint plane is formed.
-    float dxc[kPxPerThread][3], dyc[kPxPerThread][3];
-#pragma unroll
-    for (int r = 0; r < kPxPerThread; ++r) {
-      const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
-      const int gy = y0 + ly, gx = x0 + lx;
-      float dd;
-      const float depth = decode_depth(invt[(ly + 2) * W2 + (lx + 2)], DRO_DEPTH_INV, 0.f, 0.f, &dd);
-      Proj q;
-      Taps T;
-      project(ki, kr, R, t, (float)gx, (float)gy, depth, H, W, q);
-      bilinear_taps(q.ix, q.iy, H, W, T);
-      const float omy = 1.f - T.ty, omx = 1.f - T.tx;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float x = ctx[c * HW + (T.ok[k] ? T.idx[k] : 0)];
-          v[k] = T.ok[k] ? x : 0.f;
-        }
-        dxc[r][c] = (v[1] - v[0]) * omy + (v[3] - v[2]) * T.ty;
-        dyc[r][c] = (v[2] - v[0]) * omx + (v[3] - v[1]) * T.tx;
+    // a ref none of whose candidates is selected in the tile's 1-px ring adds
+    // nothing (every adjoint and L1 term of the tile is zero): skip it
+    if (a.reduce_min) {
+      int any = 0;
+      for (int k = threadIdx.x; k < PL1; k += kThreads) any |= selt[k] == kw;
+      if (!__syncthreads_or(any)) {
+        if (a.part_pose && threadIdx.x < 12)
+          a.part_pose[(((size_t)(j * a.n + i) * a.B + b) * tiles + tile) * 12 + threadIdx.x] = 0.0;
+        continue;
       }
+    } else if (j) {
+      __syncthreads();
     }
+    // (1) the warped tile and, from the same gathers, the bilinear derivative
+    // terms of the thread's own pixels (the projection is recomputed for the
+    // chain rule in (3))
+    float dxc[kPxPerThread][3], dyc[kPxPerThread][3];
+    stage_warp_bwd(a, ctx, invt, ki, kr, R, t, x0, y0, est, dxc, dyc);
+    __syncthreads();
     float gix[kPxPerThread], giy[kPxPerThread];
 #pragma unroll
     for (int r = 0; r < kPxPerThread; ++r) gix[r] = giy[r] = 0.f;
