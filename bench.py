@@ -129,7 +129,11 @@ def roofline_photometric(B, device, iters=20):
     g.manual_seed(5)
     img = smooth_images(B, g, device)
     ctx = torch.stack([smooth_images(B, g, device) for _ in range(NREF)])
-    invs = (0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g, device=device)).requires_grad_(True)
+    # inverse depths as the net produces them: smooth fields upsampled from 1/8
+    # resolution (per-pixel noise would scatter every warp's gathers)
+    low = 0.02 + 0.3 * torch.rand(n * B, 1, H // 8, W // 8, generator=g, device=device)
+    invs = torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
+    invs = invs.view(n, B, 1, H, W).contiguous().requires_grad_(True)
     pose = torch.cat([0.1 * torch.randn(NREF, n, B, 3, generator=g, device=device),
                       0.02 * torch.randn(NREF, n, B, 3, generator=g, device=device)], 3).requires_grad_(True)
     K = torch.tensor(WL["K"], device=device).unsqueeze(0).repeat(B, 1, 1)
@@ -154,19 +158,11 @@ def roofline_photometric(B, device, iters=20):
     bwd_bytes = HW * B * (12 + 12 * NREF) + HW * B * n * 9
     total_bytes = fwd_bytes + bwd_bytes
     achieved = total_bytes / ((fwd_ms + bwd_ms) * 1e-3) / 1e9
-    # HBM bytes of a call pair at this shape from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over
-    # tools/bench_photo.py (profiles/r2_photometric_counters.json, FETCH_SIZE x2 for gfx950)
-    traffic = None
-    pf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2_photometric_counters.json")
-    if os.path.exists(pf) and n == 9 and (H, W) == (192, 640) and B == 2:
-        pc = json.load(open(pf))
-        traffic = int(sum(v["hbm_fetch_bytes_corrected"] for v in pc["xcd_band_order"].values())
-                      + sum(pc["write_bytes_per_call"].values()))
     return {"bound": "hbm", "kernel": "photometric fwd+bwd (photo_fwd_kernel + photo_bwd_kernel)",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "note": "latency-bound, not HBM-bound: VALU issue ~16% of the chip, ~49% of wave cycles "
-                    "waiting (profiles/r2_photometric_counters.json)",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "note": "gather/latency-bound, not HBM-bound (profiles/r2_photometric_counters.json); the "
+                    "backward's time depends on the min-selection (a ref unselected in a tile is skipped)",
             "algorithmic_bytes": int(total_bytes), "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)}
 
 
@@ -404,8 +400,9 @@ def main():
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",
                     help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
-    ap.add_argument("--concurrent-blocks", action="store_true",
-                    help="pose update block on a side stream beside the depth block (A/B)")
+    ap.add_argument("--serial-blocks", action="store_true",
+                    help="A/B: pose update block after the depth block on one stream (default: the "
+                         "pose block on a side stream beside the depth block)")
     ap.add_argument("--no-grad-sinks", action="store_true",
                     help="autograd's per-use gradient sums instead of in-place gradient sinks (A/B)")
     ap.add_argument("--aten-maxpool", action="store_true",
@@ -441,7 +438,7 @@ def main():
     _update.set_conv_backend(args.conv_backend)
     from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
     _dpn.set_concurrent_encoders(args.concurrent_encoders)
-    _dpn.set_concurrent_blocks(args.concurrent_blocks)
+    _dpn.set_concurrent_blocks(not args.serial_blocks)
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     _extractor.set_native_maxpool(not args.aten_maxpool)
@@ -505,7 +502,7 @@ def main():
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_convs": args.conv_backend,
                    "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
-                   "update_blocks": "concurrent streams" if args.concurrent_blocks else "serial",
+                   "update_blocks": "serial" if args.serial_blocks else "concurrent streams",
                    "grad_sinks": not args.no_grad_sinks,
                    "split_engine": args.split_engine,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",

@@ -61,13 +61,16 @@ def set_concurrent_encoders(enabled):
     _CONCURRENT[0] = bool(enabled)
 
 
-_CONCURRENT_BLOCKS = [False]
+_CONCURRENT_BLOCKS = [True]
 
 
 def set_concurrent_blocks(enabled):
     """Run the pose update block on a side stream beside the depth update block
-    (they are independent within an outer iteration: each reads the other's
-    state of the previous iteration, detached; DepthPoseNet.py:154-197)."""
+    (default True; False for A/B runs).  They are independent within an outer
+    iteration: each reads the other's state of the previous iteration,
+    detached (DepthPoseNet.py:154-197).  Under hipGraph replay the two chains
+    of small launches overlap: 16.9 vs 19.0 ms/step (round 3, one box, two
+    interleaved runs each); eager, 32.7 vs 32.0."""
     _CONCURRENT_BLOCKS[0] = bool(enabled)
 
 
@@ -169,11 +172,11 @@ class DepthPoseNet(nn.Module):
         fmaps = self.fnet(torch.cat([target_image] + list(ref_imgs), 0))
         assert target_image.shape[2] // fmaps.shape[2] == self.feat_ratio
         h, w = fmaps.shape[2:]
-        fmap1, frefs = torch.split(fmaps, [B, N * B], 0)
-        frefs = frefs.view(N, B, C, h, w)               # free view: all refs, one tensor
+        fmap1_raw, frefs_raw = torch.split(fmaps, [B, N * B], 0)
+        frefs_raw = frefs_raw.view(N, B, C, h, w)       # free view: all refs, one tensor
         # every cost call reads the same feature maps: their gradients are summed
         # in place by the warp-cost backward (no per-call add launches)
-        fmap1, frefs = hip.grad_sink(fmap1), hip.grad_sink(frefs)
+        fmap1, frefs = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_raw)
 
         # initial poses of all refs in one pass: cat([fmap1, fmap_ref_j]) per ref j
         pair = torch.cat([fmap1.unsqueeze(0).expand(N, B, C, h, w), frefs], 2).view(N * B, 2 * C, h, w)
@@ -190,12 +193,25 @@ class DepthPoseNet(nn.Module):
             for t in (h_d, x_d, h_p, x_p):
                 t.record_stream(main)
 
-        if self.iters > 0:
-            # the context features feed every GRU step: gradients summed in place
-            x_d, x_p = hip.grad_sink(x_d), hip.grad_sink(x_p)
         pside = None
         if self.iters > 0 and _CONCURRENT_BLOCKS[0] and target_image.is_cuda:
             pside = _side_streams(target_image.device)[1]
+        fmap1_p, frefs_p = fmap1, frefs
+        if self.iters > 0:
+            # the context features feed every GRU step: gradients summed in place
+            x_d = hip.grad_sink(x_d)
+            if pside is None:
+                x_p = hip.grad_sink(x_p)
+            else:
+                # the pose block's sinks live on its stream: their consumers (the
+                # pose block's backward kernels) write them there, and the sink
+                # nodes hand them on from there (a sink shared with the depth
+                # block would be written from two streams at once)
+                main = torch.cuda.current_stream(target_image.device)
+                pside.wait_stream(main)
+                with torch.cuda.stream(pside):
+                    x_p = hip.grad_sink(x_p)
+                    fmap1_p, frefs_p = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_raw)
         for _ in range(self.iters):
             disp = disp.detach()
             poses = poses.detach()
@@ -212,7 +228,7 @@ class DepthPoseNet(nn.Module):
 
             def pose_block(h_p):
                 # pose block over all N refs at once; depth frozen at this outer step
-                pose_cost = lambda q: self._cost(fmap1, frefs, frozen_disp, q.view(N, B, 6), K,
+                pose_cost = lambda q: self._cost(fmap1_p, frefs_p, frozen_disp, q.view(N, B, 6), K,
                                                  False).view(N * B, C, h, w)
                 h_p, seq = self.update_block_pose(h_p, pose_cost, frozen_poses.reshape(N * B, 6), x_p,
                                                   seq_len=self.seq_len)
@@ -227,7 +243,7 @@ class DepthPoseNet(nn.Module):
                 # outer step: it runs on a side stream beside the depth block
                 main = torch.cuda.current_stream(target_image.device)
                 pside.wait_stream(main)
-                for t in (fmap1, frefs, frozen_disp, frozen_poses, h_p, x_p, K):
+                for t in (fmap1_p, frefs_p, frozen_disp, frozen_poses, h_p, x_p, K):
                     t.record_stream(pside)
                 with torch.cuda.stream(pside):
                     h_p, seq = pose_block(h_p)

@@ -146,3 +146,40 @@ def test_grad_sinks_match_per_use_gradients():
             assert err < 1e-2, (k, err)
         else:
             torch.testing.assert_close(g1[k], g2[k], rtol=1e-4, atol=1e-6, msg=lambda m, k=k: f"{k}: {m}")
+
+
+def test_concurrent_blocks_match_serial():
+    """The pose update block on a side stream beside the depth block (the
+    default) gives the serial step's loss and gradients -- eager and under
+    hipGraph replay.  The blocks share the feature maps: each stream has its
+    own gradient sinks for them (DepthPoseNet._forward), so the only
+    difference left is the order in which the two blocks' feature gradients
+    are summed (fp32 reassociation)."""
+    from dro_sfm_amd.networks.depth_pose import DepthPoseNet as dpn
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep
+    batch = _batch()
+    K0 = batch["intrinsics"].clone()
+    res = {}
+    try:
+        with torch.backends.cudnn.flags(enabled=False):
+            for name, concurrent, graph in (("serial", False, False), ("concurrent", True, False),
+                                            ("concurrent_graph", True, True)):
+                dpn.set_concurrent_blocks(concurrent)
+                m = _setup()
+                tr = DataParallelTrainer(m, capturable=graph, lr=0.0)
+                batch["intrinsics"].copy_(K0)
+                if graph:
+                    gs = GraphedTrainStep(tr, batch, warmup=2)
+                    batch["intrinsics"].copy_(K0)
+                    loss = gs.step(batch, flip=False)[0].clone()
+                else:
+                    loss = tr.step(batch, flip=False)[0].clone()
+                torch.cuda.synchronize()
+                res[name] = (loss, tr.grads.flat.clone())
+    finally:
+        dpn.set_concurrent_blocks(True)
+    l0, g0 = res["serial"]
+    for name in ("concurrent", "concurrent_graph"):
+        l1, g1 = res[name]
+        assert O.rel_err(l1.cpu(), l0.cpu()) < 1e-5, name
+        assert float((g1 - g0).norm() / g0.norm()) < 1e-4, name
