@@ -31,7 +31,8 @@ for step in "$@"; do
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchmi) run bench_miopen 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --conv-backend miopen ;;
     benchnd) run bench_nodirect 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-direct-wgrad ;;
-    benchside) run bench_side 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
+    benchside) run bench_side 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
+    benchnosink) run bench_nosink 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-grad-sinks ;;
     benchsf) run bench_splitfinish 600 env DRO_SPLIT_FINISH=1 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     benche) run bench_eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --eager ;;
     benchn) run bench_native 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-miopen ;;
@@ -46,7 +47,7 @@ for step in "$@"; do
     benchsink) run bench_sink 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --grad-sinks ;;
     benchab) run bench_a 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     benchnobn) run bench_nofusedbn 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-fused-bn ;;
-    benchconc) run bench_conc 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --concurrent-encoders ;;
+    benchconc) run bench_conc 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --concurrent-encoders ;;
     convkin) for k in 1 2 4; do run "bench_conv_kin$k" 300 env DRO_CONV_KIN=$k python tools/bench_conv.py --iters 30; done ;;
     stampkin) for k in 1 2 4; do run "conv_stamps_kin$k" 300 env DRO_CONV_KIN=$k python tools/conv_stamps.py; done ;;
     kinthr) for t in 512 1024 2048; do run "bench_kin2_below$t" 600 env DRO_CONV_KIN2_BELOW=$t python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline; done ;;
