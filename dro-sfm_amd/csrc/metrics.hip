@@ -35,7 +35,20 @@ struct MetArgs {
   int y1, y2, x1, x2;   // crop rectangle [y1, y2) x [x1, x2); y1 < 0: no crop
   float sy, sx;         // (h-1)/(H-1), (w-1)/(W-1) in fp32 (ATen's area_pixel_compute_scale)
   int same;             // prediction already at the gt resolution
+  // compute_depth_metrics_demon (utils/depth.py:343-398): no clamp to the
+  // depth range; with gt scaling the gt is divided by the norm of the first
+  // reference's gt translation, gpose[b * pose_stride + {3, 7, 11}]
+  int demon;
+  const float* gpose;
+  long long pose_stride;
 };
+
+// |t| of image b's first-reference gt translation (torch.sqrt(t.dot(t)) in fp32)
+__device__ __forceinline__ float met_tnorm(const MetArgs& a, int b) {
+  const float* p = a.gpose + (size_t)b * a.pose_stride;
+  const float x = p[3], y = p[7], z = p[11];
+  return sqrtf(__fadd_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)), __fmul_rn(z, z)));
+}
 
 __device__ __forceinline__ bool met_valid(const MetArgs& a, float g, int y, int x) {
   bool v = g > a.min_d && g < a.max_d;
@@ -67,13 +80,14 @@ __global__ __launch_bounds__(kMetThreads) void metrics_prepare_kernel(MetArgs a,
   const size_t HW = (size_t)a.H * a.W;
   const size_t p = (size_t)blockIdx.x * kMetThreads + threadIdx.x;
   int v = 0;
+  const float tn = a.gpose ? met_tnorm(a, b) : 1.f;
   if (p < HW) {
     const int y = (int)(p / a.W), x = (int)(p % a.W);
     const float g = gt[b * HW + p];
     const float pv = fmaxf(met_upsample(a, pred + (size_t)b * a.h * a.w, y, x), 1e-6f);
     pred_up[b * HW + p] = pv;
     v = met_valid(a, g, y, x) ? 1 : 0;
-    ratio[b * HW + p] = v ? g / pv : INFINITY;
+    ratio[b * HW + p] = v ? (a.gpose ? g / tn : g) / pv : INFINITY;
   }
   // block count of valid pixels (wave ballot, then the block's waves in order)
   const unsigned long long m = __ballot(v);
@@ -94,17 +108,23 @@ __global__ __launch_bounds__(kMetThreads) void metrics_reduce_kernel(MetArgs a, 
   const int b = blockIdx.y;
   const size_t HW = (size_t)a.H * a.W;
   const float s = scale ? scale[b] : 1.f;
+  const float tn = a.gpose ? met_tnorm(a, b) : 1.f;
   double acc[kMetSlots];
 #pragma unroll
   for (int k = 0; k < kMetSlots; ++k) acc[k] = 0.0;
   // grid-stride over the image: a fixed pixel -> (block, thread) assignment
   for (size_t p = (size_t)blockIdx.x * kMetThreads + threadIdx.x; p < HW; p += (size_t)gridDim.x * kMetThreads) {
     const int y = (int)(p / a.W), x = (int)(p % a.W);
-    const float g = gt[b * HW + p];
+    float g = gt[b * HW + p];
     if (!met_valid(a, g, y, x)) continue;
     float pv = pred_up[b * HW + p];
-    if (scale) pv = fminf(fmaxf(pv * s, a.min_d), a.max_d);   // median scaling + clamp
-    pv = fminf(fmaxf(pv, a.min_d), a.max_d);
+    if (a.demon) {                                              // :364-373: no clamps
+      if (a.gpose) g = g / tn;
+      if (scale) pv = pv * s;
+    } else {
+      if (scale) pv = fminf(fmaxf(pv * s, a.min_d), a.max_d);   // median scaling + clamp
+      pv = fminf(fmaxf(pv, a.min_d), a.max_d);
+    }
     const float th = fmaxf(g / pv, pv / g);
     const float d = g - pv;
     const float ld = logf(g) - logf(pv);
@@ -276,6 +296,9 @@ int met_setup(MetArgs& a, int B, int H, int W, int h, int w, float min_d, float 
   a.same = (h == H && w == W) ? 1 : 0;
   a.sy = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
   a.sx = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  a.demon = 0;
+  a.gpose = nullptr;
+  a.pose_stride = 0;
   return DRO_OK;
 }
 }  // namespace
@@ -347,6 +370,53 @@ extern "C" int dro_depth_metrics_reduce(const float* gt, const float* pred_up, c
   MetArgs a;
   int st = met_setup(a, B, H, W, H, W, min_depth, max_depth, crop_y1, crop_y2, crop_x1, crop_x2);
   if (st) return st;
+  double* partial = (double*)workspace;
+  hipLaunchKernelGGL(metrics_reduce_kernel, dim3(kReduceBlocks, B), dim3(kMetThreads), 0, (hipStream_t)stream,
+                     a, gt, pred_up, scale, partial);
+  if ((st = launch_status("metrics_reduce_kernel launch failed"))) return st;
+  hipLaunchKernelGGL(metrics_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, kReduceBlocks,
+                     partial, metrics);
+  return launch_status("metrics_finalize_kernel launch failed");
+}
+
+// compute_depth_metrics_demon (utils/depth.py:343-398): the same three passes
+// (prepare, dro_depth_metrics_median, reduce) without crop or clamps; with
+// gt_pose (gt scaling on) the ground truth is divided by |t| of each image's
+// first-reference gt translation (gt_pose + b * pose_stride floats, a row-major
+// 4x4 or 3x4 transform).  gt_pose NULL: no gt normalisation (use_gt_scale False).
+extern "C" int dro_depth_metrics_demon_prepare(const float* gt, const float* pred, const float* gt_pose,
+                                               long long pose_stride, int B, int H, int W, int h, int w,
+                                               float min_depth, float max_depth, float* pred_up, float* ratio,
+                                               int* block_counts, void* stream) {
+  if (!gt || !pred || !pred_up || !ratio || !block_counts) {
+    set_error("depth_metrics_demon_prepare: NULL pointer");
+    return DRO_E_NULL;
+  }
+  MetArgs a;
+  int st = met_setup(a, B, H, W, h, w, min_depth, max_depth, -1, -1, -1, -1);
+  if (st) return st;
+  a.demon = 1;
+  a.gpose = gt_pose;
+  a.pose_stride = pose_stride;
+  hipLaunchKernelGGL(metrics_prepare_kernel, dim3(dro_depth_metrics_blocks(H, W), B), dim3(kMetThreads), 0,
+                     (hipStream_t)stream, a, gt, pred, pred_up, ratio, block_counts);
+  return launch_status("metrics_prepare_kernel launch failed");
+}
+
+extern "C" int dro_depth_metrics_demon_reduce(const float* gt, const float* pred_up, const float* scale,
+                                              const float* gt_pose, long long pose_stride, int B, int H, int W,
+                                              float min_depth, float max_depth, float* metrics, void* workspace,
+                                              void* stream) {
+  if (!gt || !pred_up || !metrics || !workspace) {
+    set_error("depth_metrics_demon_reduce: NULL pointer");
+    return DRO_E_NULL;
+  }
+  MetArgs a;
+  int st = met_setup(a, B, H, W, H, W, min_depth, max_depth, -1, -1, -1, -1);
+  if (st) return st;
+  a.demon = 1;
+  a.gpose = gt_pose;
+  a.pose_stride = pose_stride;
   double* partial = (double*)workspace;
   hipLaunchKernelGGL(metrics_reduce_kernel, dim3(kReduceBlocks, B), dim3(kMetThreads), 0, (hipStream_t)stream,
                      a, gt, pred_up, scale, partial);

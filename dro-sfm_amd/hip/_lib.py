@@ -33,6 +33,7 @@ def load():
             "`make -C dro-sfm_amd/csrc` (or __graft_entry__.build()).  There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     P, I, F, S, Z = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+    LL = ctypes.c_longlong
     _sig(lib.dro_last_error, restype=ctypes.c_char_p)
     _sig(lib.dro_abi_version)
     _sig(lib.dro_warp_cost_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, P, S)
@@ -60,6 +61,8 @@ def load():
     _sig(lib.dro_depth_metrics_reduce, P, P, P, I, I, I, F, F, I, I, I, I, P, P, S)
     _sig(lib.dro_depth_metrics_median_workspace_bytes, I, restype=Z)
     _sig(lib.dro_depth_metrics_median, P, P, I, I, I, P, P, S)
+    _sig(lib.dro_depth_metrics_demon_prepare, P, P, P, LL, I, I, I, I, I, F, F, P, P, P, S)
+    _sig(lib.dro_depth_metrics_demon_reduce, P, P, P, P, LL, I, I, I, F, F, P, P, S)
     _sig(lib.dro_resize_rgb8_to_tensor, P, I, I, I, I, I, P, P, I, P, P, I, P, P, S)
     _sig(lib.dro_color_jitter_rgb8, P, I, I, I, P, P, S)
     _sig(lib.dro_resize_rgb8, P, I, I, I, I, I, P, P, I, P, P, I, P, P, S)
@@ -98,6 +101,7 @@ EXPORTED = (
     "dro_maxpool3x3s2_forward", "dro_maxpool3x3s2_backward",
     "dro_depth_metrics_blocks", "dro_depth_metrics_workspace_bytes", "dro_depth_metrics_prepare",
     "dro_depth_metrics_reduce", "dro_depth_metrics_median_workspace_bytes", "dro_depth_metrics_median",
+    "dro_depth_metrics_demon_prepare", "dro_depth_metrics_demon_reduce",
     "dro_resize_rgb8_to_tensor", "dro_color_jitter_rgb8", "dro_resize_rgb8", "dro_rgb8_to_tensor",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",

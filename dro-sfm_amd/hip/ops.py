@@ -524,6 +524,49 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="", use_gt_scale=True):
     return out
 
 
+def depth_metrics_demon(gt, gt_pose, pred, min_depth, max_depth, use_gt_scale=True):
+    """compute_depth_metrics_demon (dro_sfm/utils/depth.py:343-398) on the GPU.
+
+    gt [B,1,H,W], pred [B,1,h,w] depths; gt_pose [B,N,3|4,4] ground-truth
+    transforms (image b's FIRST reference normalises its ground truth when
+    use_gt_scale).  Returns float32 [9] like depth_metrics.  Same three passes
+    (prepare, on-device median, reduce), no crop, no clamp of the scaled
+    prediction to the depth range."""
+    lib = _lib.load()
+    require_device(gt, pred, gt_pose, what="depth_metrics_demon")
+    if gt.dim() != 4 or pred.dim() != 4 or gt.shape[1] != 1 or pred.shape[1] != 1 or gt.shape[0] != pred.shape[0]:
+        raise RuntimeError("depth_metrics_demon: gt [B,1,H,W] and pred [B,1,h,w] expected")
+    B, _, H, W = gt.shape
+    if gt_pose.dim() != 4 or gt_pose.shape[0] != B or gt_pose.shape[-1] != 4 or gt_pose.shape[-2] not in (3, 4):
+        raise RuntimeError("depth_metrics_demon: gt_pose [B,N,3|4,4] expected")
+    h, w = pred.shape[-2:]
+    gt, pred = gt.contiguous(), pred.contiguous()
+    first = gt_pose[:, 0].float().contiguous()                 # [B,3|4,4]
+    pose_stride = first.shape[1] * 4
+    nblk = lib.dro_depth_metrics_blocks(H, W)
+    pred_up = torch.empty(B, H * W, device=gt.device, dtype=torch.float32)
+    ratio = torch.empty_like(pred_up)
+    counts = torch.empty(B, nblk, device=gt.device, dtype=torch.int32)
+    st = stream_of(gt)
+    pose_p = ptr(first) if use_gt_scale else None
+    check(lib.dro_depth_metrics_demon_prepare(ptr(gt), ptr(pred), pose_p, pose_stride, B, H, W, h, w,
+                                              float(min_depth), float(max_depth), ptr(pred_up), ptr(ratio),
+                                              ptr(counts), st), "dro_depth_metrics_demon_prepare")
+    scale = None
+    if use_gt_scale:
+        scale = torch.empty(B, device=gt.device, dtype=torch.float32)
+        mws = torch.empty(lib.dro_depth_metrics_median_workspace_bytes(B) // 4 + 1, device=gt.device,
+                          dtype=torch.int32)
+        check(lib.dro_depth_metrics_median(ptr(ratio), ptr(counts), B, H, W, ptr(scale), ptr(mws), st),
+              "dro_depth_metrics_median")
+    ws = torch.empty(lib.dro_depth_metrics_workspace_bytes(B) // 8 + 1, device=gt.device, dtype=torch.float64)
+    out = torch.empty(9, device=gt.device, dtype=torch.float32)
+    check(lib.dro_depth_metrics_demon_reduce(ptr(gt), ptr(pred_up), ptr(scale), pose_p, pose_stride, B, H, W,
+                                             float(min_depth), float(max_depth), ptr(out), ptr(ws), st),
+          "dro_depth_metrics_demon_reduce")
+    return out
+
+
 class _BatchNormAct(torch.autograd.Function):
     """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
 

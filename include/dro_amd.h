@@ -215,6 +215,22 @@ int dro_depth_metrics_reduce(const float* gt, const float* pred_up, const float*
                              int W, float min_depth, float max_depth, int crop_y1, int crop_y2,
                              int crop_x1, int crop_x2, float* metrics, void* workspace, void* stream);
 
+/* compute_depth_metrics_demon (dro_sfm/utils/depth.py:343-398, ScanNet/DeMoN
+ * evaluation): prepare -> dro_depth_metrics_median -> reduce as above, no crop,
+ * no clamp of the (scaled) prediction to [min_depth, max_depth].  gt_pose:
+ * per image the first reference's ground-truth transform (row-major 4x4 or
+ * 3x4 floats at gt_pose + b * pose_stride); the ground truth is divided by the
+ * norm of its translation.  gt_pose NULL = use_gt_scale False (then scale is
+ * NULL too). */
+int dro_depth_metrics_demon_prepare(const float* gt, const float* pred, const float* gt_pose,
+                                    long long pose_stride, int B, int H, int W, int h, int w,
+                                    float min_depth, float max_depth, float* pred_up, float* ratio,
+                                    int* block_counts, void* stream);
+int dro_depth_metrics_demon_reduce(const float* gt, const float* pred_up, const float* scale,
+                                   const float* gt_pose, long long pose_stride, int B, int H, int W,
+                                   float min_depth, float max_depth, float* metrics, void* workspace,
+                                   void* stream);
+
 /* Resize + ToTensor of decoded uint8 RGB frames, bit-identical to Pillow's
  * BILINEAR resampling (torchvision Resize on PIL images, datasets/
  * augmentations.py:69-111, then ToTensor :149-160 of the reference).

@@ -511,6 +511,58 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="", use_gt_scale=True):
     return torch.tensor([float(a) / B for a in acc], dtype=gt.dtype)
 
 
+def depth_metrics_demon(gt, gt_pose, pred, min_depth, max_depth, use_gt_scale=True):
+    """compute_depth_metrics_demon (utils/depth.py:343-398): valid pixels
+    min < gt < max (no crop); with scaling the ground truth is divided by the
+    norm of the first reference's gt translation (gt_pose [B,N,4,4]) and the
+    prediction multiplied by the median ratio -- no clamp to the depth range
+    afterwards (unlike compute_depth_metrics)."""
+    B, _, H, W = gt.shape
+    if pred.shape[-2:] != gt.shape[-2:]:
+        pred = F.interpolate(pred, size=(H, W), mode="bilinear", align_corners=True)
+    pred = pred.clamp(min=1e-6)
+    acc = [0.0] * 9
+    for pred_i, gt_i, pose_i in zip(pred, gt, gt_pose):
+        gt_i, pred_i = gt_i.squeeze(), pred_i.squeeze()
+        valid = (gt_i > min_depth) & (gt_i < max_depth)
+        if valid.sum() == 0:
+            continue
+        gt_i, pred_i = gt_i[valid], pred_i[valid]
+        if use_gt_scale:
+            t = pose_i[:, :3, 3]
+            gt_i = gt_i / torch.sqrt(t[0].dot(t[0]))
+            pred_i = pred_i * torch.median(gt_i / pred_i)
+        thresh = torch.max(gt_i / pred_i, pred_i / gt_i)
+        diff = gt_i - pred_i
+        d = gt_i.log() - pred_i.log()
+        vals = [torch.mean(diff.abs() / gt_i), torch.mean(diff ** 2 / gt_i), torch.sqrt(torch.mean(diff ** 2)),
+                torch.sqrt(torch.mean((gt_i.log() - pred_i.log()) ** 2)),
+                (thresh < 1.25).to(gt.dtype).mean(), (thresh < 1.25 ** 2).to(gt.dtype).mean(),
+                (thresh < 1.25 ** 3).to(gt.dtype).mean(),
+                ((d ** 2).mean() - d.sum() ** 2 / len(d) ** 2) ** 0.5,
+                torch.mean((1.0 / pred_i - 1.0 / gt_i).abs())]
+        acc = [a + v for a, v in zip(acc, vals)]
+    return torch.tensor([float(a) / B for a in acc], dtype=gt.dtype)
+
+
+def pose_metrics(gt, pred):
+    """compute_pose_metrics (utils/depth.py:400-421) of one pair of 4x4
+    transforms, in numpy float32 as the reference computes it: rotation angle
+    of R1^T R2 (deg), angle between the translations (deg), and the
+    translation error after a least-squares scale fit (cm)."""
+    import numpy as np
+    pr, g = pred.squeeze().cpu().numpy(), gt.squeeze().cpu().numpy()
+    R1, t1 = g[:3, :3], g[:3, 3]
+    R2, t2 = pr[:3, :3], pr[:3, 3]
+    cos_r = np.minimum((np.trace(np.dot(R1.T, R2)) - 1.0) / 2.0, 1.0)
+    rdeg = np.arccos(cos_r) * (180 / np.pi)
+    cos_t = np.dot(t1, t2) / (np.sqrt(np.dot(t1, t1)) * np.sqrt(np.dot(t2, t2)))
+    tdeg = np.arccos(cos_t) * (180 / np.pi)
+    a = np.dot(t1, t2) / np.dot(t2, t2)
+    tcm = 100 * np.sqrt(np.sum((t1 - a * t2) ** 2, axis=-1))
+    return torch.tensor([rdeg, tdeg, tcm], dtype=torch.float32)
+
+
 # ============================================================================ data pipeline
 def resize_bilinear_pil(a, H, W):
     """Pillow's Image.resize((W, H), BILINEAR) of a uint8 HWC array, as

@@ -589,6 +589,43 @@ def gen_metrics():
              crop=np.array({"": 0, "garg": 1, "eigen_nyu": 2}[crop], dtype=np.int32))
 
 
+def gen_demon():
+    """compute_depth_metrics_demon (utils/depth.py:343-398: ScanNet/DeMoN
+    evaluation -- ground truth normalised by the first reference's gt
+    translation norm, median scaling, no crop, no clamp to the depth range)
+    and compute_pose_metrics (:400-421: rotation angle, translation angle,
+    scale-fitted translation error of the first reference)."""
+    from types import SimpleNamespace
+    from dro_sfm.geometry.pose import Pose
+    from dro_sfm.utils.depth import compute_depth_metrics_demon, compute_pose_metrics
+    g = torch.Generator().manual_seed(78)
+    B, N, H, W, h, w, lo, hi = 3, 2, 96, 128, 48, 64, 0.2, 10.0
+    gt = torch.zeros(B, 1, H, W)
+    keep = torch.rand(B, 1, H, W, generator=g) < 0.8
+    gt[keep] = (lo + 0.05 + (hi - lo - 0.1) * torch.rand(B, 1, H, W, generator=g))[keep]
+    gt[-1] = 0.0                                                       # empty image
+    base = torch.nn.functional.interpolate(torch.rand(B, 1, 6, 8, generator=g), size=(h, w),
+                                           mode="bilinear", align_corners=False)
+    pred = (0.3 + 4.0 * base) * (1.0 + 0.05 * torch.randn(B, 1, h, w, generator=g))
+    vec = torch.cat([0.3 * torch.randn(B * N, 3, generator=g), 0.05 * torch.randn(B * N, 3, generator=g)], 1)
+    gt_pose = Pose.from_vec(vec, "euler").mat.view(B, N, 4, 4)
+    cfg = SimpleNamespace(min_depth=lo, max_depth=hi)
+    out_s = compute_depth_metrics_demon(cfg, gt, gt_pose, pred, use_gt_scale=True)
+    out_u = compute_depth_metrics_demon(cfg, gt, gt_pose, pred, use_gt_scale=False)
+    pose_gt, pose_pred, pose_out = [], [], []
+    for k in range(6):
+        v1 = torch.cat([0.2 * torch.randn(1, 3, generator=g), 0.05 * torch.randn(1, 3, generator=g)], 1)
+        v2 = v1 + torch.cat([0.02 * torch.randn(1, 3, generator=g), 0.005 * torch.randn(1, 3, generator=g)], 1)
+        T1 = Pose.from_vec(v1, "euler").mat
+        P2 = Pose.from_vec(v2, "euler")
+        pose_out.append(compute_pose_metrics(cfg, [T1], [P2]))
+        pose_gt.append(T1[0])
+        pose_pred.append(P2.mat[0])
+    save("metrics_demon", gt=gt, pred=pred, gt_pose=gt_pose, metrics_scaled=out_s, metrics_unscaled=out_u,
+         min_depth=torch.tensor(lo), max_depth=torch.tensor(hi))
+    save("metrics_pose", gt=torch.stack(pose_gt), pred=torch.stack(pose_pred), metrics=torch.stack(pose_out))
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: golden fixtures can only be regenerated in the build container")
@@ -607,3 +644,5 @@ if __name__ == "__main__":
         gen_metrics()
     if "scannet" in which:
         gen_scannet()
+    if "demon" in which:
+        gen_demon()

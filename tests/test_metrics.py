@@ -79,3 +79,59 @@ def test_depth_metrics_rejects_cpu():
     import dro_sfm_amd.hip as hip
     with pytest.raises(RuntimeError):
         hip.depth_metrics(torch.ones(1, 1, 4, 4), torch.ones(1, 1, 4, 4), 0.1, 80.0)
+
+
+def _angle_tol(deg, rel=1e-4):
+    """|error| allowed on an arccos angle: the reference computes cos in
+    numpy float32 (a few ulp of cos), and d(arccos)/d(cos) = -1/sin."""
+    import math
+    s = max(math.sin(math.radians(abs(deg))), 1e-4)
+    return math.degrees(4e-7 / s) + rel * abs(deg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scaled", [True, False])
+def test_depth_metrics_demon_golden(scaled):
+    """compute_depth_metrics_demon (utils/depth.py:343-398; configs[4]'s ScanNet
+    evaluation) against the reference's own outputs: gt normalised by the first
+    reference's gt translation, median scaling, no clamps; 1e-4."""
+    from dro_sfm_amd.utils.depth import compute_depth_metrics_demon
+    d = load_fixture(os.path.join(G, "metrics_demon.npz"))
+    cfg = SimpleNamespace(min_depth=fval(d["min_depth"]), max_depth=fval(d["max_depth"]))
+    out = compute_depth_metrics_demon(cfg, d["gt"].cuda(), d["gt_pose"].cuda(), d["pred"].cuda(),
+                                      use_gt_scale=scaled)
+    want = d["metrics_scaled" if scaled else "metrics_unscaled"]
+    assert out.is_cuda and out.shape == (9,)
+    assert close(out, want), (out.cpu(), want)
+
+
+@pytest.mark.gpu
+def test_depth_metrics_demon_scannet_size_vs_oracle():
+    """ScanNet evaluation size (480x640 dense gt, 240x320 prediction, B=4, N=2
+    gt poses) against the oracle restatement; 1e-4."""
+    import dro_sfm_amd.hip as hip
+    B, H, W, h, w = 4, 480, 640, 240, 320
+    gt, g = sparse_gt(B, H, W, 0.2, 10.0, 0.9, 12)
+    pred = torch.nn.functional.interpolate(gt.clamp(min=0.7), size=(h, w), mode="area")
+    pred = pred * (1.0 + 0.2 * torch.randn(B, 1, h, w, generator=g)).abs() + 0.05
+    vec = torch.cat([0.3 * torch.randn(B * 2, 3, generator=g), 0.05 * torch.randn(B * 2, 3, generator=g)], 1)
+    pose = O.vec_to_transform(vec).view(B, 2, 4, 4)
+    for scaled in (True, False):
+        want = O.depth_metrics_demon(gt, pose, pred, 0.2, 10.0, scaled)
+        out = hip.depth_metrics_demon(gt.cuda(), pose.cuda(), pred.cuda(), 0.2, 10.0, use_gt_scale=scaled)
+        assert close(out, want), (scaled, out.cpu(), want)
+
+
+def test_pose_metrics_golden():
+    """compute_pose_metrics (utils/depth.py:400-421) against the reference's
+    outputs on six near pose pairs (CPU tensors here; the function runs on the
+    pair's device): angles within the float32 conditioning of arccos, the
+    translation error at 1e-4."""
+    from dro_sfm_amd.utils.depth import compute_pose_metrics
+    d = load_fixture(os.path.join(G, "metrics_pose.npz"))
+    for k in range(d["gt"].shape[0]):
+        out = compute_pose_metrics(None, [d["gt"][k:k + 1]], [d["pred"][k:k + 1]])
+        want = d["metrics"][k]
+        assert abs(float(out[0] - want[0])) <= _angle_tol(float(want[0])), (k, out, want)
+        assert abs(float(out[1] - want[1])) <= _angle_tol(float(want[1])), (k, out, want)
+        assert abs(float(out[2] - want[2])) <= 1e-4 * abs(float(want[2])) + 1e-5, (k, out, want)

@@ -315,3 +315,23 @@ def test_train_step_selfsup_view5_n4():
     _, g64 = _train_step_oracle("depthposenet_it12h", "it12-h-out", mind, maxd, batch, "selfsup", torch.float64)
     bad, worst = _grad_pin(f, g32, g64)
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("scaled", [True, False])
+def test_depth_metrics_demon(scaled):
+    """compute_depth_metrics_demon (utils/depth.py:343-398): the restatement
+    reproduces the reference's metrics bit for bit (dense ScanNet-like gt, a
+    lower-resolution prediction, the gt translation normalisation, an image
+    without valid pixels)."""
+    d = load_fixture(os.path.join(G, "metrics_demon.npz"))
+    out = O.depth_metrics_demon(d["gt"], d["gt_pose"], d["pred"], fval(d["min_depth"]), fval(d["max_depth"]),
+                                scaled)
+    assert torch.equal(out, d["metrics_scaled" if scaled else "metrics_unscaled"])
+
+
+def test_pose_metrics():
+    """compute_pose_metrics (utils/depth.py:400-421) on six near pose pairs:
+    bit for bit."""
+    d = load_fixture(os.path.join(G, "metrics_pose.npz"))
+    for k in range(d["gt"].shape[0]):
+        assert torch.equal(O.pose_metrics(d["gt"][k], d["pred"][k]), d["metrics"][k]), k
