@@ -105,6 +105,21 @@ def make_batch(B, seed, device):
     return batch
 
 
+def raw_host_batch(batch, raw=(375, 1242)):
+    """The synthetic batch as the data loader would hand it over before the
+    GPU pipeline (datasets/gpu_loader.collate_decoded): decoded uint8 HWC
+    frames at the KITTI raw size in pinned host memory, raw intrinsics."""
+    def to_raw(t):
+        up = torch.nn.functional.interpolate(t, size=raw, mode="bilinear", align_corners=False)
+        u8 = (up.clamp(0, 1) * 255).round().to(torch.uint8).permute(0, 2, 3, 1).contiguous().cpu()
+        return [f.pin_memory() for f in u8]
+    K = batch["_K0"].detach().cpu().clone()
+    K[:, 0] *= raw[1] / W
+    K[:, 1] *= raw[0] / H
+    return {"rgb": to_raw(batch["rgb"]), "rgb_context": [to_raw(c) for c in batch["rgb_context"]],
+            "intrinsics": K}
+
+
 def build_model(device, flip_prob):
     from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
     if WL["kind"] == "sup":
@@ -400,6 +415,8 @@ def main():
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",
                     help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
+    ap.add_argument("--pose-encoder-main", action="store_true",
+                    help="A/B: cnet_pose on the main stream (default: on the pose block's stream)")
     ap.add_argument("--serial-blocks", action="store_true",
                     help="A/B: pose update block after the depth block on one stream (default: the "
                          "pose block on a side stream beside the depth block)")
@@ -407,6 +424,11 @@ def main():
                     help="autograd's per-use gradient sums instead of in-place gradient sinks (A/B)")
     ap.add_argument("--aten-maxpool", action="store_true",
                     help="A/B: the ResNet stem max pooling through ATen instead of hip.maxpool3x3s2")
+    ap.add_argument("--pipeline", choices=("resident", "gpu"), default="resident",
+                    help="resident: float batches already in HBM (the metric's contract); gpu: every step "
+                         "starts from decoded uint8 KITTI raw frames (375x1242) in pinned host memory and "
+                         "runs the data pipeline (H2D, resize, colour jitter, to_tensor) on the GPU "
+                         "(datasets/gpu_loader.py) inside the timed region")
     ap.add_argument("--miopen-encoder-convs", action="store_true",
                     help="A/B: the encoders' stride-1 3x3 convolutions on MIOpen instead of the HIP engine")
     ap.add_argument("--no-fused-bn", action="store_true",
@@ -439,6 +461,7 @@ def main():
     from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
     _dpn.set_concurrent_encoders(args.concurrent_encoders)
     _dpn.set_concurrent_blocks(not args.serial_blocks)
+    _dpn.set_pose_encoder_stream(not args.pose_encoder_main)
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     _extractor.set_native_maxpool(not args.aten_maxpool)
@@ -465,11 +488,21 @@ def main():
             print(f"[bench] graph capture failed ({type(exc).__name__}: {exc}); running eager",
                   file=sys.stderr, flush=True)
 
+    pipe, host_batches = None, None
+    if args.pipeline == "gpu":
+        from dro_sfm_amd.datasets.gpu_loader import GPUTrainPipeline
+        pipe = GPUTrainPipeline((H, W), (0.2, 0.2, 0.2, 0.05), device=device,
+                                generator=torch.Generator().manual_seed(7 + rank))
+        host_batches = [raw_host_batch(b) for b in batches]
+
     def run(step_i):
         b = batches[step_i % len(batches)]
+        if pipe is not None:
+            b = pipe(host_batches[step_i % len(host_batches)])
         if stepper is not None:
             return stepper.step(b)
-        b["intrinsics"].copy_(b["_K0"])      # the data loader hands a fresh K every step
+        if "_K0" in b:                       # the data loader hands a fresh K every step
+            b["intrinsics"].copy_(b["_K0"])
         return trainer.step(b)
 
     for i in range(args.warmup):
@@ -495,7 +528,9 @@ def main():
         "metric": WL["metric"], "value": round(images / elapsed, 3), "unit": "images/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic" if args.pipeline == "resident" else
+                "synthetic decoded uint8 375x1242 frames, GPU data pipeline in the timed region",
         "config": {"workload": WL["name"], "model": f"DepthPoseNet {VERSION}",
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch, "ref_frames": NREF,
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
@@ -503,6 +538,7 @@ def main():
                    "update_convs": args.conv_backend,
                    "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
                    "update_blocks": "serial" if args.serial_blocks else "concurrent streams",
+                   "pose_encoder": "main stream" if (args.pose_encoder_main or args.serial_blocks) else "pose-block stream",
                    "grad_sinks": not args.no_grad_sinks,
                    "split_engine": args.split_engine,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",

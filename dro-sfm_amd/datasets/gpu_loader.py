@@ -1,0 +1,126 @@
+"""The GPU data path hooked to the reference's datasets.
+
+The reference's datasets decode frames on CPU workers and then apply
+`data_transform` = train_transforms (resize, duplicate, colour jitter,
+to_tensor; dro_sfm/datasets/transforms.py:8-31) there too
+(KITTIDataset.__getitem__, kitti_dataset.py:348-404, `self.data_transform(sample)`
+at :399).  Here the same dataset classes are built with `data_transform=None`
+(their __getitem__ then returns the decoded PIL frames, the intrinsics and
+the context poses untouched), and:
+
+  * `collate_decoded` (DataLoader collate_fn, CPU worker) stacks the decoded
+    uint8 HWC frames into pinned host tensors -- one quarter of the bytes the
+    float tensors of the reference's path would move;
+  * `GPUTrainPipeline` (training process) copies them to the GPU
+    (non_blocking) and runs train_transforms there
+    (datasets/gpu_transforms.py: Pillow-exact resize, torchvision-exact
+    ColorJitter in the reference's draw order, ToTensor), intrinsics scaled per
+    sample by its own raw size.  KITTI drives differ in raw size (375x1242,
+    370x1226, 374x1238, ...): samples of one size are resized in one launch,
+    per size group, and the batch is reassembled in sample order.
+
+Decoding stays on the host (PNG/JPEG entropy decoding is serial per image;
+there is no ROCm image decoder in this image).
+"""
+import numpy as np
+import torch
+
+from .gpu_transforms import train_transforms
+
+
+def _as_uint8(img):
+    a = np.asarray(img)
+    if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
+        a = np.asarray(img.convert("RGB") if hasattr(img, "convert") else a, dtype=np.uint8)
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def collate_decoded(samples):
+    """Collate reference samples built WITHOUT data_transform: 'rgb' and
+    'rgb_context' (PIL images or uint8 HWC arrays) become lists of uint8
+    [H0, W0, 3] tensors (pinned when a GPU is present; per sample, raw sizes
+    may differ); 'intrinsics' float32 [B, 3, 3]; 'pose_context' a list over
+    references of float32 [B, 4, 4]; 'depth' float32 [B, 1, H, W] when
+    present; other keys as lists."""
+    pin = torch.cuda.is_available()
+    out = {}
+    rgb = [_as_uint8(s["rgb"]) for s in samples]
+    out["rgb"] = [t.pin_memory() if pin else t for t in rgb]
+    if "rgb_context" in samples[0]:
+        n = len(samples[0]["rgb_context"])
+        out["rgb_context"] = [[(lambda t: t.pin_memory() if pin else t)(_as_uint8(s["rgb_context"][j]))
+                               for s in samples] for j in range(n)]
+    if "intrinsics" in samples[0]:
+        out["intrinsics"] = torch.stack([torch.as_tensor(np.asarray(s["intrinsics"]), dtype=torch.float32)
+                                         for s in samples])
+    if "pose_context" in samples[0]:
+        n = len(samples[0]["pose_context"])
+        out["pose_context"] = [torch.stack([torch.as_tensor(np.asarray(s["pose_context"][j]), dtype=torch.float32)
+                                            for s in samples]) for j in range(n)]
+    if "depth" in samples[0]:
+        out["depth"] = torch.stack([torch.as_tensor(np.asarray(s["depth"]), dtype=torch.float32).reshape(
+            1, *np.asarray(s["depth"]).shape[-2:]) for s in samples])
+    for k in samples[0]:
+        if k not in out:
+            out[k] = [s[k] for s in samples]
+    return out
+
+
+class GPUTrainPipeline:
+    """Host batch from `collate_decoded` -> the model's training batch on the
+    GPU: train_transforms(image_shape, jittering) exactly as the reference's
+    data_transform would have produced it on the CPU workers (same random
+    draws from `generator`, in the reference's per-sample order)."""
+
+    def __init__(self, image_shape, jittering=(0.2, 0.2, 0.2, 0.05), device=None, generator=None):
+        self.image_shape = tuple(int(v) for v in image_shape)
+        self.jittering = tuple(jittering)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.generator = generator
+
+    def __call__(self, host):
+        dev = self.device
+        B = len(host["rgb"])
+        N = len(host.get("rgb_context", []))
+        frames = [[t.to(dev, non_blocking=True) for t in host["rgb"]]]
+        frames += [[t.to(dev, non_blocking=True) for t in host["rgb_context"][j]] for j in range(N)]
+        K = host["intrinsics"].to(dev, non_blocking=True) if "intrinsics" in host else None
+        sizes = [tuple(f.shape[:2]) for f in frames[0]]
+        # jitter draws must follow sample order: group only consecutive equal sizes
+        groups, start = [], 0
+        for b in range(1, B + 1):
+            if b == B or sizes[b] != sizes[start]:
+                groups.append((start, b))
+                start = b
+        parts = []
+        for lo, hi in groups:
+            sub = {"rgb": torch.stack(frames[0][lo:hi]),
+                   "rgb_context": [torch.stack(frames[1 + j][lo:hi]) for j in range(N)]}
+            if K is not None:
+                sub["intrinsics"] = K[lo:hi]
+            parts.append(train_transforms(sub, self.image_shape, self.jittering, self.generator))
+        cat = lambda key: torch.cat([p[key] for p in parts]) if len(parts) > 1 else parts[0][key]
+        out = {k: v for k, v in host.items() if k not in ("rgb", "rgb_context", "intrinsics")}
+        out["rgb"], out["rgb_original"] = cat("rgb"), cat("rgb_original")
+        out["rgb_context"] = [torch.cat([p["rgb_context"][j] for p in parts]) for j in range(N)]
+        out["rgb_context_original"] = [torch.cat([p["rgb_context_original"][j] for p in parts])
+                                       for j in range(N)]
+        if K is not None:
+            out["intrinsics"] = cat("intrinsics")
+        if "pose_context" in host:
+            out["pose_context"] = [p.to(dev, non_blocking=True) for p in host["pose_context"]]
+        if "depth" in host:
+            out["depth"] = host["depth"].to(dev, non_blocking=True)
+        return out
+
+
+def gpu_data_loader(dataset, batch_size, image_shape, jittering=(0.2, 0.2, 0.2, 0.05), num_workers=4,
+                    shuffle=True, generator=None, device=None, **loader_kw):
+    """Iterate a reference dataset built with data_transform=None through the
+    GPU pipeline: a DataLoader over collate_decoded (workers decode and stack
+    uint8 frames) whose batches GPUTrainPipeline transforms on the GPU."""
+    loader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
+                                         collate_fn=collate_decoded, **loader_kw)
+    pipe = GPUTrainPipeline(image_shape, jittering, device=device, generator=generator)
+    for host in loader:
+        yield pipe(host)

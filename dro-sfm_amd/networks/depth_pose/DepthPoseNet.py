@@ -74,6 +74,16 @@ def set_concurrent_blocks(enabled):
     _CONCURRENT_BLOCKS[0] = bool(enabled)
 
 
+_POSE_ENCODER_SIDE = [True]
+
+
+def set_pose_encoder_stream(enabled):
+    """With the concurrent update blocks: run the pose context encoder
+    (cnet_pose, read only by the pose block) on the pose block's stream too
+    (default True), beside fnet and cnet_depth; its backward follows."""
+    _POSE_ENCODER_SIDE[0] = bool(enabled)
+
+
 def _side_streams(device):
     ss = _SIDE_STREAMS.get(device)
     if ss is None:
@@ -149,6 +159,15 @@ class DepthPoseNet(nn.Module):
 
         # context encoders first, on side streams (they depend on the images only)
         side = None
+        pside = None
+        if self.iters > 0 and _CONCURRENT_BLOCKS[0] and target_image.is_cuda:
+            pside = _side_streams(target_image.device)[1]
+        pose_enc_side = pside is not None and _POSE_ENCODER_SIDE[0] and not _CONCURRENT[0]
+        if pose_enc_side:
+            # cnet_pose feeds only the pose block: it runs on that block's stream
+            pside.wait_stream(torch.cuda.current_stream(target_image.device))
+            for t in [target_image, *ref_imgs]:
+                t.record_stream(pside)
         if self.iters > 0:
             if _CONCURRENT[0] and target_image.is_cuda:
                 main = torch.cuda.current_stream(target_image.device)
@@ -162,7 +181,7 @@ class DepthPoseNet(nn.Module):
                 ctx_d = self.cnet_depth(target_image)
                 h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
-            with torch.cuda.stream(side[1]) if side else _null():
+            with torch.cuda.stream(side[1]) if side else (torch.cuda.stream(pside) if pose_enc_side else _null()):
                 pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
                                    torch.stack(list(ref_imgs))], 2).flatten(0, 1)
                 ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
@@ -193,9 +212,6 @@ class DepthPoseNet(nn.Module):
             for t in (h_d, x_d, h_p, x_p):
                 t.record_stream(main)
 
-        pside = None
-        if self.iters > 0 and _CONCURRENT_BLOCKS[0] and target_image.is_cuda:
-            pside = _side_streams(target_image.device)[1]
         fmap1_p, frefs_p = fmap1, frefs
         if self.iters > 0:
             # the context features feed every GRU step: gradients summed in place
