@@ -158,30 +158,32 @@ class DepthPoseNet(nn.Module):
         K = intrinsics.float().contiguous()
 
         # context encoders first, on side streams (they depend on the images only)
-        side = None
+        cuda = target_image.is_cuda
         pside = None
-        if self.iters > 0 and _CONCURRENT_BLOCKS[0] and target_image.is_cuda:
+        if self.iters > 0 and _CONCURRENT_BLOCKS[0] and cuda:
             pside = _side_streams(target_image.device)[1]
-        pose_enc_side = pside is not None and _POSE_ENCODER_SIDE[0] and not _CONCURRENT[0]
-        if pose_enc_side:
-            # cnet_pose feeds only the pose block: it runs on that block's stream
-            pside.wait_stream(torch.cuda.current_stream(target_image.device))
-            for t in [target_image, *ref_imgs]:
-                t.record_stream(pside)
-        if self.iters > 0:
-            if _CONCURRENT[0] and target_image.is_cuda:
-                main = torch.cuda.current_stream(target_image.device)
-                side = _side_streams(target_image.device)
-                for st in side:
-                    st.wait_stream(main)
+        # cnet_depth: beside fnet when set_concurrent_encoders (joined before the
+        # depth block); cnet_pose: on the pose block's stream (no join needed),
+        # or beside fnet without concurrent blocks
+        d_stream = p_stream = None
+        if self.iters > 0 and cuda:
+            if _CONCURRENT[0]:
+                d_stream = _side_streams(target_image.device)[0]
+            if pside is not None and _POSE_ENCODER_SIDE[0]:
+                p_stream = pside
+            elif _CONCURRENT[0]:
+                p_stream = _side_streams(target_image.device)[1]
+            main = torch.cuda.current_stream(target_image.device)
+            for st in {d_stream, p_stream} - {None}:
+                st.wait_stream(main)
                 for t in [target_image, *ref_imgs]:
-                    for st in side:
-                        t.record_stream(st)
-            with torch.cuda.stream(side[0]) if side else _null():
+                    t.record_stream(st)
+        if self.iters > 0:
+            with torch.cuda.stream(d_stream) if d_stream is not None else _null():
                 ctx_d = self.cnet_depth(target_image)
                 h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
-            with torch.cuda.stream(side[1]) if side else (torch.cuda.stream(pside) if pose_enc_side else _null()):
+            with torch.cuda.stream(p_stream) if p_stream is not None else _null():
                 pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
                                    torch.stack(list(ref_imgs))], 2).flatten(0, 1)
                 ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
@@ -205,11 +207,16 @@ class DepthPoseNet(nn.Module):
         inv_preds = [self.upsample_scaled(disp, self.upmask_net(fmap1), self.feat_ratio)]
         pose_preds = [poses]
 
-        if side:                                          # join: the update blocks read h/x
-            main = torch.cuda.current_stream(target_image.device)
-            for st in side:
-                main.wait_stream(st)
-            for t in (h_d, x_d, h_p, x_p):
+        # join: the depth block (main stream) reads h_d/x_d; h_p/x_p only when the
+        # pose block runs on the main stream too
+        main = torch.cuda.current_stream(target_image.device) if cuda else None
+        if d_stream is not None:
+            main.wait_stream(d_stream)
+            for t in (h_d, x_d):
+                t.record_stream(main)
+        if p_stream is not None and p_stream is not pside:
+            main.wait_stream(p_stream)
+            for t in (h_p, x_p):
                 t.record_stream(main)
 
         fmap1_p, frefs_p = fmap1, frefs
