@@ -429,6 +429,8 @@ def main():
                          "starts from decoded uint8 KITTI raw frames (375x1242) in pinned host memory and "
                          "runs the data pipeline (H2D, resize, colour jitter, to_tensor) on the GPU "
                          "(datasets/gpu_loader.py) inside the timed region")
+    ap.add_argument("--native-strided-convs", action="store_true",
+                    help="A/B: the encoders' stride-2 convs on the HIP engine instead of MIOpen")
     ap.add_argument("--miopen-encoder-convs", action="store_true",
                     help="A/B: the encoders' stride-1 3x3 convolutions on MIOpen instead of the HIP engine")
     ap.add_argument("--no-fused-bn", action="store_true",
@@ -466,6 +468,7 @@ def main():
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     _extractor.set_native_maxpool(not args.aten_maxpool)
     _extractor.set_native_convs(not args.miopen_encoder_convs)
+    _extractor.set_native_strided_convs(args.native_strided_convs)
     from dro_sfm_amd.hip import ops as _hops
     _hops.set_grad_sinks(not args.no_grad_sinks)
 
@@ -543,6 +546,7 @@ def main():
                    "split_engine": args.split_engine,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",
                    "encoder_3x3_s1": "miopen" if args.miopen_encoder_convs else "hip",
+                   "encoder_strided": "hip" if args.native_strided_convs else "miopen",
                    "stem_pool": "aten" if args.aten_maxpool else "hip",
                    "weight_grads": "autograd" if args.no_direct_wgrad else
                    ("in place, side stream" if args.wgrad_side_stream else "in place")},

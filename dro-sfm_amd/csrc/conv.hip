@@ -64,6 +64,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   __shared__ float Xs[2][kBK][kBN];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
+  const int Hsrc = a.Hs, Wsrc = a.Ws, sh = a.sshift;   // staged operand size, log2 stride
+  const unsigned HWs = (unsigned)Hsrc * (unsigned)Wsrc;
   const int Cin = a.g.Cin, Cout = a.g.Cout, rows = a.rows, kch = a.kch, K = a.K;
   const FastDiv kdiv = a.kdiv, kwdiv = a.kwdiv;
   const float* __restrict__ Wt = a.weight;
@@ -74,7 +76,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   const int row0 = rt * BM;
   const long long p0 = (long long)pt * kBN;
   const size_t HW = (size_t)H * W;
-  const unsigned HWu = (unsigned)HW;
   const long long P = (long long)a.g.B * HW;
   const int T = a.g.KH * KW;
   const int nchunks = (K + kBK - 1) / kBK;
@@ -103,17 +104,20 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
       const int kk = kv ? k : 0;
       const int tap = fdiv(kk, kdiv), ch = kk - tap * kch;
       const int ty = fdiv(tap, kwdiv), dy = ty - PH, dx = tap - ty * KW - PW;
-      // per lane
-      const int yy = MODE == 0 ? py + dy : py - dy, xx = MODE == 0 ? px + dx : px - dx;
-      const bool ok = kv && pv && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-      const unsigned pix = (unsigned)(yy * W + xx);
+      // per lane.  Stride 2^sh: the forward reads input (S*y + dy, S*x + dx);
+      // the data gradient of input pixel y takes G at (y - dy) / S where exact
+      const int ny = MODE == 0 ? (py << sh) + dy : py - dy, nx = MODE == 0 ? (px << sh) + dx : px - dx;
+      const bool onp = MODE == 0 || ((ny | nx) & ((1 << sh) - 1)) == 0;
+      const int yy = MODE == 0 ? ny : (ny >> sh), xx = MODE == 0 ? nx : (nx >> sh);
+      const bool ok = kv && pv && onp && (unsigned)yy < (unsigned)Hsrc && (unsigned)xx < (unsigned)Wsrc;
+      const unsigned pix = (unsigned)(yy * Wsrc + xx);
       xmask |= ok ? (1u << i) : 0u;
       if (MODE == 0) {
-        const RowDesc d = row_desc(cb1, cb2, cb3, ch, HWu);
+        const RowDesc d = row_desc(cb1, cb2, cb3, ch, HWs);
         const unsigned e = (unsigned)pb * d.A + d.Bc + (d.M ? pix : 0u);
         xr[i] = d.p[ok ? e : 0u];
       } else {
-        const unsigned e = ((unsigned)pb * (unsigned)Cout + (unsigned)ch) * HWu + pix;
+        const unsigned e = ((unsigned)pb * (unsigned)Cout + (unsigned)ch) * HWs + pix;
         xr[i] = Gp[ok ? e : 0u];
       }
     }
@@ -590,6 +594,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
   __shared__ float Xs[2][kWP][64 + 1];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
+  const int Hsrc = a.Hs, Wsrc = a.Ws, sh = a.sshift;   // input size, log2 stride
+  const unsigned HWs = (unsigned)Hsrc * (unsigned)Wsrc;
   const int Cin = a.g.Cin, Cout = a.g.Cout;
   const float* __restrict__ Gp = a.G;
   const FastDiv cindiv = a.cindiv, kwdiv = a.kwdiv;
@@ -626,12 +632,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
       const bool nv = n < NK;
       const int tap = nv ? fdiv(n, cindiv) : 0, ch = nv ? n - tap * Cin : 0;
       const int ty = fdiv(tap, kwdiv), dy = ty - PH, dx = tap - ty * KW - PW;
-      const int yy = py + dy, xx = px + dx;
-      const bool ok = v && nv && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-      const unsigned spix = (unsigned)(yy * W + xx);
+      const int yy = (py << sh) + dy, xx = (px << sh) + dx;
+      const bool ok = v && nv && (unsigned)yy < (unsigned)Hsrc && (unsigned)xx < (unsigned)Wsrc;
+      const unsigned spix = (unsigned)(yy * Wsrc + xx);
       xmask |= ok ? (1u << j) : 0u;
       omask |= (v && n == NK) ? (1u << j) : 0u;
-      const RowDesc d = row_desc(cb1, cb2, cb3, ch, HWu);
+      const RowDesc d = row_desc(cb1, cb2, cb3, ch, HWs);
       const unsigned e = (unsigned)b * d.A + d.Bc + (d.M ? spix : 0u);
       xr[j] = d.p[ok ? e : 0u];
     }
@@ -1579,6 +1585,9 @@ int conv_setup_geom(IgArgs& a, const dro_slice* srcs, int nsrc, int B, int H, in
   }
   a.kwdiv = make_fdiv(KW);
   a.cindiv = make_fdiv(cin);
+  a.Hs = H;
+  a.Ws = W;
+  a.sshift = 0;
   return DRO_OK;
 }
 
@@ -1816,7 +1825,8 @@ unsigned long long* g_conv_stamps = nullptr;   // dro_debug_conv_stamps
 // rows / kch set by the caller; `ws` must hold plan.part_bytes
 template <int MODE, int ACT, int EPI>
 int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
-  const IgPlan pl = plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
+  const IgPlan pl = a.flat_only ? plan_igemm_flat(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W)
+                                 : plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
   a.stamps = g_conv_stamps;
   a.dbg = 0;
   if (g_conv_stamps) {
@@ -1825,12 +1835,12 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   }
   a.K = a.kch * a.g.KH * a.g.KW;
   static const bool thin_off = getenv("DRO_CONV_NO_THIN") != nullptr;   // A/B switch
-  if (!thin_off && thin_ok<MODE, EPI>(a)) {
+  if (!a.flat_only && !thin_off && thin_ok<MODE, EPI>(a)) {
     a.part = reinterpret_cast<float*>(ws);
     return launch_thin<MODE, ACT>(a, pl.ksplit, s);
   }
   // split-bf16 MFMA engine (xconv.hip) when the caller passed split weights
-  if (a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
+  if (!a.flat_only && a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
@@ -2205,6 +2215,168 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     conv_log("wgrad_kernel(", 2.0 * Cout * a.g.Cin * T * (double)P);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits),
                        dim3(256), 0, s, a);
+    if ((st = launch_status("wgrad_kernel launch failed"))) return st;
+    const long long total = (long long)Cout * (a.K + 1);
+    long long blocks = (total + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pl.splits);
+    if ((st = launch_status("wgrad_finish_kernel launch failed"))) return st;
+  }
+  return DRO_OK;
+}
+
+// ------------------------------------------------------------------ strided convolutions
+// The ResNet encoders' stride-2 convolutions (extractor.py:7-107 /
+// torchvision BasicBlock + stem): 7x7/s2 pad 3 stems, 3x3/s2 pad 1 stage
+// entries, 1x1/s2 downsamples; one dense NCHW input, no bias / activation
+// needed there (BN follows) but both are supported in the forward.  They run
+// on the flattened implicit GEMM (igemm_kernel: per-tap gathers, so any
+// kernel size and stride) and the generic weight-gradient kernel
+// (wgrad_kernel), with the staged operand's own size and the stride:
+//   forward      out[o, y, x] = sum W[o, c, t] * X[c, S*y + ty - P, S*x + tx - P]
+//   data grad    dX[c, y, x]  = sum W[o, c, t] * G[o, (y + P - ty) / S, (x + P - tx) / S]  (exact only)
+//   weight grad  dW[o, c, t]  = sum G[o, y, x] * X[c, S*y + ty - P, S*x + tx - P]
+namespace {
+int strided_setup(IgArgs& a, const float* x, int B, int Hi, int Wi, int Cin, int Cout, int KH, int KW,
+                  int stride, int pad, int& Ho, int& Wo) {
+  if (!x) {
+    set_error("conv2d_strided: NULL input");
+    return DRO_E_NULL;
+  }
+  if (B < 1 || Hi < 1 || Wi < 1 || Cin < 1 || Cout < 1 || KH < 1 || KW < 1 || pad < 0 ||
+      (stride != 1 && stride != 2) || Cin >= 4096 || Cout >= 4096 || (long long)Cin * KH * KW >= 65535 ||
+      (long long)Cout * KH * KW >= 65535) {
+    set_error("conv2d_strided: sizes out of range (stride 1 or 2, C < 4096, C*KH*KW < 65535)");
+    return DRO_E_SHAPE;
+  }
+  Ho = (Hi + 2 * pad - KH) / stride + 1;
+  Wo = (Wi + 2 * pad - KW) / stride + 1;
+  if (Ho < 1 || Wo < 1 || too_big(B, Cin, (long long)Hi * Wi) || too_big(B, Cout, (long long)Ho * Wo)) {
+    set_error("conv2d_strided: empty output or a tensor of >= 2^30 elements");
+    return DRO_E_SHAPE;
+  }
+  const dro_slice src = {x, Cin, Cin, 0, 0};
+  // geometry of the output (the forward's GEMM columns); 'same' checks skipped
+  ConvGeom& g = a.g;
+  g.B = B;
+  g.H = Ho;
+  g.W = Wo;
+  g.Cin = Cin;
+  g.Cout = Cout;
+  g.KH = KH;
+  g.KW = KW;
+  g.PH = pad;
+  g.PW = pad;
+  for (int i = 0; i < kMaxSrc; ++i) {
+    a.src[i].p = src.data;
+    a.src[i].C = Cin;
+    a.src[i].ctot = Cin;
+    a.src[i].coff = 0;
+    a.src[i].bcast = 0;
+    a.cbase[i] = i == 0 ? 0 : Cin;
+  }
+  a.kwdiv = make_fdiv(KW);
+  a.cindiv = make_fdiv(Cin);
+  a.Hs = Hi;
+  a.Ws = Wi;
+  a.sshift = stride == 2 ? 1 : 0;
+  a.flat_only = 1;
+  return DRO_OK;
+}
+}  // namespace
+
+extern "C" size_t dro_conv2d_strided_workspace_bytes(int B, int Hi, int Wi, int Cin, int Cout, int KH, int KW,
+                                                     int stride, int pad) {
+  if (stride < 1) return 0;
+  const int Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
+  if (Ho < 1 || Wo < 1) return 0;
+  const size_t fwd = plan_igemm_flat(Cout, Cin, KH, KW, B, Ho, Wo).part_bytes;
+  const size_t dg = plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes;
+  const size_t wg = plan_wgrad(Cin, Cout, KH * KW, (long long)B * Ho * Wo).part_bytes;
+  return std::max(fwd, align256(dg) + wg);
+}
+
+extern "C" int dro_conv2d_strided_forward(const float* x, const float* weight, const float* bias, int B, int Hi,
+                                          int Wi, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                                          int act, float* out, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  IgArgs a = {};
+  int Ho, Wo;
+  int st = strided_setup(a, x, B, Hi, Wi, Cin, Cout, KH, KW, stride, pad, Ho, Wo);
+  if (st) return st;
+  if (!weight || !out) {
+    set_error("conv2d_strided_forward: NULL weight/out");
+    return DRO_E_NULL;
+  }
+  if ((st = check_ws(workspace, workspace_bytes,
+                     dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad),
+                     "conv2d_strided_forward")))
+    return st;
+  a.weight = weight;
+  a.bias = bias;
+  a.alpha = 1.f;
+  a.out = out;
+  a.out_ctot = Cout;
+  a.out_coff = 0;
+  a.rows = Cout;
+  a.kch = Cin;
+  const long long P = (long long)B * Ho * Wo;
+  hipStream_t s = (hipStream_t)stream;
+  DRO_ACT_SWITCH(act, st = (launch_igemm<0, A_, 0>(a, P, static_cast<char*>(workspace), s)));
+  return st;
+}
+
+extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, const float* dout, int B, int Hi,
+                                           int Wi, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                                           float* grad_x, int grad_x_accumulate, float* grad_weight,
+                                           float* grad_bias, int grad_weight_accumulate, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  IgArgs a = {};
+  int Ho, Wo;
+  int st = strided_setup(a, x, B, Hi, Wi, Cin, Cout, KH, KW, stride, pad, Ho, Wo);
+  if (st) return st;
+  if (!weight || !dout || (grad_bias && !grad_weight)) {
+    set_error("conv2d_strided_backward: NULL weight/dout, or grad_bias without grad_weight");
+    return DRO_E_NULL;
+  }
+  if ((st = check_ws(workspace, workspace_bytes,
+                     dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad),
+                     "conv2d_strided_backward")))
+    return st;
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = static_cast<char*>(workspace);
+  a.weight = weight;
+  a.G = dout;
+  a.galpha = 1.f;
+  if (grad_x) {
+    // data gradient: GEMM columns = input pixels, staged operand = G (output size)
+    IgArgs d = a;
+    d.g.H = Hi;
+    d.g.W = Wi;
+    d.Hs = Ho;
+    d.Ws = Wo;
+    d.rows = Cin;
+    d.kch = Cout;
+    d.gsrc[0] = grad_x;
+    d.gsrc_ctot[0] = Cin;
+    d.gsrc_coff[0] = 0;
+    d.gsrc_acc[0] = grad_x_accumulate ? 1 : 0;
+    if ((st = launch_igemm<1, 0, 0>(d, (long long)B * Hi * Wi, ws, s))) return st;
+  }
+  if (grad_weight) {
+    const long long P = (long long)B * Ho * Wo;
+    const int T = KH * KW;
+    const WgPlan pl = plan_wgrad(Cin, Cout, T, P);
+    a.gweight = grad_weight;
+    a.gbias = grad_bias;
+    a.wacc = grad_weight_accumulate ? 1 : 0;
+    a.K = Cin * T;
+    a.otiles = pl.otiles;
+    a.pchunk = pl.pchunk;
+    a.part = reinterpret_cast<float*>(ws + align256(plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes));
+    conv_log("wgrad_kernel(", 2.0 * Cout * Cin * T * (double)P);
+    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits), dim3(256), 0,
+                       s, a);
     if ((st = launch_status("wgrad_kernel launch failed"))) return st;
     const long long total = (long long)Cout * (a.K + 1);
     long long blocks = (total + 255) / 256;

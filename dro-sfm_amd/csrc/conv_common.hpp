@@ -96,6 +96,11 @@ struct IgArgs {
   const char* wsplit;           // nullptr: the f32 engine runs
   unsigned long long wplane;    // bytes per plane
   unsigned wrow;                // bytes per row (chunks * T * 64)
+  // strided convolutions (flattened implicit GEMM and generic weight gradient
+  // only): the staged operand's spatial size (input for the forward and the
+  // weight gradient, the output gradient for the data gradient), log2 stride
+  int Hs, Ws, sshift;
+  int flat_only;                // 1: the flattened implicit GEMM (no halo / thin / split-bf16 paths)
   unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
   int dbg;                      // diagnostics with stamps on (env DRO_CONV_DBG): 1 skip the K
                                 // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)

@@ -7,9 +7,9 @@ be captured into a hipGraph.
 from .ops import (DEPTH_DISP, DEPTH_INV, DEPTH_METRIC, POSE_EULER, POSE_MATRIX,
                   batchnorm_act, bilinear_upsample2x, grad_sink, maxpool3x3s2, depth_metrics, depth_metrics_demon, convex_upsample, photometric_loss, plane_sweep_cost,
                   supervised_loss, warp_cost)
-from .conv import cached_cat, conv2d, sepconvgru_half, weight_grad_scope
+from .conv import cached_cat, conv2d, conv2d_strided, sepconvgru_half, weight_grad_scope
 
-__all__ = ["conv2d", "sepconvgru_half", "weight_grad_scope", "cached_cat", "warp_cost", "plane_sweep_cost", "photometric_loss", "supervised_loss",
+__all__ = ["conv2d", "conv2d_strided", "sepconvgru_half", "weight_grad_scope", "cached_cat", "warp_cost", "plane_sweep_cost", "photometric_loss", "supervised_loss",
            "convex_upsample",
            "bilinear_upsample2x", "maxpool3x3s2", "depth_metrics", "depth_metrics_demon", "batchnorm_act", "grad_sink",
            "POSE_EULER", "POSE_MATRIX", "DEPTH_METRIC", "DEPTH_INV", "DEPTH_DISP"]

@@ -61,6 +61,9 @@ def load():
     _sig(lib.dro_depth_metrics_reduce, P, P, P, I, I, I, F, F, I, I, I, I, P, P, S)
     _sig(lib.dro_depth_metrics_median_workspace_bytes, I, restype=Z)
     _sig(lib.dro_depth_metrics_median, P, P, I, I, I, P, P, S)
+    _sig(lib.dro_conv2d_strided_workspace_bytes, I, I, I, I, I, I, I, I, I, restype=Z)
+    _sig(lib.dro_conv2d_strided_forward, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, Z, S)
+    _sig(lib.dro_conv2d_strided_backward, P, P, P, I, I, I, I, I, I, I, I, I, P, I, P, P, I, P, Z, S)
     _sig(lib.dro_depth_metrics_demon_prepare, P, P, P, LL, I, I, I, I, I, F, F, P, P, P, S)
     _sig(lib.dro_depth_metrics_demon_reduce, P, P, P, P, LL, I, I, I, F, F, P, P, S)
     _sig(lib.dro_resize_rgb8_to_tensor, P, I, I, I, I, I, P, P, I, P, P, I, P, P, S)
@@ -102,6 +105,7 @@ EXPORTED = (
     "dro_depth_metrics_blocks", "dro_depth_metrics_workspace_bytes", "dro_depth_metrics_prepare",
     "dro_depth_metrics_reduce", "dro_depth_metrics_median_workspace_bytes", "dro_depth_metrics_median",
     "dro_depth_metrics_demon_prepare", "dro_depth_metrics_demon_reduce",
+    "dro_conv2d_strided_workspace_bytes", "dro_conv2d_strided_forward", "dro_conv2d_strided_backward",
     "dro_resize_rgb8_to_tensor", "dro_color_jitter_rgb8", "dro_resize_rgb8", "dro_rgb8_to_tensor",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",

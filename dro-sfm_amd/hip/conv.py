@@ -497,6 +497,71 @@ def conv2d(srcs, weight, bias=None, act=None, alpha=1.0, parts=None):
     return _Conv2d.apply(weight, bias, ACT[act], float(alpha), current_scope(), None, len(srcs), *srcs)
 
 
+class _Conv2dStrided(torch.autograd.Function):
+    """act(conv2d(x, weight, bias, stride, padding)) on the flattened implicit
+    GEMM (csrc/conv.hip dro_conv2d_strided_*): the encoders' stride-2 (and any
+    non-'same') convolutions.  Backward supports act none only (BatchNorm
+    follows every such conv in the encoders)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, act, direct):
+        lib = _lib.load()
+        require_device(x, weight, bias, what="conv2d_strided")
+        B, Cin, Hi, Wi = x.shape
+        Cout, cin_w, KH, KW = weight.shape
+        if cin_w != Cin:
+            raise RuntimeError("conv2d_strided: input channels do not match the weight")
+        Ho, Wo = (Hi + 2 * pad - KH) // stride + 1, (Wi + 2 * pad - KW) // stride + 1
+        x, weight = x.contiguous(), weight.contiguous()
+        out = torch.empty(B, Cout, Ho, Wo, device=x.device, dtype=torch.float32)
+        nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
+        check(lib.dro_conv2d_strided_forward(ptr(x), ptr(weight), ptr(bias), B, Hi, Wi, Cin, Cout, KH, KW, stride,
+                                             pad, act, ptr(out), ptr(ws), nws, stream_of(out)),
+              "dro_conv2d_strided_forward")
+        ctx.save_for_backward(x, weight)
+        ctx.meta = (stride, pad, act, bias is not None, direct)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        x, weight = ctx.saved_tensors
+        stride, pad, act, has_bias, direct = ctx.meta
+        if act:
+            raise RuntimeError("conv2d_strided: backward through a fused activation is not supported")
+        B, Cin, Hi, Wi = x.shape
+        Cout, _, KH, KW = weight.shape
+        need = ctx.needs_input_grad
+        gout = gout.contiguous()
+        gx = torch.empty_like(x) if need[0] else None
+        if direct is not None:                 # in place into the trainer's flat .grad views
+            gw, gb, wacc = direct[2], direct[3] if has_bias else None, 1
+        else:
+            gw = torch.empty_like(weight) if need[1] else None
+            gb = torch.empty(Cout, device=x.device) if (has_bias and need[2]) else None
+            wacc = 0
+        if gw is None and gb is not None:
+            gw = torch.empty_like(weight)
+        nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
+        check(lib.dro_conv2d_strided_backward(ptr(x), ptr(weight), ptr(gout), B, Hi, Wi, Cin, Cout, KH, KW, stride,
+                                              pad, ptr(gx), 0, ptr(gw), ptr(gb), wacc, ptr(ws), nws,
+                                              stream_of(gout)), "dro_conv2d_strided_backward")
+        if direct is not None:
+            return gx, None, None, None, None, None, None
+        return gx, (gw if need[1] else None), (gb if has_bias and need[2] else None), None, None, None, None
+
+
+def conv2d_strided(x, weight, bias=None, stride=2, padding=1, act=None):
+    """act(F.conv2d(x, weight, bias, stride, padding)) on the HIP conv engine
+    (stride 1 or 2, any kernel size, one dense input).  Weight gradients go in
+    place into the trainer's flat buffer when the parameters are flagged for it
+    (as hip.conv2d does)."""
+    direct = _direct_targets((weight,), (bias,) if bias is not None else ())
+    return _Conv2dStrided.apply(x, weight, bias, int(stride), int(padding), ACT[act], direct)
+
+
 class _SepGRUHalf(torch.autograd.Function):
     """One direction of SepConvGRU (update.py:59-70): z, r = sigmoid(conv([h; x]));
     q = tanh(conv([r*h; x])); h' = (1-z) h + z q.  x given as sources.

@@ -16,9 +16,11 @@ The 2x bilinear upsampling of the fusion head is a HIP kernel
 (hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.  So
 is the stem's 3x3/s2 max pooling (hip.maxpool3x3s2, bit-identical to
 F.max_pool2d forward and backward; ATen's backward took 55 us per call).
-The stride-1 3x3 convolutions (layer1-3 except each stage's first, the fusion
-head, out_conv) run on the HIP conv engine (conv3x3); the 7x7/s2 stem, the
-3x3/s2 stage entries and the 1x1/s2 downsamples stay on MIOpen.
+The stride-1 3x3 convolutions (layer1-3, the fusion head with its concat read
+in place, out_conv) run on the HIP conv engine's halo-tiled kernels
+(conv3x3).  The 7x7/s2 stems, 3x3/s2 stage entries and 1x1/s2 downsamples
+have a native path too (the flattened implicit GEMM with the stride,
+set_native_strided_convs) but stay on MIOpen by default: measured faster.
 """
 import torch
 import torch.nn as nn
@@ -30,23 +32,44 @@ from ... import hip
 _FUSED_BN = [True]
 _NATIVE_POOL = [True]
 _NATIVE_CONV = [True]
+_NATIVE_STRIDED = [False]
+
+
+def set_native_strided_convs(enabled):
+    """The stride-2 stems / stage entries / 1x1 downsamples on the HIP flattened
+    implicit GEMM (True) or MIOpen (False, default).  Measured round 3 (KITTI
+    metric step, one box): all-native 17.7-18.0 ms vs 16.6 ms with these on
+    MIOpen -- the generic kernels spend 4x the FLOPs on the stride-2 data
+    gradient (parity-masked taps) and the per-tap-gather weight gradient is
+    2x MIOpen's; parity is tested either way (tests/test_conv_engine.py)."""
+    _NATIVE_STRIDED[0] = bool(enabled)
 
 
 def set_native_convs(enabled):
-    """Stride-1 3x3 convolutions on the HIP f32-MFMA engine (default True) or
-    on MIOpen (False, A/B runs)."""
+    """Every encoder convolution on the HIP f32-MFMA engine (default True) or
+    on MIOpen (False, A/B runs): stride-1 3x3 on the halo kernels, the stride-2
+    stems / stage entries / 1x1 downsamples on the flattened implicit GEMM."""
     _NATIVE_CONV[0] = bool(enabled)
 
 
 def conv3x3(m, srcs, act=None):
-    """act(m(cat(srcs))) for an nn.Conv2d m.  Stride-1 3x3 'same' convolutions
-    on the GPU run on the HIP conv engine (csrc/conv.hip: sources read as a
-    virtual concatenation, bias + ReLU in the epilogue, weight gradient in
-    place into the trainer's flat buffer); everything else through m."""
+    """act(m(cat(srcs))) for an nn.Conv2d m on the HIP conv engine
+    (csrc/conv.hip): stride-1 3x3 'same' convolutions on the halo kernels
+    (sources read as a virtual concatenation, bias + ReLU in the epilogue);
+    stride-1/2 convolutions of one source (the 7x7/s2 stems, 3x3/s2 stage
+    entries, 1x1/s2 downsamples) on the flattened implicit GEMM; weight
+    gradients in place into the trainer's flat buffer.  CPU tensors (and the
+    MIOpen A/B switch) go through m."""
     srcs = list(srcs) if isinstance(srcs, (list, tuple)) else [srcs]
     if (_NATIVE_CONV[0] and srcs[0].is_cuda and m.kernel_size == (3, 3) and m.stride == (1, 1)
             and m.padding == (1, 1) and m.dilation == (1, 1) and m.groups == 1):
         return hip.conv2d(srcs, m.weight, m.bias, act=act)
+    if (_NATIVE_CONV[0] and _NATIVE_STRIDED[0] and srcs[0].is_cuda and len(srcs) == 1 and m.stride[0] == m.stride[1]
+            and m.stride[0] in (1, 2) and m.padding[0] == m.padding[1] and m.dilation == (1, 1)
+            and m.groups == 1 and m.padding_mode == "zeros" and (act is None or not torch.is_grad_enabled())):
+        # the stride-2 stems / stage entries / downsamples (no activation follows
+        # them in the encoders: BatchNorm does)
+        return hip.conv2d_strided(srcs[0], m.weight, m.bias, m.stride[0], m.padding[0], act)
     y = m(srcs[0] if len(srcs) == 1 else torch.cat(srcs, 1))
     return F.relu(y, inplace=True) if act == "relu" else y
 
@@ -97,7 +120,7 @@ class BasicBlock(nn.Module):
         if self.downsample is None:
             skip = x
         else:
-            skip = self.downsample[1].act(self.downsample[0](x), relu=False)
+            skip = self.downsample[1].act(conv3x3(self.downsample[0], x), relu=False)
         return self.bn2.act(conv3x3(self.conv2, y), skip=skip)
 
 
@@ -141,7 +164,7 @@ class ResNetEncoder(nn.Module):
         if isinstance(x, (list, tuple)):
             chunks = len(x)
             x = torch.cat(list(x), 0)
-        x = self.bn1.act(self.conv1(x))
+        x = self.bn1.act(conv3x3(self.conv1, x))
         x = hip.maxpool3x3s2(x) if (x.is_cuda and _NATIVE_POOL[0]) else F.max_pool2d(x, 3, 2, 1)
         s4 = self.layer1(x)
         s8 = self.layer2(s4)

@@ -404,6 +404,27 @@ int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, in
  * saved output y).  grad_weight [Cout][Cin][KH][KW] / grad_bias [Cout]
  * (nullable) are overwritten or, with accumulate, added to.  1 <= nuse <= 16;
  * kernel shapes 1x1, 1x5, 5x1, 3x3.  Deterministic (fixed reduction order). */
+/* Strided convolutions of the ResNet encoders (extractor.py:7-107: the 7x7/s2
+ * stems, 3x3/s2 stage entries, 1x1/s2 downsamples of torchvision's ResNet-18).
+ * x dense [B, Cin, Hi, Wi]; weight [Cout, Cin, KH, KW]; stride 1 or 2;
+ * symmetric zero padding `pad`; out [B, Cout, Ho, Wo] with
+ * Ho = (Hi + 2 pad - KH) / stride + 1.  Forward: bias (nullable) and act
+ * (0 none, 1 relu, 2 sigmoid, 3 tanh) in the epilogue.  Backward (act none):
+ * grad_x (nullable; grad_x_accumulate adds into it), grad_weight / grad_bias
+ * (nullable; grad_weight_accumulate adds).  Workspace from
+ * dro_conv2d_strided_workspace_bytes.  Flattened implicit GEMM on f32 MFMA,
+ * deterministic. */
+size_t dro_conv2d_strided_workspace_bytes(int B, int Hi, int Wi, int Cin, int Cout, int KH, int KW,
+                                          int stride, int pad);
+int dro_conv2d_strided_forward(const float* x, const float* weight, const float* bias, int B, int Hi,
+                               int Wi, int Cin, int Cout, int KH, int KW, int stride, int pad, int act,
+                               float* out, void* workspace, size_t workspace_bytes, void* stream);
+int dro_conv2d_strided_backward(const float* x, const float* weight, const float* dout, int B, int Hi,
+                                int Wi, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                                float* grad_x, int grad_x_accumulate, float* grad_weight,
+                                float* grad_bias, int grad_weight_accumulate, void* workspace,
+                                size_t workspace_bytes, void* stream);
+
 typedef struct dro_wgrad_use {
   const dro_slice* srcs;  /* the nsrc input slices of this use */
   const float* dout;      /* dense [B,Cout,H,W] gradient w.r.t. this use's output */

@@ -319,3 +319,43 @@ def test_weight_split_exact(hip):
     refb = w.reshape(Cout, Cin, T).flip(2).permute(1, 0, 2).double()  # [Cin][o][flipped tap]
     gotb = s.permute(0, 1, 3, 2).reshape(Cin, -1, T)[:, :Cout]
     assert ((gotb - refb).abs() <= refb.abs() * 2.0 ** -24).all()
+
+
+@pytest.mark.parametrize("case", [
+    # (B, Cin, Cout, Hi, Wi, k, stride, pad, bias, act): the encoders' strided convs
+    (2, 64, 128, 48, 160, 3, 2, 1, False, None),     # layer2 stage entry (KITTI cnet_depth)
+    (2, 128, 256, 24, 80, 3, 2, 1, False, None),     # layer3 stage entry
+    (2, 64, 128, 48, 160, 1, 2, 0, False, None),     # 1x1/s2 downsample
+    (2, 3, 64, 64, 96, 7, 2, 3, False, None),        # 7x7/s2 stem (3 channels)
+    (1, 6, 64, 47, 81, 7, 2, 3, False, None),        # cnet_pose stem, odd input size
+    (2, 20, 24, 17, 23, 3, 2, 1, True, "relu"),      # odd sizes, bias + relu forward
+    (2, 16, 40, 12, 20, 3, 1, 0, True, None),        # stride 1, no padding
+])
+def test_conv2d_strided(hip, case):
+    """hip.conv2d_strided (dro_conv2d_strided_*: flattened implicit GEMM with
+    the stride, generic weight gradient) against fp64 F.conv2d: output, input
+    gradient, weight and bias gradients; 1e-4."""
+    B, Cin, Cout, Hi, Wi, k, stride, pad, use_bias, act = case
+    g = torch.Generator().manual_seed(Cin * 7 + Cout)
+    x = torch.randn(B, Cin, Hi, Wi, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g) if use_bias else None
+    xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
+    br = b.double().requires_grad_() if use_bias else None
+    ref = ACTS[act](F.conv2d(xr, wr, br, stride=stride, padding=pad))
+    G = torch.randn(ref.shape, generator=g)
+    xd, wd = x.to(DEV).requires_grad_(), w.to(DEV).requires_grad_()
+    bd = b.to(DEV).requires_grad_() if use_bias else None
+    if act is None:
+        out = hip.conv2d_strided(xd, wd, bd, stride, pad)
+        assert out.shape == ref.shape and rel(out, ref) < TOL
+        (ref * G.double()).sum().backward()
+        (out * G.to(DEV)).sum().backward()
+        assert rel(xd.grad, xr.grad) < TOL
+        assert rel(wd.grad, wr.grad) < TOL
+        if use_bias:
+            assert rel(bd.grad, br.grad) < TOL
+    else:
+        with torch.no_grad():
+            out = hip.conv2d_strided(xd, wd, bd, stride, pad, act=act)
+        assert out.shape == ref.shape and rel(out, ref) < TOL

@@ -67,6 +67,7 @@ for step in "$@"; do
     benche20) run bench_eager20 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --eager ;;
     benchpipe) run bench_pipeline 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pipeline gpu ;;
     benchpem) run bench_pose_enc_main 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pose-encoder-main ;;
+    benchns) run bench_native_strided 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --native-strided-convs ;;
     benchab20) run bench_ab 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
