@@ -61,6 +61,8 @@ def load():
     _sig(lib.dro_depth_metrics_reduce, P, P, P, I, I, I, F, F, I, I, I, I, P, P, S)
     _sig(lib.dro_depth_metrics_median_workspace_bytes, I, restype=Z)
     _sig(lib.dro_depth_metrics_median, P, P, I, I, I, P, P, S)
+    _sig(lib.dro_pose_mean_forward, P, P, P, I, I, I, F, S)
+    _sig(lib.dro_pose_mean_backward, P, P, I, I, I, F, S)
     _sig(lib.dro_conv2d_strided_workspace_bytes, I, I, I, I, I, I, I, I, I, restype=Z)
     _sig(lib.dro_conv2d_strided_forward, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, Z, S)
     _sig(lib.dro_conv2d_strided_backward, P, P, P, I, I, I, I, I, I, I, I, I, P, I, P, P, I, P, Z, S)
@@ -106,6 +108,7 @@ EXPORTED = (
     "dro_depth_metrics_reduce", "dro_depth_metrics_median_workspace_bytes", "dro_depth_metrics_median",
     "dro_depth_metrics_demon_prepare", "dro_depth_metrics_demon_reduce",
     "dro_conv2d_strided_workspace_bytes", "dro_conv2d_strided_forward", "dro_conv2d_strided_backward",
+    "dro_pose_mean_forward", "dro_pose_mean_backward",
     "dro_resize_rgb8_to_tensor", "dro_color_jitter_rgb8", "dro_resize_rgb8", "dro_rgb8_to_tensor",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",

@@ -567,6 +567,39 @@ def depth_metrics_demon(gt, gt_pose, pred, min_depth, max_depth, use_gt_scale=Tr
     return out
 
 
+class _PoseMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, pose, rot_scale):
+        lib = _lib.load()
+        require_device(y, pose, what="pose_mean")
+        B, C, H, W = y.shape
+        y = y.contiguous()
+        p = pose.contiguous() if pose is not None else None
+        out = torch.empty(B, C, device=y.device, dtype=torch.float32)
+        check(lib.dro_pose_mean_forward(ptr(y), ptr(p), ptr(out), B, C, H * W, float(rot_scale), stream_of(y)),
+              "dro_pose_mean_forward")
+        ctx.meta = (B, C, H, W, float(rot_scale), pose is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        B, C, H, W, rs, has_pose = ctx.meta
+        gout = gout.contiguous()
+        gy = torch.empty(B, C, H, W, device=gout.device, dtype=torch.float32)
+        check(lib.dro_pose_mean_backward(ptr(gout), ptr(gy), B, C, H * W, rs, stream_of(gout)),
+              "dro_pose_mean_backward")
+        return gy, (gout if has_pose and ctx.needs_input_grad[1] else None), None
+
+
+def pose_mean(y, rot_scale=0.01, pose=None):
+    """PoseHead's output (update.py:16-28) -- y.mean((2, 3)) with the rotation
+    channels (3..5) scaled by rot_scale -- plus `pose` when given (the update
+    `pose + pose_head(net)`, update.py:189-197): one launch forward, one
+    backward.  y [B, C, H, W], pose [B, C]."""
+    return _PoseMean.apply(y, pose, rot_scale)
+
+
 class _BatchNormAct(torch.autograd.Function):
     """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
 

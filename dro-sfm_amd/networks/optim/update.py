@@ -101,9 +101,11 @@ class DepthHead(nn.Module):
 
 class PoseHead(nn.Module):
     """update.py:16-28: spatial mean of a 6-channel map; rotation scaled by 0.01.
-    One reduction over (H, W) and one multiply by [1, 1, 1, .01, .01, .01]
-    (the reference's mean(3).mean(2) + slice/cat costs 2 reductions forward and
-    2 zero-fills, 2 copies and a cat backward per call; equal to fp32 rounding)."""
+    hip.pose_mean: the mean, the scale and (forward(x, pose)) the update
+    `pose + pose_head(x)` of BasicUpdateBlockPose in one launch each way (the
+    reference's mean(3).mean(2) + slice/cat + add costs 2 reductions, a cat and
+    an add forward, zero-fills, copies and adds backward per call; equal to
+    fp32 rounding)."""
 
     def __init__(self, input_dim=256, hidden_dim=128):
         super().__init__()
@@ -112,10 +114,11 @@ class PoseHead(nn.Module):
         self.register_buffer("_scale", torch.tensor([[1.0, 1.0, 1.0, 0.01, 0.01, 0.01]]),
                              persistent=False)
 
-    def forward(self, x_p):
+    def forward(self, x_p, pose=None):
+        """The pose delta, or pose + delta when `pose` [B, 6] is given."""
         y = conv(conv(x_p, self.conv1_pose.weight, self.conv1_pose.bias, "relu"),
                  self.conv2_pose.weight, self.conv2_pose.bias)
-        return y.mean(dim=(2, 3)) * self._scale
+        return hip.pose_mean(y, 0.01, pose)
 
 
 class SepConvGRU(nn.Module):
@@ -255,6 +258,6 @@ class BasicUpdateBlockPose(nn.Module):
         seq = []
         for _ in range(seq_len):
             net = self.pose_gru(net, [inp, *self.encoder.sources(pose, cost_func(pose))])
-            pose = pose + self.pose_head(net)
+            pose = self.pose_head(net, pose)               # pose + pose_head(net), one launch
             seq.append(pose)
         return net, seq

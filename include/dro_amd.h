@@ -425,6 +425,15 @@ int dro_conv2d_strided_backward(const float* x, const float* weight, const float
                                 float* grad_bias, int grad_weight_accumulate, void* workspace,
                                 size_t workspace_bytes, void* stream);
 
+/* PoseHead spatial mean + rotation scale + pose update (update.py:16-28,
+ * 189-197): out[b, c] = (pose ? pose[b, c] : 0) + mean_{HW} y[b, c] * s_c with
+ * s_c = 1 for c < 3, rot_scale (0.01) otherwise.  y dense [B, C, HW].
+ * Backward: gy[b, c, p] = gout[b, c] * s_c / HW (the pose gradient is gout). */
+int dro_pose_mean_forward(const float* y, const float* pose, float* out, int B, int C, int HW,
+                          float rot_scale, void* stream);
+int dro_pose_mean_backward(const float* gout, float* gy, int B, int C, int HW, float rot_scale,
+                           void* stream);
+
 typedef struct dro_wgrad_use {
   const dro_slice* srcs;  /* the nsrc input slices of this use */
   const float* dout;      /* dense [B,Cout,H,W] gradient w.r.t. this use's output */

@@ -359,3 +359,21 @@ def test_conv2d_strided(hip, case):
         with torch.no_grad():
             out = hip.conv2d_strided(xd, wd, bd, stride, pad, act=act)
         assert out.shape == ref.shape and rel(out, ref) < TOL
+
+
+def test_pose_mean(hip):
+    """hip.pose_mean (PoseHead spatial mean + rotation scale + pose update,
+    update.py:16-28, 189-197) against fp64 torch: value and both gradients."""
+    g = torch.Generator().manual_seed(4)
+    y = torch.randn(4, 6, 24, 80, generator=g)
+    pose = torch.randn(4, 6, generator=g)
+    G = torch.randn(4, 6, generator=g)
+    scale = torch.tensor([1.0, 1.0, 1.0, 0.01, 0.01, 0.01], dtype=torch.float64)
+    yr, pr = y.double().requires_grad_(), pose.double().requires_grad_()
+    ref = pr + yr.mean(dim=(2, 3)) * scale
+    (ref * G.double()).sum().backward()
+    yd, pd = y.to(DEV).requires_grad_(), pose.to(DEV).requires_grad_()
+    out = hip.pose_mean(yd, 0.01, pd)
+    (out * G.to(DEV)).sum().backward()
+    assert rel(out, ref) < TOL and rel(yd.grad, yr.grad) < TOL and rel(pd.grad, pr.grad) < TOL
+    assert rel(hip.pose_mean(yd.detach(), 0.01), yr.detach().mean(dim=(2, 3)) * scale) < TOL
