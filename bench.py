@@ -275,7 +275,7 @@ MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_32
 def roofline_kernels():
     """Names of the kernels one roofline call launches: the weight-gradient
     kernel and its split-sum finish (rocprof name prefixes)."""
-    return ["wgrad2_kernel<3, 3, 0, true>", "wgrad2_finish_kernel<"], None, None
+    return ["wgrad2_kernel<3, 3, 0, true, 1>", "wgrad2_finish_kernel<"], None, None
 
 
 def roofline_conv(device, iters=50, traffic_file=None):
@@ -286,7 +286,7 @@ def roofline_conv(device, iters=50, traffic_file=None):
     BasicBlock) over the 6 frames of a KITTI metric batch (B=2 targets + 4
     refs, 48x160, 64 -> 64 channels), through the same entry point the
     trainer's in-place path uses (dro_conv2d_weight_grad_multi, one use):
-    wgrad2_kernel<3,3,0,true> over 240 pixel splits + wgrad2_finish_kernel
+    wgrad2_kernel<3,3,0,true,1> over 240 pixel splits + wgrad2_finish_kernel
     (fixed-order split sum into the weight gradient).  HIP events bracket both
     launches on the launch stream.  Algorithmic flops per call:
     2 * Cout * Cin * 9 * B*H*W."""

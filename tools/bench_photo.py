@@ -30,7 +30,10 @@ def main():
            + 0.1 * torch.rand(B, 3, H, W, generator=g, device=dev)).clamp(0, 1)
     ctx = torch.stack([(torch.roll(img, 3 * (j + 1), 3) * 0.9
                         + 0.1 * torch.rand(B, 3, H, W, generator=g, device=dev)) for j in range(N)])
-    invs = (0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g, device=dev)).requires_grad_(True)
+    # smooth inverse depths, as the net produces them (upsampled from 1/8 resolution)
+    low = 0.02 + 0.3 * torch.rand(n * B, 1, H // 8, W // 8, generator=g, device=dev)
+    invs = torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
+    invs = invs.view(n, B, 1, H, W).contiguous().requires_grad_(True)
     pose = torch.cat([0.1 * torch.randn(N, n, B, 3, generator=g, device=dev),
                       0.02 * torch.randn(N, n, B, 3, generator=g, device=dev)], 3).requires_grad_(True)
     K = torch.tensor([[371.8, 0.0, 314.1], [0.0, 369.4, 88.5], [0.0, 0.0, 1.0]],
