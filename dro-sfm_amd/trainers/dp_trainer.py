@@ -82,6 +82,10 @@ class GradBuckets:
         # always_reduce: issue the collectives even at world size 1 (tests of the
         # RCCL path inside a captured graph on a single-GPU box)
         self.reduce = self.world > 1 or (always_reduce and dist.is_initialized())
+        # suspend: no collectives from the hooks or finish(); reduce_now() runs
+        # them after the step's backward (GraphedTrainStep keeps RCCL out of
+        # the captured graph, see there)
+        self.suspend = False
         self.params = _adjacent_order([p for p in params if p.requires_grad], groups)
         if any(p.dtype != torch.float32 for p in self.params):
             raise RuntimeError("GradBuckets: fp32 parameters only")
@@ -181,7 +185,7 @@ class GradBuckets:
             b = self._order[self._next]
             self._next += 1
             self.issued.append(b)
-            if self.reduce:
+            if self.reduce and not self.suspend:
                 if self._events[b] is not None:
                     torch.cuda.current_stream().wait_event(self._events[b])
                 self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
@@ -247,6 +251,16 @@ class GradBuckets:
             for work in self._pending:
                 work.wait()
             self._pending = []
+        if self.world > 1 and not self.suspend:
+            self.flat.div_(self.world)
+
+    def reduce_now(self):
+        """All-reduce the whole flat gradient (one collective) and average: the
+        exchange of a step whose backward ran with `suspend` set.  Slots of
+        parameters without a gradient are zeros and reduce harmlessly."""
+        if not self.reduce:
+            return
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         if self.world > 1:
             self.flat.div_(self.world)
 
@@ -470,7 +484,7 @@ class DataParallelTrainer:
             self.optimizer = torch.optim.Adam(self.grads.params, lr=lr, betas=betas, eps=eps,
                                               foreach=True, capturable=capturable)
 
-    def _step_inner(self, batch, **fwd_kw):
+    def _forward_backward(self, batch, **fwd_kw):
         self.grads.zero()
         out = self.model(batch, **fwd_kw)
         loss = out["loss"]
@@ -479,8 +493,12 @@ class DataParallelTrainer:
         if isinstance(self.optimizer, FlatAdam) and self.optimizer.active is None \
                 and self.grads.active is not None:
             self.optimizer.active = set(self.grads.active)
-        self.optimizer.step()
         return loss.detach(), out.get("metrics", {})
+
+    def _step_inner(self, batch, **fwd_kw):
+        res = self._forward_backward(batch, **fwd_kw)
+        self.optimizer.step()
+        return res
 
     def step(self, batch, **fwd_kw):
         self.model.train()
@@ -522,13 +540,24 @@ class GraphedTrainStep:
     The first eager steps (bucket discovery, MIOpen algorithm selection) run
     before capture on a side stream and are real training steps.
 
+    With a gradient exchange (world > 1), the graph holds zero -> forward ->
+    loss -> backward only; each step() replays it, then all-reduces the flat
+    gradient eagerly (ONE RCCL collective) and runs the fused Adam launch.
+    RCCL collectives captured inside the graph (`reduce_in_graph=True`, the
+    bucketed all-reduces overlapping backward) crash this image's RCCL
+    (2.26.6 / HIP 7.0) in hipStreamEndCapture (SIGSEGV at capture_end, seen at
+    world size 1 with the collectives forced on), so they stay opt-in.
+
     The graphs hold the ADDRESSES of the parameters, gradients and Adam state:
     restore checkpoints in place (tensor.copy_), or build a new GraphedTrainStep
     after optimizer.load_state_dict (which replaces the state tensors).
     """
 
-    def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True):
+    def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True,
+                 reduce_in_graph=False):
         self.tr = trainer
+        # collectives outside the graph when there is an exchange at all
+        self.outside = trainer.grads.reduce and not reduce_in_graph
         self.model = trainer.model
         self.static = _clone_batch(example_batch)
         self.static["intrinsics_ref"] = example_batch["intrinsics"].clone()
@@ -546,13 +575,23 @@ class GraphedTrainStep:
         for f in flips:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool):
-                out = self._body(f)
+                out = self._captured(f)
             self.graphs[f] = (g, out)
         torch.cuda.synchronize()
 
     def _body(self, flip):
         self.static["intrinsics"].copy_(self.static["intrinsics_ref"])
         return self.tr._step_inner(self.static, flip=flip)
+
+    def _captured(self, flip):
+        if not self.outside:
+            return self._body(flip)
+        self.static["intrinsics"].copy_(self.static["intrinsics_ref"])
+        self.tr.grads.suspend = True
+        try:
+            return self.tr._forward_backward(self.static, flip=flip)
+        finally:
+            self.tr.grads.suspend = False
 
     def step(self, batch, flip=None):
         sync = getattr(self.tr.optimizer, "sync_hyper", None)
@@ -564,4 +603,7 @@ class GraphedTrainStep:
             flip = self.model._rng.random() < self.model.flip_lr_prob
         g, out = self.graphs[bool(flip)]
         g.replay()
+        if self.outside:
+            self.tr.grads.reduce_now()
+            self.tr.optimizer.step()
         return out

@@ -64,7 +64,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, steps, out, skip=False):
+def _worker(rank, world, port, steps, out, skip=False, outside=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, init_distributed
@@ -77,7 +77,17 @@ def _worker(rank, world, port, steps, out, skip=False):
         batch = data(rank, s)
         if skip:
             batch["use_d"] = (s, rank) not in SKIP
-        tr.step(batch)
+        if outside and s > 0:
+            # GraphedTrainStep's sequence at world > 1: backward with the
+            # collectives suspended (the captured part), then one all-reduce
+            # of the flat gradient and the optimizer step
+            tr.grads.suspend = True
+            tr._forward_backward(batch)
+            tr.grads.suspend = False
+            tr.grads.reduce_now()
+            tr.optimizer.step()
+        else:
+            tr.step(batch)
     flat = torch.cat([p.detach().flatten() for p in model.parameters()])
     out[rank] = (flat, len(tr.grads.buckets), torch.equal(model.dead.weight, dead0) or rank)
     dist.barrier()
@@ -85,12 +95,14 @@ def _worker(rank, world, port, steps, out, skip=False):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_matches_single_process():
+@pytest.mark.parametrize("outside", [False, True])
+def test_two_rank_gloo_matches_single_process(outside):
+    """outside=True: the exchange after backward (GraphedTrainStep at world > 1)."""
     steps = 4
     port = _free_port()
     with mp.Manager() as mgr:
         out = mgr.dict()
-        mp.spawn(_worker, args=(2, port, steps, out), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, port, steps, out, False, outside), nprocs=2, join=True)
         res = dict(out)
     (p0, nb0, dead_ok), (p1, nb1, _) = res[0], res[1]
     assert torch.equal(p0, p1), "ranks diverged"

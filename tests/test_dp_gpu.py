@@ -6,9 +6,13 @@
   bit-identical, and equal (to fp32 reassociation) to one process minimising
   the mean of the two per-rank losses -- the exact data-parallel semantics with
   per-replica BatchNorm statistics (no SyncBN, as the reference).
-* RCCL inside a captured hipGraph: a world-size-1 "nccl" (RCCL) group with the
-  bucket all-reduces forced on (always_reduce), GraphedTrainStep replay vs the
-  eager step from the same state.
+* RCCL with the captured hipGraph step: a world-size-1 "nccl" (RCCL) group
+  with the exchange forced on (always_reduce); GraphedTrainStep (graph of
+  zero -> forward -> backward, then ONE eager RCCL all-reduce and Adam, its
+  world > 1 mode) replay vs the eager step (bucketed all-reduces issued from
+  the backward hooks) from the same state.  Collectives captured INSIDE the
+  graph crash this image's RCCL at capture_end (SIGSEGV): opt-in only
+  (GraphedTrainStep reduce_in_graph), not run here.
 
 Reference: horovod_trainer.py:67-69 (dormant DistributedOptimizer),
 model_wrapper.py:818-822 (DistributedSampler).
@@ -133,9 +137,16 @@ def test_two_ranks_one_gpu_real_model_direct_weight_grads():
 
 
 def _rccl_graph_worker(rank, port, out):
-    """World-size-1 RCCL group; GraphedTrainStep with the bucket all-reduces
-    captured; replay vs eager from the same state.  Runs in a child process so
+    """World-size-1 RCCL group; GraphedTrainStep with the exchange after the
+    replayed graph; replay vs eager from the same state.  Runs in a child process so
     that RCCL's watchdog or teardown cannot take the test runner down."""
+    import faulthandler
+    import sys
+    faulthandler.enable()
+
+    def stage(msg):
+        print(f"[rccl-graph worker] {msg}", file=sys.stderr, flush=True)
+
     from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep
     from oracle import dro_oracle as O
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -146,7 +157,10 @@ def _rccl_graph_worker(rank, port, out):
         K0 = batch["intrinsics"].clone()
         m = _model()
         tr = DataParallelTrainer(m, capturable=True, bucket_mb=4.0, always_reduce=True)
+        stage("trainer built; capturing")
         gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False,))
+        stage("captured")
+        assert gs.outside, "the exchange must run outside the captured graph"
         nb, issued = len(tr.grads.buckets), list(tr.grads.issued)
         snap_m = {k: v.clone() for k, v in m.state_dict().items()}
         snap_s = [{k: v.clone() for k, v in st.items()} for st in tr.optimizer.state.values()]
@@ -161,24 +175,28 @@ def _rccl_graph_worker(rank, port, out):
             batch["intrinsics"].copy_(K0)
 
         restore()
+        stage("replay")
         lg = gs.step(batch, flip=False)[0].clone()
         gg = tr.grads.flat.clone()
         restore()
+        stage("eager")
         le = tr.step(batch, flip=False)[0].clone()
         ge = tr.grads.flat.clone()
         torch.cuda.synchronize()
         out["res"] = (nb, issued, O.rel_err(lg.cpu(), le.cpu()), float((gg - ge).norm() / ge.norm()))
+    stage("results recorded; teardown")
     # the graphs hold RCCL kernels of this communicator: release them first
     del gs
     torch.cuda.synchronize()
     dist.barrier()
     dist.destroy_process_group()
+    stage("teardown done")
 
 
 @pytest.mark.timeout(300)
-def test_rccl_all_reduce_inside_captured_graph():
-    """The bucket all-reduces (RCCL, forced on at world size 1) captured inside
-    the step's hipGraph: replay == eager from the same state."""
+def test_rccl_exchange_with_captured_graph_step():
+    """RCCL (forced on at world size 1) around the step's hipGraph: replay +
+    all-reduce + Adam == the eager step with hook-issued bucket all-reduces."""
     with mp.Manager() as mgr:
         out = mgr.dict()
         mp.spawn(_rccl_graph_worker, args=(_free_port(), out), nprocs=1, join=True)
