@@ -12,6 +12,8 @@
 // 4*r^2*hw written per image.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "dro_common.hpp"
 
 namespace dro {
@@ -289,6 +291,157 @@ __global__ __launch_bounds__(512) void convex_up_bwd_cw_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// n predictions in one launch each way (every kept prediction of a training
+// step: DepthPoseNet.py:180-181 per iteration, stacked by the losses).  The
+// forward writes [n, B, 1, hr, wr] directly (the losses' stack is a view).
+// The backward is deterministic: one block per (pred, image, 64-pixel run),
+// wave c = sub-pixel column, each thread loops over the r sub-pixel rows and
+// keeps its 9 tap sums; the waves' sums are added in the order c = 0..r-1
+// through LDS and written per (tap, low-res pixel) to a workspace; a second
+// launch gathers each low-res pixel's 9 neighbour-tap sums in tap order
+// (no atomics, no zero-fill of the inverse-depth gradient).
+constexpr int kMaxPred = 32;
+struct UpMany {
+  const float* inv[kMaxPred];
+  const float* mask[kMaxPred];
+  float* ginv[kMaxPred];
+  float* gmask[kMaxPred];
+};
+typedef __attribute__((address_space(4))) const char* KArg;
+template <typename Tp>
+__device__ __forceinline__ Tp up_ptr(size_t field, int i) {   // table entry read from the kernarg segment
+  return *(__attribute__((address_space(4))) Tp const*)((KArg)__builtin_amdgcn_kernarg_segment_ptr() + field +
+                                                       (size_t)i * sizeof(Tp));
+}
+
+__global__ __launch_bounds__(256) void convex_up_many_fwd_kernel(UpMany t, int B, int h, int w, int r, float add,
+                                                                float mul, float* __restrict__ out) {
+  const int hw = h * w, pred = blockIdx.y;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * r * hw * r) return;
+  const float* __restrict__ inv = up_ptr<const float*>(offsetof(UpMany, inv), pred);
+  const float* __restrict__ mask = up_ptr<const float*>(offsetof(UpMany, mask), pred);
+  int b, a, y, x, c;
+  cu_decode(idx, h, w, r, b, a, y, x, c);
+  const int pix = y * w + x;
+  float d[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    d[k] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? inv[(size_t)b * hw + yy * w + xx] : 0.f;
+  }
+  const float* mb = mask + (size_t)b * 9 * r * r * hw + pix;
+  float m[9], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = mb[(size_t)(k * r * r + a * r + c) * hw];
+    mx = fmaxf(mx, m[k]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = expf(m[k] - mx);
+    s += m[k];
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc += (m[k] / s) * d[k];
+  out[(size_t)pred * B * hw * r * r + ((size_t)b * h * r + (size_t)y * r + a) * (w * r) + (size_t)x * r + c] =
+      __fadd_rn(add, __fmul_rn(mul, acc));
+}
+
+// block = 64 * r threads; grid (ceil(hw / 64), B, n); tsum [n][B][9][hw].
+// R > 0: the ratio as a compile-time constant (the sub-pixel row loop fully
+// unrolled, so every row's mask loads are in flight together); R = 0: runtime r.
+template <int R>
+__global__ __launch_bounds__(512) void convex_up_many_bwd_kernel(UpMany t, const float* __restrict__ gout, int B,
+                                                                int h, int w, int r_, float mul,
+                                                                float* __restrict__ tsum) {
+  const int r = R > 0 ? R : r_;
+  __shared__ float red[kMaxR][9][64];
+  const int hw = h * w, pred = blockIdx.z, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, c = threadIdx.x >> 6;
+  const int pix = blockIdx.x * 64 + lane;
+  const bool live = pix < hw;
+  const int pp = live ? pix : 0;
+  const int y = pp / w, x = pp - y * w;
+  const float* __restrict__ inv = up_ptr<const float*>(offsetof(UpMany, inv), pred);
+  const float* __restrict__ mask = up_ptr<const float*>(offsetof(UpMany, mask), pred);
+  float* __restrict__ gmask = up_ptr<float*>(offsetof(UpMany, gmask), pred);
+  const bool want_inv = up_ptr<float*>(offsetof(UpMany, ginv), pred) != nullptr;
+  float d[9], tk[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    d[k] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? inv[(size_t)b * hw + yy * w + xx] : 0.f;
+    tk[k] = 0.f;
+  }
+  const float* mb = mask + (size_t)b * 9 * r * r * hw + pp;
+  float* gmb = gmask + (size_t)b * 9 * r * r * hw + pix;
+  const float* gb = gout + (size_t)pred * B * hw * r * r + ((size_t)b * h * r + (size_t)y * r) * (w * r) +
+                    (size_t)x * r + c;
+#pragma unroll
+  for (int a = 0; a < (R > 0 ? R : kMaxR); ++a) {
+    if (R == 0 && a >= r) break;
+    const float G = __fmul_rn(gb[(size_t)a * (w * r)], mul);
+    float m[9], mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      m[k] = mb[(size_t)(k * r * r + a * r + c) * hw];
+      mx = fmaxf(mx, m[k]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      m[k] = expf(m[k] - mx);
+      s += m[k];
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      m[k] = m[k] / s;
+      tk[k] += m[k] * G;
+      dot += m[k] * (G * d[k]);
+    }
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gmb[(size_t)(k * r * r + a * r + c) * hw] = m[k] * (G * d[k] - dot);
+    }
+  }
+  if (!want_inv) return;   // block-uniform
+#pragma unroll
+  for (int k = 0; k < 9; ++k) red[c][k][lane] = tk[k];
+  __syncthreads();
+  if (c == 0 && live) {
+    float* ts = tsum + ((size_t)pred * B + b) * 9 * hw + pix;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      float v = 0.f;
+      for (int cc = 0; cc < r; ++cc) v += red[cc][k][lane];
+      ts[(size_t)k * hw] = v;
+    }
+  }
+}
+
+// ginv[pred][b][q] = sum_k tsum[pred][b][k][q - off(k)], off(k) = (k/3 - 1, k%3 - 1)
+__global__ __launch_bounds__(256) void convex_up_many_gather_kernel(UpMany t, const float* __restrict__ tsum, int B,
+                                                                   int h, int w) {
+  const int hw = h * w, pred = blockIdx.z, b = blockIdx.y;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  float* __restrict__ ginv = up_ptr<float*>(offsetof(UpMany, ginv), pred);
+  if (q >= hw || ginv == nullptr) return;
+  const int qy = q / w, qx = q - qy * w;
+  const float* ts = tsum + ((size_t)pred * B + b) * 9 * hw;
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int py = qy - (k / 3 - 1), px = qx - (k % 3 - 1);
+    if (py >= 0 && py < h && px >= 0 && px < w) v += ts[(size_t)k * hw + py * w + px];
+  }
+  ginv[(size_t)b * hw + q] = v;
+}
+
+// ---------------------------------------------------------------------------
 // Bilinear 2x upsampling (align_corners=False) of the feature/context trunks:
 // F.interpolate(x, scale_factor=2, mode="bilinear") in networks/optim/
 // extractor.py:91-97 of the reference.  ATen's kernel runs one thread per
@@ -422,6 +575,90 @@ extern "C" int dro_convex_upsample_backward(const float* inv, const float* mask,
   hipLaunchKernelGGL(convex_up_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, inv, mask,
                      grad_out, B, h, w, ratio, mul, grad_inv, grad_mask);
   return launch_status("convex_up_bwd_kernel launch failed");
+}
+
+static int up_many_check(const float* const* inv, const float* const* mask, int n, int B, int h, int w,
+                         int ratio, UpMany& t) {
+  if (!inv || !mask) {
+    set_error("convex_upsample_many: NULL pointer table");
+    return DRO_E_NULL;
+  }
+  if (n < 1 || n > kMaxPred) {
+    set_error("convex_upsample_many: 1..32 predictions per call");
+    return DRO_E_SHAPE;
+  }
+  for (int i = 0; i < n; ++i) {
+    int st = up_check(inv[i], mask[i], B, h, w, ratio);
+    if (st) return st;
+    if ((long long)n * B * ratio * ratio * h * w >= (1LL << 31)) {
+      set_error("convex_upsample_many: output of >= 2^31 elements");
+      return DRO_E_SHAPE;
+    }
+    t.inv[i] = inv[i];
+    t.mask[i] = mask[i];
+  }
+  return DRO_OK;
+}
+
+extern "C" int dro_convex_upsample_many_forward(const float* const* inv, const float* const* mask, int n, int B,
+                                                int h, int w, int ratio, float add, float mul, float* out,
+                                                void* stream) {
+  UpMany t = {};
+  int st = up_many_check(inv, mask, n, B, h, w, ratio, t);
+  if (st) return st;
+  if (!out) {
+    set_error("convex_upsample_many_forward: NULL out");
+    return DRO_E_NULL;
+  }
+  const int total = B * ratio * h * w * ratio;
+  hipLaunchKernelGGL(convex_up_many_fwd_kernel, dim3((total + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, t,
+                     B, h, w, ratio, add, mul, out);
+  return launch_status("convex_up_many_fwd_kernel launch failed");
+}
+
+extern "C" size_t dro_convex_upsample_many_workspace_bytes(int n, int B, int h, int w) {
+  if (n < 1 || B < 1 || h < 1 || w < 1) return 0;
+  return (size_t)n * B * 9 * h * w * sizeof(float);
+}
+
+extern "C" int dro_convex_upsample_many_backward(const float* const* inv, const float* const* mask,
+                                                 const float* grad_out, int n, int B, int h, int w, int ratio,
+                                                 float mul, float* const* grad_inv, float* const* grad_mask,
+                                                 void* workspace, size_t workspace_bytes, void* stream) {
+  UpMany t = {};
+  int st = up_many_check(inv, mask, n, B, h, w, ratio, t);
+  if (st) return st;
+  if (!grad_out || !grad_mask || B > 65535) {
+    set_error("convex_upsample_many_backward: NULL grad_out/grad_mask table, or B > 65535");
+    return DRO_E_NULL;
+  }
+  bool any_inv = false;
+  for (int i = 0; i < n; ++i) {
+    if (!grad_mask[i]) {
+      set_error("convex_upsample_many_backward: NULL grad_mask entry");
+      return DRO_E_NULL;
+    }
+    t.gmask[i] = grad_mask[i];
+    t.ginv[i] = grad_inv ? grad_inv[i] : nullptr;
+    any_inv |= t.ginv[i] != nullptr;
+  }
+  if (any_inv && (!workspace || workspace_bytes < dro_convex_upsample_many_workspace_bytes(n, B, h, w))) {
+    set_error("convex_upsample_many_backward: workspace too small (dro_convex_upsample_many_workspace_bytes)");
+    return DRO_E_SHAPE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  float* tsum = static_cast<float*>(workspace);
+  if (ratio == 8)
+    hipLaunchKernelGGL(convex_up_many_bwd_kernel<8>, dim3((h * w + 63) / 64, B, n), dim3(64 * ratio), 0, s, t,
+                       grad_out, B, h, w, ratio, mul, tsum);
+  else
+    hipLaunchKernelGGL(convex_up_many_bwd_kernel<0>, dim3((h * w + 63) / 64, B, n), dim3(64 * ratio), 0, s, t,
+                       grad_out, B, h, w, ratio, mul, tsum);
+  if ((st = launch_status("convex_up_many_bwd_kernel launch failed"))) return st;
+  if (!any_inv) return DRO_OK;
+  hipLaunchKernelGGL(convex_up_many_gather_kernel, dim3((h * w + 255) / 256, B, n), dim3(256), 0, s, t, tsum, B, h,
+                     w);
+  return launch_status("convex_up_many_gather_kernel launch failed");
 }
 
 static int bl2_check(const float* a, const float* b, long long planes, int h, int w) {

@@ -51,6 +51,9 @@ def load():
     _sig(lib.dro_supervised_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, P, P, S)
     _sig(lib.dro_convex_upsample_forward, P, P, I, I, I, I, F, F, P, S)
     _sig(lib.dro_convex_upsample_backward, P, P, P, I, I, I, I, F, P, P, S)
+    _sig(lib.dro_convex_upsample_many_forward, P, P, I, I, I, I, I, F, F, P, S)
+    _sig(lib.dro_convex_upsample_many_workspace_bytes, I, I, I, I, restype=Z)
+    _sig(lib.dro_convex_upsample_many_backward, P, P, P, I, I, I, I, I, F, P, P, P, Z, S)
     _sig(lib.dro_bilinear_upsample2x_forward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_bilinear_upsample2x_backward, P, ctypes.c_longlong, I, I, P, S)
     _sig(lib.dro_maxpool3x3s2_forward, P, ctypes.c_longlong, I, I, P, P, S)
@@ -102,6 +105,8 @@ EXPORTED = (
     "dro_photometric_workspace_bytes", "dro_photometric_forward", "dro_photometric_backward",
     "dro_supervised_workspace_bytes", "dro_supervised_forward", "dro_supervised_backward",
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
+    "dro_convex_upsample_many_forward", "dro_convex_upsample_many_workspace_bytes",
+    "dro_convex_upsample_many_backward",
     "dro_bilinear_upsample2x_forward", "dro_bilinear_upsample2x_backward",
     "dro_maxpool3x3s2_forward", "dro_maxpool3x3s2_backward",
     "dro_depth_metrics_blocks", "dro_depth_metrics_workspace_bytes", "dro_depth_metrics_prepare",

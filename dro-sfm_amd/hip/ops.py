@@ -400,6 +400,77 @@ def convex_upsample(inv, mask, ratio=8, affine=None):
     return _ConvexUpsample.apply(inv, mask, int(ratio), float(add), float(mul))
 
 
+def _ptr_table(ts):
+    arr = (ctypes.c_void_p * len(ts))()
+    for i, t in enumerate(ts):
+        arr[i] = t.data_ptr() if t is not None else None
+    return arr
+
+
+class _ConvexUpsampleMany(torch.autograd.Function):
+    """n convex upsamples in one launch each way -> [n, B, 1, rh, rw]."""
+
+    @staticmethod
+    def forward(ctx, ratio, add, mul, n, *tensors):
+        lib = _lib.load()
+        invs = [t.contiguous() for t in tensors[:n]]
+        masks = [t.contiguous() for t in tensors[n:]]
+        require_device(*invs, *masks, what="convex_upsample_many")
+        B, _, h, w = invs[0].shape
+        for i, m in zip(invs, masks):
+            if i.shape != (B, 1, h, w) or m.shape != (B, 9 * ratio * ratio, h, w):
+                raise RuntimeError("convex_upsample_many: every inv must be [B,1,h,w] and mask [B,9*r*r,h,w]")
+        out = torch.empty(n, B, 1, h * ratio, w * ratio, device=invs[0].device, dtype=torch.float32)
+        check(lib.dro_convex_upsample_many_forward(_ptr_table(invs), _ptr_table(masks), n, B, h, w, ratio,
+                                                   ctypes.c_float(add), ctypes.c_float(mul), ptr(out),
+                                                   stream_of(out)), "dro_convex_upsample_many_forward")
+        ctx.save_for_backward(*invs, *masks)
+        ctx.n, ctx.ratio, ctx.mul = n, ratio, mul
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        n = ctx.n
+        saved = ctx.saved_tensors
+        invs, masks = saved[:n], saved[n:]
+        B, _, h, w = invs[0].shape
+        g_inv = [torch.empty_like(t) if ctx.needs_input_grad[4 + i] else None for i, t in enumerate(invs)]
+        g_mask = [torch.empty_like(m) for m in masks]
+        nb = int(lib.dro_convex_upsample_many_workspace_bytes(n, B, h, w))
+        ws = torch.empty(nb, dtype=torch.uint8, device=gout.device)
+        check(lib.dro_convex_upsample_many_backward(_ptr_table(invs), _ptr_table(masks), ptr(gout.contiguous()),
+                                                    n, B, h, w, ctx.ratio, ctypes.c_float(ctx.mul),
+                                                    _ptr_table(g_inv), _ptr_table(g_mask), ptr(ws), nb,
+                                                    stream_of(gout)), "dro_convex_upsample_many_backward")
+        g_mask = [g if ctx.needs_input_grad[4 + n + i] else None for i, g in enumerate(g_mask)]
+        return (None, None, None, None, *g_inv, *g_mask)
+
+
+def convex_upsample_many(invs, masks, ratio=8, affine=None):
+    """convex_upsample of n (inv, mask) pairs in one launch each way: returns the
+    stacked [n, B, 1, rh, rw] (the losses read the predictions stacked;
+    stacked_view() recovers it from its unbind() views).  Deterministic
+    backward (no atomics)."""
+    if not 1 <= len(invs) == len(masks) <= 32:
+        raise RuntimeError("convex_upsample_many: 1..32 (inv, mask) pairs")
+    add, mul = affine if affine is not None else (0.0, 1.0)
+    return _ConvexUpsampleMany.apply(int(ratio), float(add), float(mul), len(invs), *invs, *masks)
+
+
+def stacked_view(ts):
+    """torch.stack(ts) without the copy when ts are, in order, the unbind()
+    views of one contiguous [n, ...] tensor (convex_upsample_many's output);
+    otherwise torch.stack(ts)."""
+    ts = list(ts)
+    base = ts[0]._base if ts else None
+    if (base is not None and base.is_contiguous() and base.dim() == ts[0].dim() + 1 and base.shape[0] == len(ts)
+            and all(t._base is base and t.shape == base.shape[1:] and
+                    t.storage_offset() == base.storage_offset() + i * base.stride(0) for i, t in enumerate(ts))):
+        return base
+    return torch.stack(ts, 0)
+
+
 # ------------------------------------------------------------------ bilinear 2x upsample
 class _Bilinear2x(torch.autograd.Function):
     @staticmethod

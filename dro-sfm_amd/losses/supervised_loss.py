@@ -11,7 +11,7 @@ forward, 2 backward.  There is no CPU path: the op raises on CPU tensors.
 import torch
 
 from ..geometry.pose import Pose, kernel_pose_tensor
-from ..hip import supervised_loss
+from ..hip import stacked_view, supervised_loss
 from .loss_base import LossBase, ProgressiveScaling
 
 
@@ -41,7 +41,7 @@ class SupervisedDepthPoseLoss(LossBase):
         if any(d.shape[-2:] != gt_inv_depth.shape[-2:] for d in inv_depths):
             raise NotImplementedError("predictions must be at the ground-truth resolution")
         n, N = self.n, len(gt_pose_context)
-        invs = torch.stack(list(inv_depths), 0)                                  # [n,B,1,H,W]
+        invs = stacked_view(inv_depths)                                  # [n,B,1,H,W]
         pose_t = kernel_pose_tensor(poses, n)                                    # [N,n,B,6|3x4]
         gt_t = torch.stack([_gt_matrix(p).float() for p in gt_pose_context], 0)  # [N,B,4,4]
         loss, metrics = supervised_loss(gt_inv_depth.float(), invs, pose_t, gt_t, K.float(),

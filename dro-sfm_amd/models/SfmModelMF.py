@@ -4,6 +4,7 @@ import random
 import torch
 import torch.nn as nn
 
+from .. import hip
 from ..geometry.pose import Pose, PoseGrid
 
 
@@ -64,7 +65,8 @@ class SfmModelMF(nn.Module):
             inv_depths, poses = self.depth_net(image, ref_imgs, intrinsics)
         inv_depths = inv_depths if isinstance(inv_depths, (list, tuple)) else [inv_depths]
         if flip:
-            inv_depths = [flip_lr(d) for d in inv_depths]
+            # the flip back: one launch over the stacked predictions
+            inv_depths = list(torch.flip(hip.stacked_view(inv_depths), [-1]).unbind(0))
         # upsample_depth_maps: predictions are already full resolution (identity)
         return list(inv_depths), poses
 

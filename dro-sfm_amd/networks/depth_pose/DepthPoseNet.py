@@ -28,6 +28,7 @@ Execution plan (what changes versus the reference, never the math):
 """
 import contextlib
 import logging
+import os
 
 import torch
 import torch.nn as nn
@@ -54,6 +55,15 @@ def parse_version(version):
 
 _CONCURRENT = [False]
 _SIDE_STREAMS = {}
+
+
+_UPSAMPLE_MANY = [os.environ.get("DRO_UPSAMPLE_MANY", "1") != "0"]
+
+
+def set_upsample_many(enabled):
+    """All kept predictions upsampled in one launch each way after the
+    recurrence (default), or one upsample launch per prediction (A/B)."""
+    _UPSAMPLE_MANY[0] = bool(enabled)
 
 
 def set_concurrent_encoders(enabled):
@@ -141,6 +151,17 @@ class DepthPoseNet(nn.Module):
         lo, hi = 1.0 / self.max_depth, 1.0 / self.min_depth
         return hip.convex_upsample(depth, mask, ratio, affine=(lo, hi - lo))
 
+    def upsample_many(self, pairs, ratio=8):
+        """upsample_scaled of every kept (disp, mask) pair of a training step in
+        ONE launch each way (the upsampled maps feed only the losses, which read
+        them stacked): the [n, B, 1, H, W] stack's unbind() views."""
+        affine = None
+        if self.out_normalize:
+            lo, hi = 1.0 / self.max_depth, 1.0 / self.min_depth
+            affine = (lo, hi - lo)
+        disps, masks = zip(*pairs)
+        return list(hip.convex_upsample_many(list(disps), list(masks), ratio, affine=affine).unbind(0))
+
     def _cost(self, fmap1, frefs, disp, poses, K, reduce_mean):
         return hip.warp_cost(fmap1, frefs, disp, poses, K, depth_mode=self.depth_mode,
                              min_depth=self.min_depth, max_depth=self.max_depth,
@@ -204,7 +225,9 @@ class DepthPoseNet(nn.Module):
         poses = self.pose_head(pair).view(N, B, 6)
 
         disp = self.depth_head(fmap1, act_fn=torch.sigmoid)
-        inv_preds = [self.upsample_scaled(disp, self.upmask_net(fmap1), self.feat_ratio)]
+        # every kept (disp, mask) pair; upsampled together after the loop
+        # (upsample_many; eval: only the last one is upsampled)
+        up_pairs = [(disp, self.upmask_net(fmap1))]
         pose_preds = [poses]
 
         # join: the depth block (main stream) reads h_d/x_d; h_p/x_p only when the
@@ -246,7 +269,7 @@ class DepthPoseNet(nn.Module):
                                                             seq_len=self.seq_len)
                 keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
                 for k in keep:
-                    inv_preds.append(self.upsample_scaled(disps[k], masks[k], self.feat_ratio))
+                    up_pairs.append((disps[k], masks[k]))
                 return h_d, disps[-1]
 
             def pose_block(h_p):
@@ -278,5 +301,9 @@ class DepthPoseNet(nn.Module):
             disp, poses = disp_last, seq[-1]
 
         if not self.training:
-            return inv_preds[-1], pose_preds[-1].permute(1, 0, 2)          # [B,N,6]
+            return self.upsample_scaled(*up_pairs[-1], self.feat_ratio), pose_preds[-1].permute(1, 0, 2)  # [B,N,6]
+        if cuda and _UPSAMPLE_MANY[0]:
+            inv_preds = self.upsample_many(up_pairs, self.feat_ratio)
+        else:
+            inv_preds = [self.upsample_scaled(d, m, self.feat_ratio) for d, m in up_pairs]
         return inv_preds, torch.stack(pose_preds, 2).permute(1, 0, 2, 3)  # [B,N,n_pred,6]

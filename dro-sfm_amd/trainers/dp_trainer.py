@@ -574,7 +574,11 @@ class GraphedTrainStep:
         self.graphs = {}
         for f in flips:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            # thread_local: the RCCL watchdog thread queries the events of the
+            # warm-up steps' collectives; under the default (global) mode that
+            # query from another thread invalidated the capture (measured:
+            # hipErrorStreamCaptureUnsupported in the watchdog, then an abort)
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                 out = self._captured(f)
             self.graphs[f] = (g, out)
         torch.cuda.synchronize()

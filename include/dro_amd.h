@@ -169,6 +169,23 @@ int dro_convex_upsample_forward(const float* inv, const float* mask, int B, int 
 int dro_convex_upsample_backward(const float* inv, const float* mask, const float* grad_out,
                                  int B, int h, int w, int ratio, float mul,
                                  float* grad_inv, float* grad_mask, void* stream);
+/* n predictions (1..32) in one launch each way -- every kept prediction of a
+ * training step, which the losses read stacked (DepthPoseNet.py:180-181 per
+ * iteration, multiview_photometric_loss_mf.py / supervised_loss stacks):
+ *   inv[i] [B,1,h,w], mask[i] [B,9*r*r,h,w] (host pointer tables)
+ *   -> out [n,B,1,h*r,w*r] (add + mul * up, as the single call).
+ * Backward: grad_out [n,B,1,h*r,w*r] -> grad_mask[i] (required) and
+ * grad_inv[i] (table and entries nullable), both WRITTEN; deterministic (no
+ * atomics): the tap sums go through a workspace of
+ * dro_convex_upsample_many_workspace_bytes(n, B, h, w) bytes. */
+int dro_convex_upsample_many_forward(const float* const* inv, const float* const* mask, int n, int B,
+                                     int h, int w, int ratio, float add, float mul, float* out,
+                                     void* stream);
+size_t dro_convex_upsample_many_workspace_bytes(int n, int B, int h, int w);
+int dro_convex_upsample_many_backward(const float* const* inv, const float* const* mask,
+                                      const float* grad_out, int n, int B, int h, int w, int ratio,
+                                      float mul, float* const* grad_inv, float* const* grad_mask,
+                                      void* workspace, size_t workspace_bytes, void* stream);
 
 /* Bilinear 2x upsampling, align_corners=False (F.interpolate(scale_factor=2,
  * mode="bilinear") in networks/optim/extractor.py:91-97 of the reference).

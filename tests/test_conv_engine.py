@@ -201,6 +201,10 @@ MULTI_CASES = [
     ([("dense", 128)], 6, (3, 3), "tanh", 1.0, 17, 2, 12, 20),
     ([("slice", 128)], 576, (1, 1), None, 0.25, 4, 2, 24, 80),
     ([("dense", 37), ("slice", 11)], 45, (3, 3), "sigmoid", 1.0, 2, 3, 7, 13),
+    # the encoders' shapes: fnet layer1 at the KITTI metric batch (the bench
+    # roofline call), layer3 with 64-row output tiles
+    ([("dense", 64)], 64, (3, 3), None, 1.0, 1, 6, 48, 160),
+    ([("dense", 256)], 256, (3, 3), "relu", 1.0, 2, 2, 12, 40),
 ]
 
 

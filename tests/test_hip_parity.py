@@ -316,6 +316,52 @@ def test_convex_upsample_fused_scale(hip):
     assert rel(b.grad, a.grad) < 1e-6 and rel(bm.grad, am.grad) < 1e-6
 
 
+def test_convex_upsample_many(hip):
+    """convex_upsample_many (n predictions, one launch each way, the training
+    step's path): each slice of the stacked output and every input gradient vs
+    the fp64 oracle restatement (1e-4), one prediction without an inv gradient,
+    the backward bitwise deterministic (no atomics), and stacked_view returning
+    the stack itself for its unbind() views."""
+    g = torch.Generator().manual_seed(5)
+    n, B, h, w = 5, 2, 24, 80
+    lo, hi = 1.0 / 80.0, 1.0 / 0.5
+    invs = [torch.rand(B, 1, h, w, generator=g) for _ in range(n)]
+    masks = [torch.randn(B, 576, h, w, generator=g) for _ in range(n)]
+    G = torch.randn(n, B, 1, 8 * h, 8 * w, generator=g)
+    refs, rg = [], []
+    for i in range(n):
+        ic = invs[i].double().requires_grad_(i != 2)
+        mc = masks[i].double().requires_grad_(True)
+        r = lo + (hi - lo) * O.convex_upsample(ic, mc, 8)
+        (r * G[i].double()).sum().backward()
+        refs.append(r.detach())
+        rg.append((ic.grad, mc.grad))
+
+    def run():
+        di = [t.to(DEV).requires_grad_(i != 2) for i, t in enumerate(invs)]
+        dm = [t.to(DEV).requires_grad_(True) for t in masks]
+        out = hip.convex_upsample_many(di, dm, 8, affine=(lo, hi - lo))
+        views = list(out.unbind(0))
+        assert hip.stacked_view(views) is out
+        (hip.stacked_view(views) * G.to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        return out.detach(), [t.grad for t in di], [t.grad for t in dm]
+
+    out, gi, gm = run()
+    assert out.shape == (n, B, 1, 8 * h, 8 * w)
+    for i in range(n):
+        assert rel(out[i], refs[i]) < TOL
+        assert rel(gm[i], rg[i][1]) < TOL
+        if i == 2:
+            assert gi[i] is None
+        else:
+            assert rel(gi[i], rg[i][0]) < TOL
+    out2, gi2, gm2 = run()
+    assert torch.equal(out, out2)
+    assert all(torch.equal(a, b) for a, b in zip(gm, gm2))
+    assert all(a is None or torch.equal(a, b) for a, b in zip(gi, gi2))
+
+
 # ------------------------------------------------------------------ network level
 def _load_net(tag, version, mind, maxd):
     from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet

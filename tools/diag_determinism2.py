@@ -13,9 +13,10 @@ from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer
 from test_graph_step import _batch, _setup
 
 
-def run(backend, cudnn=True):
+def run(backend, cudnn=True, det=False):
     update.set_conv_backend(backend)
     torch.backends.cudnn.enabled = cudnn
+    torch.backends.cudnn.deterministic = det
     batch = _batch()
     K0 = batch["intrinsics"].clone()
     m = _setup()
@@ -51,7 +52,7 @@ def run(backend, cudnn=True):
         torch.cuda.synchronize()
         g = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
         res.append((float(loss.double()), g))
-    print(f"== backend={backend} cudnn={cudnn}: fwd max|diff| vs run0 {fwd}")
+    print(f"== backend={backend} cudnn={cudnn} deterministic={det}: fwd max|diff| vs run0 {fwd}")
     print("   losses " + " ".join(f"{l:.9g}" for l, _ in res))
     g0 = res[0][1]
     tot0 = torch.sqrt(sum((v.double() ** 2).sum() for v in g0.values()))
@@ -67,6 +68,10 @@ def run(backend, cudnn=True):
 
 
 if __name__ == "__main__":
-    run("hip")
-    run("hip", cudnn=False)
-    run("miopen")
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "det"):
+        run("hip", det=True)
+    if which == "all":
+        run("hip")
+        run("hip", cudnn=False)
+        run("miopen")

@@ -60,6 +60,8 @@ for step in "$@"; do
          run croof_mfma 300 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/croof_mfma" -o run -- python tools/conv_roofline.py run "$OUT/croof_mfma" &&
          run croof_table 60 python tools/conv_roofline.py table "$OUT/croof" --pmc-dirs "$OUT/croof_fetch" "$OUT/croof_write" "$OUT/croof_mfma" ;;
     v5iso) run py_view5iso 600 python tools/diag_train_steps.py view5iso ;;
+    roofonly) run roofonly 300 python bench.py --roofline-only ;;
+    envr:*) kv=${step#envr:}; run "roof_${kv%%=*}_${kv#*=}" 300 env "$kv" python bench.py --roofline-only ;;
     envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     benchmienc) run bench_miopen_enc 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --miopen-encoder-convs ;;
     photo) run photo_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/photo" -o run -- python tools/bench_photo.py --iters 20 ;;
@@ -69,6 +71,7 @@ for step in "$@"; do
     benchpem) run bench_pose_enc_main 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pose-encoder-main ;;
     benchns) run bench_native_strided 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --native-strided-convs ;;
     benchab20) run bench_ab 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
+    k:*) kk=${step#k:}; run "pytest_k_${kk//[^a-zA-Z0-9]/_}" 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider -k "$kk" ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
