@@ -475,6 +475,9 @@ def main():
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
     rank, world, local = init_distributed()
+    # DRO_BENCH_DEVICE: every rank on this device (an N > 1 rehearsal on a
+    # one-GPU box with DRO_DIST_BACKEND=gloo; never set by the driver)
+    local = int(os.environ.get("DRO_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     torch.manual_seed(42)
