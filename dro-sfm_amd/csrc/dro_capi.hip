@@ -52,7 +52,38 @@ int launch_zero(float* p, size_t n, hipStream_t s) {
   return launch_status("zero_fill_kernel launch failed");
 }
 
+// In-graph step timeline (tools/step_timeline.py): one thread records the
+// device's constant-rate real-time counter (wall_clock64, 100 MHz, common to
+// all XCDs) into slot `slot` when the stream reaches this launch.
+__global__ void timestamp_kernel(unsigned long long* __restrict__ buf, int slot) {
+  if (threadIdx.x == 0) buf[slot] = wall_clock64();
+}
+
 }  // namespace dro
+
+extern "C" int dro_timestamp(unsigned long long* buf, int slot, void* stream) {
+  if (!buf || slot < 0) {
+    dro::set_error("timestamp: NULL buffer or negative slot");
+    return DRO_E_NULL;
+  }
+  hipLaunchKernelGGL(dro::timestamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, buf, slot);
+  return dro::launch_status("timestamp_kernel launch failed");
+}
+
+extern "C" int dro_wall_clock_hz(long long* hz) {
+  if (!hz) {
+    dro::set_error("wall_clock_hz: NULL");
+    return DRO_E_NULL;
+  }
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) {
+    dro::set_error("wall_clock_hz: hipDeviceGetAttribute failed");
+    return DRO_E_MODE;
+  }
+  *hz = (long long)khz * 1000;
+  return DRO_OK;
+}
 
 extern "C" const char* dro_last_error(void) { return dro::g_last_error; }
 

@@ -36,6 +36,8 @@ def load():
     LL = ctypes.c_longlong
     _sig(lib.dro_last_error, restype=ctypes.c_char_p)
     _sig(lib.dro_abi_version)
+    _sig(lib.dro_timestamp, P, I, S)
+    _sig(lib.dro_wall_clock_hz, P)
     _sig(lib.dro_warp_cost_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, P, S)
     _sig(lib.dro_warp_cost_workspace_bytes, I, I, I, I, restype=Z)
     _sig(lib.dro_warp_cost_backward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I,
@@ -99,7 +101,7 @@ def load():
 
 # names every consumer can check against include/dro_amd.h
 EXPORTED = (
-    "dro_last_error", "dro_abi_version",
+    "dro_last_error", "dro_abi_version", "dro_timestamp", "dro_wall_clock_hz",
     "dro_warp_cost_forward", "dro_warp_cost_workspace_bytes", "dro_warp_cost_backward",
     "dro_plane_sweep_forward",
     "dro_photometric_workspace_bytes", "dro_photometric_forward", "dro_photometric_backward",

@@ -13,6 +13,7 @@ Anything else raises NotImplementedError rather than running a slow path.
 import torch
 
 from ..hip import photometric_loss, stacked_view
+from ..hip.timeline import stamp_grad
 from ..geometry.pose import kernel_pose_tensor
 from .loss_base import LossBase, ProgressiveScaling
 
@@ -60,7 +61,7 @@ class MultiViewPhotometricDecayLoss(LossBase):
         self._check_supported(image, inv_depths)
         n, N = self.n, len(context)
         ctx = torch.stack(list(context), 0)                                   # [N,B,3,H,W]
-        invs = stacked_view(inv_depths)                               # [n,B,1,H,W]
+        invs = stamp_grad(stacked_view(inv_depths), "bwd:loss_done")                               # [n,B,1,H,W]
         pose_t = kernel_pose_tensor(poses, n)                                 # [N,n,B,6|3x4]
         loss, metrics, sel = photometric_loss(
             image, ctx, invs, pose_t, K.float(), ref_K.float(), ssim_w=self.ssim_loss_weight,

@@ -34,6 +34,7 @@ import torch
 import torch.nn as nn
 
 from ... import hip
+from ...hip.timeline import stamp, stamp_grad
 from ..optim.extractor import ResNetEncoder
 from ..optim.update import (BasicUpdateBlockDepth, BasicUpdateBlockPose, DepthHead, PoseHead,
                             UpMaskNet)
@@ -177,6 +178,7 @@ class DepthPoseNet(nn.Module):
         B, N = target_image.shape[0], len(ref_imgs)
         C, hd, cd = self.foutput_dim, self.hdim, self.cdim
         K = intrinsics.float().contiguous()
+        stamp("fwd:begin")
 
         # context encoders first, on side streams (they depend on the images only)
         cuda = target_image.is_cuda
@@ -204,14 +206,17 @@ class DepthPoseNet(nn.Module):
                 ctx_d = self.cnet_depth(target_image)
                 h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
+                stamp("fwd:cnet_depth")
             with torch.cuda.stream(p_stream) if p_stream is not None else _null():
                 pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
                                    torch.stack(list(ref_imgs))], 2).flatten(0, 1)
                 ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
                 h_p, x_p = torch.split(ctx_p, [hd, cd], 1)
                 h_p, x_p = torch.tanh(h_p), torch.relu(x_p)
+                stamp("fwd:cnet_pose")
 
-        fmaps = self.fnet(torch.cat([target_image] + list(ref_imgs), 0))
+        fmaps = stamp_grad(self.fnet(torch.cat([target_image] + list(ref_imgs), 0)), "bwd:fnet_begin")
+        stamp("fwd:fnet")
         assert target_image.shape[2] // fmaps.shape[2] == self.feat_ratio
         h, w = fmaps.shape[2:]
         fmap1_raw, frefs_raw = torch.split(fmaps, [B, N * B], 0)
@@ -228,6 +233,7 @@ class DepthPoseNet(nn.Module):
         # every kept (disp, mask) pair; upsampled together after the loop
         # (upsample_many; eval: only the last one is upsampled)
         up_pairs = [(disp, self.upmask_net(fmap1))]
+        stamp("fwd:init_heads")
         pose_preds = [poses]
 
         # join: the depth block (main stream) reads h_d/x_d; h_p/x_p only when the
@@ -258,7 +264,7 @@ class DepthPoseNet(nn.Module):
                 with torch.cuda.stream(pside):
                     x_p = hip.grad_sink(x_p)
                     fmap1_p, frefs_p = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_raw)
-        for _ in range(self.iters):
+        for it in range(self.iters):
             disp = disp.detach()
             poses = poses.detach()
             frozen_poses, frozen_disp = poses, disp
@@ -270,7 +276,8 @@ class DepthPoseNet(nn.Module):
                 keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
                 for k in keep:
                     up_pairs.append((disps[k], masks[k]))
-                return h_d, disps[-1]
+                stamp(f"fwd:depth_iter{it}")
+                return stamp_grad(h_d, f"bwd:depth_iter{it}"), disps[-1]
 
             def pose_block(h_p):
                 # pose block over all N refs at once; depth frozen at this outer step
@@ -279,7 +286,8 @@ class DepthPoseNet(nn.Module):
                 h_p, seq = self.update_block_pose(h_p, pose_cost, frozen_poses.reshape(N * B, 6), x_p,
                                                   seq_len=self.seq_len)
                 seq = seq if self.inter_sup else [seq[-1]]
-                return h_p, [q.view(N, B, 6) for q in seq]
+                stamp(f"fwd:pose_iter{it}")
+                return stamp_grad(h_p, f"bwd:pose_iter{it}"), [q.view(N, B, 6) for q in seq]
 
             if pside is None:
                 h_d, disp_last = depth_block(h_d)
@@ -304,6 +312,7 @@ class DepthPoseNet(nn.Module):
             return self.upsample_scaled(*up_pairs[-1], self.feat_ratio), pose_preds[-1].permute(1, 0, 2)  # [B,N,6]
         if cuda and _UPSAMPLE_MANY[0]:
             inv_preds = self.upsample_many(up_pairs, self.feat_ratio)
+            stamp("fwd:upsample")
         else:
             inv_preds = [self.upsample_scaled(d, m, self.feat_ratio) for d, m in up_pairs]
         return inv_preds, torch.stack(pose_preds, 2).permute(1, 0, 2, 3)  # [B,N,n_pred,6]

@@ -487,10 +487,14 @@ class DataParallelTrainer:
                                               foreach=True, capturable=capturable)
 
     def _forward_backward(self, batch, **fwd_kw):
+        from ..hip.timeline import stamp, stamp_grad
+        stamp("step:begin")
         self.grads.zero()
         out = self.model(batch, **fwd_kw)
         loss = out["loss"]
-        loss.sum().backward()
+        stamp("fwd:loss")
+        stamp_grad(loss, "bwd:begin").sum().backward()
+        stamp("bwd:end")
         self.grads.finish()
         if isinstance(self.optimizer, FlatAdam) and self.optimizer.active is None \
                 and self.grads.active is not None:
@@ -498,8 +502,10 @@ class DataParallelTrainer:
         return loss.detach(), out.get("metrics", {})
 
     def _step_inner(self, batch, **fwd_kw):
+        from ..hip.timeline import stamp
         res = self._forward_backward(batch, **fwd_kw)
         self.optimizer.step()
+        stamp("step:end")
         return res
 
     def step(self, batch, **fwd_kw):

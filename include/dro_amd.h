@@ -52,6 +52,12 @@ extern "C" {
 const char* dro_last_error(void);
 int dro_abi_version(void);   /* 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
+/* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
+ * device's constant-rate real-time counter into buf[slot] when `stream`
+ * reaches this launch (capturable: replays overwrite the same slot). */
+int dro_timestamp(unsigned long long* buf, int slot, void* stream);
+int dro_wall_clock_hz(long long* hz);   /* that counter's rate */
+
 /* ------------------------------------------------------------------------
  * Inverse warp + feature cost.
  * Replaces DepthPoseNet.get_cost_each (networks/depth_pose/DepthPoseNet.py:76-96)

@@ -334,6 +334,11 @@ def test_weight_split_exact(hip):
     (1, 6, 64, 47, 81, 7, 2, 3, False, None),        # cnet_pose stem, odd input size
     (2, 20, 24, 17, 23, 3, 2, 1, True, "relu"),      # odd sizes, bias + relu forward
     (2, 16, 40, 12, 20, 3, 1, 0, True, None),        # stride 1, no padding
+    # the ScanNet view5 fixture's fnet (5 frames of 64x96)
+    (5, 3, 64, 64, 96, 7, 2, 3, False, None),
+    (5, 64, 128, 16, 24, 3, 2, 1, False, None),
+    (5, 64, 128, 16, 24, 1, 2, 0, False, None),
+    (5, 128, 256, 8, 12, 3, 2, 1, False, None),
 ])
 def test_conv2d_strided(hip, case):
     """hip.conv2d_strided (dro_conv2d_strided_*: flattened implicit GEMM with
