@@ -216,35 +216,43 @@ def _mark_direct(params):
 
 
 _SIDE = {}
-_JOIN = [False]
+_JOINS = {}          # forking stream -> its side stream, joined at the end of this backward
 _USE_SIDE = [False]
 
 
 def set_weight_grad_stream(side):
     """Run the direct weight-gradient kernels on a side stream (True) or in order
     on the current stream (False, default: measured faster under hipGraph replay,
-    where cross-stream edges add ~4 us bubbles per fork)."""
+    where cross-stream edges add ~4 us bubbles per fork).  Each forking stream
+    (the main chain, the pose block's stream) gets its own side stream."""
     _USE_SIDE[0] = bool(side)
 
 
-def _fork_side():
-    """The weight-gradient stream: the current stream, or a side stream forked
-    from it whose join back is queued once per backward pass as an engine final
-    callback."""
-    main = torch.cuda.current_stream()
+def _fork_side(main=None):
+    """The weight-gradient stream: `main` (default: the current stream), or a
+    side stream forked from it; every side stream forked during a backward pass
+    is joined back into its forking stream by one engine final callback."""
+    main = torch.cuda.current_stream() if main is None else main
     if not _USE_SIDE[0]:
         return main
-    side = _SIDE.get(main.device)
+    key = (main.device, main.stream_id)
+    side = _SIDE.get(key)
     if side is None:
-        side = _SIDE[main.device] = torch.cuda.Stream(device=main.device)
+        side = _SIDE[key] = torch.cuda.Stream(device=main.device)
     side.wait_stream(main)
-    if not _JOIN[0]:
-        _JOIN[0] = True
-
+    if not _JOINS:
         def join():
-            main.wait_stream(side)
-            _JOIN[0] = False
+            # into the forking stream AND the stream the backward returns on
+            # (the engine may already have synchronised the forking stream
+            # with it; work forked after that point would be left unjoined)
+            cur = torch.cuda.current_stream()
+            for m, sd in list(_JOINS.values()):
+                m.wait_stream(sd)
+                if cur != m:
+                    cur.wait_stream(sd)
+            _JOINS.clear()
         torch.autograd.Variable._execution_engine.queue_callback(join)
+    _JOINS[key] = (main, side)
     return side
 
 
@@ -328,7 +336,7 @@ def flush_param_grads(param):
     if not keys:
         return None
     items = [_PENDING.pop(k) for k in keys]
-    return _launch_weight_grads(items, items[0][2][0])
+    return _launch_weight_grads(items, _fork_side(items[0][2][0]))
 
 
 def flush_weight_grads(stream=None):
