@@ -336,7 +336,9 @@ def flush_param_grads(param):
     if not keys:
         return None
     items = [_PENDING.pop(k) for k in keys]
-    return _launch_weight_grads(items, _fork_side(items[0][2][0]))
+    # on the stream of the first use (a side stream here, forked from the
+    # parameter hook, crashed the graph-captured step with SIGSEGV: round 3)
+    return _launch_weight_grads(items, items[0][2][0])
 
 
 def flush_weight_grads(stream=None):
