@@ -218,6 +218,15 @@ def _mark_direct(params):
 _SIDE = {}
 _JOINS = {}          # forking stream -> its side stream, joined at the end of this backward
 _USE_SIDE = [False]
+_FORK_ROLES = {}     # stream id of a persistent model stream -> its own side-stream key
+
+
+def register_fork_stream(stream):
+    """A persistent stream of the model (DepthPoseNet's pose-block stream)
+    whose backward work forks weight gradients onto a side stream of its own.
+    Every other stream (the main chain: a warm-up stream, then torch's
+    capture stream) shares one side stream, created before capture."""
+    _FORK_ROLES[stream.stream_id] = ("model", stream.stream_id)
 
 
 def set_weight_grad_stream(side):
@@ -235,7 +244,10 @@ def _fork_side(main=None):
     main = torch.cuda.current_stream() if main is None else main
     if not _USE_SIDE[0]:
         return main
-    key = (main.device, main.stream_id)
+    # keyed by role, not by stream: the main chain runs on a different stream
+    # in the eager warm-up than under capture, and a stream created during
+    # capture crashed the captured step
+    key = (main.device, _FORK_ROLES.get(main.stream_id, "main"))
     side = _SIDE.get(key)
     if side is None:
         side = _SIDE[key] = torch.cuda.Stream(device=main.device)
@@ -254,6 +266,19 @@ def _fork_side(main=None):
         torch.autograd.Variable._execution_engine.queue_callback(join)
     _JOINS[key] = (main, side)
     return side
+
+
+def join_weight_grad_streams():
+    """Make the CURRENT stream wait for every weight-gradient side stream used
+    since the last join.  Call on the thread that ran backward(), right after
+    it: the engine's final callback may run on an autograd worker thread whose
+    current stream is not the caller's (under graph capture that left the side
+    stream unjoined and capture_end crashed)."""
+    cur = torch.cuda.current_stream()
+    for (dev, _), sd in _SIDE.items():
+        if dev == cur.device:
+            cur.wait_stream(sd)
+    _JOINS.clear()
 
 
 def _on_side(side, tensors):
@@ -336,8 +361,9 @@ def flush_param_grads(param):
     if not keys:
         return None
     items = [_PENDING.pop(k) for k in keys]
-    # on the stream of the first use (a side stream here, forked from the
-    # parameter hook, crashed the graph-captured step with SIGSEGV: round 3)
+    # on the stream of the first use.  Forked onto a side stream here (from
+    # the parameter hook), the graph-captured step crashed in capture_end
+    # (SIGSEGV; eager ran, at 36-50 ms/step): round 3, not adopted
     return _launch_weight_grads(items, items[0][2][0])
 
 

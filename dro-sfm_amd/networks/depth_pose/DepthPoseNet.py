@@ -99,6 +99,8 @@ def _side_streams(device):
     ss = _SIDE_STREAMS.get(device)
     if ss is None:
         ss = _SIDE_STREAMS[device] = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
+        for st in ss:
+            hip.conv.register_fork_stream(st)
     return ss
 
 

@@ -494,6 +494,9 @@ class DataParallelTrainer:
         loss = out["loss"]
         stamp("fwd:loss")
         stamp_grad(loss, "bwd:begin").sum().backward()
+        if self.grads.flat.is_cuda:
+            from ..hip.conv import join_weight_grad_streams
+            join_weight_grad_streams()              # weight-gradient side streams, if any
         stamp("bwd:end")
         self.grads.finish()
         if isinstance(self.optimizer, FlatAdam) and self.optimizer.active is None \
