@@ -410,7 +410,7 @@ def main():
     ap.add_argument("--conv-backend", choices=("hip", "miopen"), default="hip",
                     help="update-block convolutions: native f32-MFMA engine or MIOpen (A/B only)")
     ap.add_argument("--wgrad-side-stream", action="store_true",
-                    help="direct weight-gradient kernels on a side stream (A/B)")
+                    help="per-call weight-gradient kernels on a side stream (A/B; eager only)")
     ap.add_argument("--no-direct-wgrad", action="store_true",
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",

@@ -230,11 +230,16 @@ def register_fork_stream(stream):
 
 
 def set_weight_grad_stream(side):
-    """Run the direct weight-gradient kernels on a side stream (True) or in order
-    on the current stream (False, default: measured faster under hipGraph replay,
-    where cross-stream edges add ~4 us bubbles per fork).  Each forking stream
-    (the main chain, the pose block's stream) gets its own side stream."""
+    """Run the per-call (non-batched) direct weight-gradient kernels on a side
+    stream (True) or in order on the current stream (False, default: measured
+    faster under hipGraph replay, where cross-stream edges add ~4 us bubbles
+    per fork).  Eager only: GraphedTrainStep refuses to capture with it on
+    (round 3: side-stream weight gradients crashed capture_end)."""
     _USE_SIDE[0] = bool(side)
+
+
+def weight_grad_stream_enabled():
+    return _USE_SIDE[0]
 
 
 def _fork_side(main=None):

@@ -566,6 +566,10 @@ class GraphedTrainStep:
 
     def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True,
                  reduce_in_graph=False):
+        from ..hip.conv import weight_grad_stream_enabled
+        if weight_grad_stream_enabled():
+            raise RuntimeError("GraphedTrainStep: weight-gradient side streams (hip.conv.set_weight_grad_stream) "
+                               "are eager-only")
         self.tr = trainer
         # collectives outside the graph when there is an exchange at all
         self.outside = trainer.grads.reduce and not reduce_in_graph
