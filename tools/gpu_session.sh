@@ -63,6 +63,7 @@ for step in "$@"; do
     dp2) run bench_dp2_gloo_onegpu 600 env DRO_DIST_BACKEND=gloo DRO_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 10 --warmup 3 --no-roofline ;;
     sidediag) run side_eager 300 env PYTHONFAULTHANDLER=1 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --wgrad-side-stream --eager &&
               run side_graph 300 env PYTHONFAULTHANDLER=1 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
+    profns) run rocprof_ns 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profns" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --native-strided-convs ;;
     roofonly) run roofonly 300 python bench.py --roofline-only ;;
     envr:*) kv=${step#envr:}; run "roof_${kv%%=*}_${kv#*=}" 300 env "$kv" python bench.py --roofline-only ;;
     envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
