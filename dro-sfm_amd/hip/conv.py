@@ -42,6 +42,7 @@ afresh) and the split buffers are saved for the backward.
 """
 import contextlib
 import ctypes
+import os
 
 import torch
 
@@ -284,6 +285,10 @@ def join_weight_grad_streams():
         if dev == cur.device:
             cur.wait_stream(sd)
     _JOINS.clear()
+    fl = _FLUSH.get(cur.device)
+    if fl is not None:
+        cur.wait_stream(fl)
+    _INFLIGHT.clear()
 
 
 def _on_side(side, tensors):
@@ -366,10 +371,7 @@ def flush_param_grads(param):
     if not keys:
         return None
     items = [_PENDING.pop(k) for k in keys]
-    # on the stream of the first use.  Forked onto a side stream here (from
-    # the parameter hook), the graph-captured step crashed in capture_end
-    # (SIGSEGV; eager ran, at 36-50 ms/step): round 3, not adopted
-    return _launch_weight_grads(items, items[0][2][0])
+    return _launch_weight_grads(items, _flush_stream(items[0][2][0]))
 
 
 def flush_weight_grads(stream=None):
@@ -383,16 +385,55 @@ def flush_weight_grads(stream=None):
     _launch_weight_grads(items, stream or torch.cuda.current_stream())
 
 
+_FLUSH = {}          # device -> the weight-gradient flush stream (set_flush_stream)
+_USE_FLUSH = [os.environ.get("DRO_WGRAD_FLUSH_STREAM", "0") == "1"]
+_INFLIGHT = []       # uses launched on the flush stream, released at the join
+
+
+def set_flush_stream(enabled):
+    """Batched weight gradients (flushed from the parameter hooks as the last
+    use of a weight is back-propagated) on their own stream, so the
+    data-gradient chain -- iteration 0 of the update blocks, the heads, the
+    encoders -- does not wait for them (profiles/r3_step_timeline.txt:
+    iteration 0's backward 3.7 ms against 1.4 ms for iteration 1, the
+    difference being these launches).  Their operands stay referenced until
+    join_weight_grad_streams() (no record_stream).  Off by default
+    (DRO_WGRAD_FLUSH_STREAM=1): captured and replayed it is correct (graph,
+    DP and metric-config parity tests green) but slower, 19.7-19.9 vs
+    16.3-16.4 ms/step A/B on one box -- the weight-gradient kernels (240-block
+    grids) then share the chip with both update-block chains and the
+    encoders' data gradients, and the pose chain's iteration-1 backward
+    stretched from 1.5 to 5.1 ms (profiles/r3_step_timeline_flush_stream.txt)."""
+    _USE_FLUSH[0] = bool(enabled)
+
+
+def _flush_stream(use_stream):
+    if not _USE_FLUSH[0]:
+        return use_stream
+    dev = use_stream.device
+    st = _FLUSH.get(dev)
+    if st is None:
+        if torch.cuda.is_current_stream_capturing():
+            return use_stream            # never create a stream inside a capture
+        st = _FLUSH[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
 def _launch_weight_grads(items, stream):
     lib = _lib.load()
+    side = any(s != stream for _, _, streams in items for s in streams)
     for _, uses, streams in items:       # uses queued from other streams (concurrent blocks)
         for s in streams:
             if s != stream:
                 stream.wait_stream(s)
-                for srcs, dout, y in uses:
-                    for x in (*srcs, dout, y):
-                        if x is not None:
-                            x.record_stream(stream)
+    if side and stream in _FLUSH.values():
+        _INFLIGHT.append(items)          # operands live until the join
+    elif side:
+        for _, uses, streams in items:
+            for srcs, dout, y in uses:
+                for x in (*srcs, dout, y):
+                    if x is not None:
+                        x.record_stream(stream)
     with torch.cuda.stream(stream):
         for meta, uses, _ in items:
             B, H, W, Cin, Cout, KH, KW, act, alpha, gw, gb, nsrc = meta

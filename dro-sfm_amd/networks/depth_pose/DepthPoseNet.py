@@ -205,14 +205,14 @@ class DepthPoseNet(nn.Module):
                     t.record_stream(st)
         if self.iters > 0:
             with torch.cuda.stream(d_stream) if d_stream is not None else _null():
-                ctx_d = self.cnet_depth(target_image)
+                ctx_d = stamp_grad(self.cnet_depth(target_image), "bwd:cnet_depth_begin")
                 h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
                 stamp("fwd:cnet_depth")
             with torch.cuda.stream(p_stream) if p_stream is not None else _null():
                 pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
                                    torch.stack(list(ref_imgs))], 2).flatten(0, 1)
-                ctx_p = self.cnet_pose(pairs)                 # [N*B, hd+cd, h, w]
+                ctx_p = stamp_grad(self.cnet_pose(pairs), "bwd:cnet_pose_begin")   # [N*B, hd+cd, h, w]
                 h_p, x_p = torch.split(ctx_p, [hd, cd], 1)
                 h_p, x_p = torch.tanh(h_p), torch.relu(x_p)
                 stamp("fwd:cnet_pose")
@@ -231,7 +231,7 @@ class DepthPoseNet(nn.Module):
         pair = torch.cat([fmap1.unsqueeze(0).expand(N, B, C, h, w), frefs], 2).view(N * B, 2 * C, h, w)
         poses = self.pose_head(pair).view(N, B, 6)
 
-        disp = self.depth_head(fmap1, act_fn=torch.sigmoid)
+        disp = stamp_grad(self.depth_head(fmap1, act_fn=torch.sigmoid), "bwd:init_depth_head")
         # every kept (disp, mask) pair; upsampled together after the loop
         # (upsample_many; eval: only the last one is upsampled)
         up_pairs = [(disp, self.upmask_net(fmap1))]

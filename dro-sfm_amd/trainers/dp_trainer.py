@@ -155,10 +155,15 @@ class GradBuckets:
         if self.flat.is_cuda:
             # the hook runs on the stream that produced this gradient (the context
             # encoders' backward runs on side streams), the in-place weight
-            # gradient went to `wrote`: remember both for the bucket
-            self._bstreams[b].add(torch.cuda.current_stream())
+            # gradient went to `wrote`: remember both for the bucket.  A `wrote`
+            # other than the hook's stream (the weight-gradient flush stream)
+            # must not be waited for here: that would put the data-gradient
+            # chain behind the weight gradients again; the collective waits for
+            # it instead, and the step's end joins it
+            cur = torch.cuda.current_stream()
+            self._bstreams[b].add(cur)
             if wrote is not None:
-                self._bstreams[b].add(wrote)
+                (self._bstreams[b] if wrote == cur else self._bside[b]).add(wrote)
         self._left[b] -= 1
         if self._left[b] == 0:
             self._complete(b)
@@ -188,10 +193,28 @@ class GradBuckets:
             self._next += 1
             self.issued.append(b)
             if self.reduce and not self.suspend:
+                side = self._bside[b] if self.flat.is_cuda else ()
+                if side:
+                    # in-place weight gradients from another stream: issue from a
+                    # comm stream that waits for them and for the gather
+                    comm = self._comm_stream()
+                    comm.wait_event(self._events[b])
+                    for st in side:
+                        comm.wait_stream(st)
+                    with torch.cuda.stream(comm):
+                        self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
+                                                             group=self.group, async_op=True))
+                    continue
                 if self._events[b] is not None:
                     torch.cuda.current_stream().wait_event(self._events[b])
                 self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
                                                      group=self.group, async_op=True))
+
+    def _comm_stream(self):
+        st = getattr(self, "_comm", None)
+        if st is None:
+            st = self._comm = torch.cuda.Stream(device=self.flat.device)
+        return st
 
     def _gather(self, b):
         """Copy bucket b's adopted gradients into the flat buffer (one launch).
@@ -225,6 +248,7 @@ class GradBuckets:
             self._events = [None] * len(self.buckets)
             self._next = 0
             self._bstreams = [set() for _ in self.buckets]
+            self._bside = [set() for _ in self.buckets]
             for ps in self._adopt:
                 for p in ps:
                     p.grad = None

@@ -62,6 +62,9 @@ def main():
             ("loss backward", "bwd:begin", "bwd:loss_done"),
             ("update blocks (bwd, depth chain)", "bwd:loss_done", "bwd:depth_iter0"),
             ("update blocks (bwd, pose chain)", "bwd:loss_done", "bwd:pose_iter0"),
+            ("to the initial depth head's backward", "bwd:begin", "bwd:init_depth_head"),
+            ("cnet_depth backward begins", "bwd:begin", "bwd:cnet_depth_begin"),
+            ("cnet_pose backward begins", "bwd:begin", "bwd:cnet_pose_begin"),
             ("fnet backward begins", "bwd:begin", "bwd:fnet_begin"),
             ("encoders (bwd) to the end of backward", "bwd:fnet_begin", "bwd:end"),
             ("all-reduce (world 1: none) + Adam", "bwd:end", "step:end")]
