@@ -413,6 +413,8 @@ def main():
                     help="per-call weight-gradient kernels on a side stream (A/B; eager only)")
     ap.add_argument("--no-direct-wgrad", action="store_true",
                     help="weight gradients through autograd instead of in place on a side stream (A/B)")
+    ap.add_argument("--depth-encoder-main", action="store_true",
+                    help="cnet_depth on the main stream instead of the pose block's stream (A/B)")
     ap.add_argument("--concurrent-encoders", action="store_true",
                     help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
     ap.add_argument("--pose-encoder-main", action="store_true",
@@ -464,6 +466,7 @@ def main():
     _dpn.set_concurrent_encoders(args.concurrent_encoders)
     _dpn.set_concurrent_blocks(not args.serial_blocks)
     _dpn.set_pose_encoder_stream(not args.pose_encoder_main)
+    _dpn.set_depth_encoder_pose_stream(not args.depth_encoder_main)
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_fused_batchnorm(not args.no_fused_bn)
     _extractor.set_native_maxpool(not args.aten_maxpool)
@@ -545,6 +548,8 @@ def main():
                    "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
                    "update_blocks": "serial" if args.serial_blocks else "concurrent streams",
                    "pose_encoder": "main stream" if (args.pose_encoder_main or args.serial_blocks) else "pose-block stream",
+                   "depth_encoder": "main stream" if (args.depth_encoder_main or args.pose_encoder_main
+                                                      or args.serial_blocks) else "pose-block stream, first",
                    "grad_sinks": not args.no_grad_sinks,
                    "split_engine": args.split_engine,
                    "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",

@@ -59,6 +59,18 @@ _SIDE_STREAMS = {}
 
 
 _UPSAMPLE_MANY = [os.environ.get("DRO_UPSAMPLE_MANY", "1") != "0"]
+_DEPTH_ENCODER_POSE_STREAM = [os.environ.get("DRO_CNET_DEPTH_POSE_STREAM", "1") != "0"]
+
+
+def set_depth_encoder_pose_stream(enabled):
+    """cnet_depth on the pose block's stream, ahead of cnet_pose (default), or
+    on the main stream.  On the pose stream its forward runs beside fnet (the
+    depth block waits for it through an event) and its backward beside fnet's
+    backward: the in-graph timeline put it after fnet's backward on the main
+    stream (1.3 ms on the critical path, profiles/r3_step_timeline.txt).
+    Measured A/B on one box: 14.92-15.15 vs 16.38-17.16 ms/step
+    (profiles/r3_step_timeline_cnet_depth_pose_stream.txt)."""
+    _DEPTH_ENCODER_POSE_STREAM[0] = bool(enabled)
 
 
 def set_upsample_many(enabled):
@@ -191,11 +203,17 @@ class DepthPoseNet(nn.Module):
         # depth block); cnet_pose: on the pose block's stream (no join needed),
         # or beside fnet without concurrent blocks
         d_stream = p_stream = None
+        d_event = None
         if self.iters > 0 and cuda:
             if _CONCURRENT[0]:
                 d_stream = _side_streams(target_image.device)[0]
             if pside is not None and _POSE_ENCODER_SIDE[0]:
                 p_stream = pside
+                if _DEPTH_ENCODER_POSE_STREAM[0]:
+                    # cnet_depth first on the pose block's stream (its backward
+                    # then runs there too, beside fnet's); the depth block
+                    # waits for cnet_depth only, through an event
+                    d_stream = pside
             elif _CONCURRENT[0]:
                 p_stream = _side_streams(target_image.device)[1]
             main = torch.cuda.current_stream(target_image.device)
@@ -209,6 +227,9 @@ class DepthPoseNet(nn.Module):
                 h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
                 stamp("fwd:cnet_depth")
+                if d_stream is not None and d_stream is p_stream:
+                    d_event = torch.cuda.Event()
+                    d_event.record(d_stream)
             with torch.cuda.stream(p_stream) if p_stream is not None else _null():
                 pairs = torch.cat([target_image.unsqueeze(0).expand(N, *target_image.shape),
                                    torch.stack(list(ref_imgs))], 2).flatten(0, 1)
@@ -242,7 +263,10 @@ class DepthPoseNet(nn.Module):
         # pose block runs on the main stream too
         main = torch.cuda.current_stream(target_image.device) if cuda else None
         if d_stream is not None:
-            main.wait_stream(d_stream)
+            if d_event is not None:
+                main.wait_event(d_event)
+            else:
+                main.wait_stream(d_stream)
             for t in (h_d, x_d):
                 t.record_stream(main)
         if p_stream is not None and p_stream is not pside:

@@ -64,6 +64,7 @@ for step in "$@"; do
     sidediag) run side_eager 300 env PYTHONFAULTHANDLER=1 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --wgrad-side-stream --eager &&
               run side_graph 300 env PYTHONFAULTHANDLER=1 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
     profns) run rocprof_ns 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profns" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --native-strided-convs ;;
+    tlcd) run step_timeline_cnetd 300 env DRO_CNET_DEPTH_POSE_STREAM=1 python tools/step_timeline.py ;;
     roofonly) run roofonly 300 python bench.py --roofline-only ;;
     envr:*) kv=${step#envr:}; run "roof_${kv%%=*}_${kv#*=}" 300 env "$kv" python bench.py --roofline-only ;;
     envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
