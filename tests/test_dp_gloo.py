@@ -121,7 +121,8 @@ def test_two_rank_gloo_matches_single_process(outside):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_missing_gradient_on_one_rank():
+@pytest.mark.parametrize("outside", [False, True])
+def test_two_rank_gloo_missing_gradient_on_one_rank(outside):
     """A parameter whose gradient arrives on one rank only (or on neither) on
     some steps: every bucket is still all-reduced exactly once per step on
     every rank, in the same order -- ranks stay identical and equal to one
@@ -130,7 +131,9 @@ def test_two_rank_gloo_missing_gradient_on_one_rank():
     port = _free_port()
     with mp.Manager() as mgr:
         out = mgr.dict()
-        mp.spawn(_worker, args=(2, port, steps, out, True), nprocs=2, join=True)
+        # outside=True: the exchange after backward, one all-reduce per run of
+        # active parameters (`dead` sits between them here)
+        mp.spawn(_worker, args=(2, port, steps, out, True, outside), nprocs=2, join=True)
         res = dict(out)
     (p0, nb0, _), (p1, _, _) = res[0], res[1]
     assert nb0 > 4, "expected one bucket per parameter"
