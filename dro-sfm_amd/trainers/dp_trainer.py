@@ -298,10 +298,8 @@ class GradBuckets:
         if not self.reduce:
             return
         runs = getattr(self, "_runs", None) or [[0, self.flat.numel()]]
-        works = [dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                 for lo, hi in runs]
-        for w in works:
-            w.wait()
+        for lo, hi in runs:
+            dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
         if self.world > 1:
             self.flat.div_(self.world)
 
