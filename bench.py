@@ -333,8 +333,8 @@ def roofline_conv(device, iters=50, traffic_file=None):
             tf = json.load(f)
         if tf.get("kernels") == kernels:       # measured on this very launch sequence
             traffic = tf.get("hbm_bytes_per_launch")
-    return {"bound": "mfma", "kernel": kernels[0] + " + " + kernels[1] + "Q> (fnet layer1 3x3 weight gradient, "
-            "B=6 48x160, 64 -> 64)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
+    return {"bound": "mfma", "kernel": kernels[0] + " + " + kernels[1].rstrip("<") +
+            " (fnet layer1 3x3 weight gradient, B=6 48x160, 64 -> 64)", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
             "flops_per_launch": int(flops), "avg_launch_us": round(us, 2), "launches": iters,
             "algorithmic_bytes_per_launch": int(4 * (x.numel() + gout.numel() + gw.numel()))}
@@ -377,7 +377,10 @@ def cpu_baseline(model, budget_s=12.0, max_steps=40):
                       f"N={NREF}, {VERSION}, CPU oracle oracle/dro_oracle.py, torch {torch.__version__}",
             "sec_per_step": round(sec, 3), "sec_per_step_min_max": [round(min(times), 3), round(max(times), 3)],
             "cpu_model": _cpu_model(), "cpu_capability": torch.backends.cpu.get_cpu_capability(),
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(),
+            "cores_note": f"cores = the CPUs in this process's affinity mask ({threads}; OMP_NUM_THREADS "
+                          f"{os.environ.get('OMP_NUM_THREADS', 'unset')}), which the GPU box sets; the host "
+                          f"has {os.cpu_count()}"}
 
 
 def _cpu_model():
@@ -390,6 +393,44 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(argv, gpus, port):
+    """The torch.distributed.run command that starts `gpus` ranks of this script
+    (one process per GPU; each rank pins cuda:LOCAL_RANK)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch_ranks(argv, gpus):
+    """`python bench.py --gpus N` without torchrun's env starts N ranks itself
+    (the reference's `mpirun -np NGPUS`, run.sh:4; its dormant DP at
+    horovod_trainer.py:66-69, model_wrapper.py:818-822).  Runs BEFORE anything
+    touches the GPU in this process: the ranks are children (no exec), and this
+    process exits with their launcher's status.  Returns None when this process
+    is itself a rank (or N == 1)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != gpus:
+            print(f"[bench] --gpus {gpus} but WORLD_SIZE={env_world}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if gpus <= 1:
+        return None
+    import subprocess
+    cmd = launch_command(argv, gpus, _free_port())
+    print(f"[bench] launching {gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ))
 
 
 # ----------------------------------------------------------------------------- main
@@ -446,6 +487,9 @@ def main():
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
     args = ap.parse_args()
+    rc = maybe_launch_ranks(sys.argv[1:], args.gpus)
+    if rc is not None:
+        sys.exit(rc)
     set_workload(args.workload)
     if args.batch is None:
         args.batch = WL["batch"]
@@ -477,12 +521,14 @@ def main():
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
-    rank, world, local = init_distributed()
     # DRO_BENCH_DEVICE: every rank on this device (an N > 1 rehearsal on a
     # one-GPU box with DRO_DIST_BACKEND=gloo; never set by the driver)
-    local = int(os.environ.get("DRO_BENCH_DEVICE", local))
+    local = int(os.environ.get("DRO_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    rank, world, _ = init_distributed()
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the process group has {world} ranks")
     torch.manual_seed(42)
     model = build_model(device, args.flip_prob)
     model.seed(42 + rank)

@@ -35,13 +35,41 @@ def _as_uint8(img):
     return torch.from_numpy(np.ascontiguousarray(a))
 
 
+def _depth_map(d):
+    """A decoded depth map (np [h,w] or [h,w,1]) as float32 [h, w]."""
+    a = np.asarray(d, dtype=np.float32)
+    if a.ndim == 3:
+        a = a[..., 0]
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def nearest_indices(src, dst):
+    """cv2.resize(..., INTER_NEAREST) source index per destination index along one
+    axis (OpenCV resizeNN: ifx = 1 / (dst / src) in double, floor(x * ifx),
+    clamped to src - 1)."""
+    ifx = 1.0 / (float(dst) / float(src))
+    return np.minimum(np.floor(np.arange(dst, dtype=np.float64) * ifx).astype(np.int64), src - 1)
+
+
+def resize_depth_nearest(depth, shape):
+    """augmentations.resize_depth (augmentations.py:47-65: cv2 INTER_NEAREST to
+    dsize=shape[::-1]) + ToTensor for a batch of depth maps of one raw size on
+    the GPU: [B, h, w] -> [B, 1, H, W], a pure gather (bit-exact)."""
+    H, W = shape
+    h, w = depth.shape[-2:]
+    iy = torch.from_numpy(nearest_indices(h, H)).to(depth.device, non_blocking=True)
+    ix = torch.from_numpy(nearest_indices(w, W)).to(depth.device, non_blocking=True)
+    return depth.index_select(-2, iy).index_select(-1, ix).unsqueeze(1)
+
+
 def collate_decoded(samples):
     """Collate reference samples built WITHOUT data_transform: 'rgb' and
     'rgb_context' (PIL images or uint8 HWC arrays) become lists of uint8
     [H0, W0, 3] tensors (pinned when a GPU is present; per sample, raw sizes
     may differ); 'intrinsics' float32 [B, 3, 3]; 'pose_context' a list over
-    references of float32 [B, 4, 4]; 'depth' float32 [B, 1, H, W] when
-    present; other keys as lists."""
+    references of float32 [B, 4, 4]; 'depth' a list of float32 [h0, w0] raw
+    maps ('depth_context' a list over references of such lists) when present;
+    other keys as lists."""
     pin = torch.cuda.is_available()
     out = {}
     rgb = [_as_uint8(s["rgb"]) for s in samples]
@@ -58,8 +86,11 @@ def collate_decoded(samples):
         out["pose_context"] = [torch.stack([torch.as_tensor(np.asarray(s["pose_context"][j]), dtype=torch.float32)
                                             for s in samples]) for j in range(n)]
     if "depth" in samples[0]:
-        out["depth"] = torch.stack([torch.as_tensor(np.asarray(s["depth"]), dtype=torch.float32).reshape(
-            1, *np.asarray(s["depth"]).shape[-2:]) for s in samples])
+        # per sample, at the raw size (drives differ); resized on the GPU
+        out["depth"] = [_depth_map(s["depth"]) for s in samples]
+    if "depth_context" in samples[0]:
+        n = len(samples[0]["depth_context"])
+        out["depth_context"] = [[_depth_map(s["depth_context"][j]) for s in samples] for j in range(n)]
     for k in samples[0]:
         if k not in out:
             out[k] = [s[k] for s in samples]
@@ -110,8 +141,23 @@ class GPUTrainPipeline:
         if "pose_context" in host:
             out["pose_context"] = [p.to(dev, non_blocking=True) for p in host["pose_context"]]
         if "depth" in host:
-            out["depth"] = host["depth"].to(dev, non_blocking=True)
+            out["depth"] = self._depths(host["depth"])
+        if "depth_context" in host:
+            out["depth_context"] = [self._depths(d) for d in host["depth_context"]]
         return out
+
+    def _depths(self, maps):
+        """Per-sample raw depth maps -> [B, 1, H, W] on the device (nearest
+        neighbour, resize_sample's depth branch, augmentations.py:135-143),
+        one gather per run of equal raw sizes."""
+        dev = self.device
+        maps = [m.to(dev, non_blocking=True) for m in maps]
+        parts, start = [], 0
+        for b in range(1, len(maps) + 1):
+            if b == len(maps) or maps[b].shape != maps[start].shape:
+                parts.append(resize_depth_nearest(torch.stack(maps[start:b]), self.image_shape))
+                start = b
+        return torch.cat(parts) if len(parts) > 1 else parts[0]
 
 
 def gpu_data_loader(dataset, batch_size, image_shape, jittering=(0.2, 0.2, 0.2, 0.05), num_workers=4,

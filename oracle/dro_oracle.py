@@ -625,6 +625,29 @@ def color_jitter_pil(a, order, factors, hue):
     return np.asarray(img)
 
 
+def resize_depth_cv2_nearest(depth, shape):
+    """augmentations.resize_depth (datasets/augmentations.py:47-65):
+    cv2.resize(depth, dsize=shape[::-1], interpolation=cv2.INTER_NEAREST) then
+    np.expand_dims(..., 2).  OpenCV (opencv-python-headless, unpinned in the
+    reference's docker/Dockerfile:84; absent here) resizeNN: fx = dsize.width /
+    src.width in double, ifx = 1 / fx, x_ofs[x] = min(cvFloor(x * ifx), src.width - 1),
+    the same per row.  Scalar loops over a numpy [h, w] array; parity unpinned
+    (no cv2 in this container or on the box)."""
+    import numpy as np
+    d = np.asarray(depth)
+    if d.ndim == 3:
+        d = d[..., 0]
+    h, w = d.shape
+    H, W = shape
+    ifx, ify = 1.0 / (W / w), 1.0 / (H / h)
+    out = np.empty((H, W), d.dtype)
+    for y in range(H):
+        sy = min(int(math.floor(y * ify)), h - 1)
+        for x in range(W):
+            out[y, x] = d[sy, min(int(math.floor(x * ifx)), w - 1)]
+    return np.expand_dims(out, axis=2)
+
+
 def rel_err(a, b):
     """max |a-b| / max(|b|) -- the relative metric the parity tests quote."""
     a, b = a.detach().double(), b.detach().double()

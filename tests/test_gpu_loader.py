@@ -10,7 +10,7 @@ import torch
 JIT = (0.2, 0.2, 0.2, 0.05)
 
 
-def _samples(sizes, seed=11, n_ctx=2):
+def _samples(sizes, seed=11, n_ctx=2, depth=False):
     from PIL import Image
     rng = np.random.default_rng(seed)
     out = []
@@ -18,9 +18,31 @@ def _samples(sizes, seed=11, n_ctx=2):
         img = lambda: Image.fromarray(rng.integers(0, 256, (h0, w0, 3), dtype=np.uint8))
         K = np.array([[721.5, 0.0, w0 / 2], [0.0, 721.5, h0 / 2], [0.0, 0.0, 1.0]], np.float32)
         poses = [np.eye(4, dtype=np.float32) + 0.01 * j for j in range(n_ctx)]
-        out.append({"idx": i, "filename": f"s{i}", "rgb": img(), "rgb_context": [img() for _ in range(n_ctx)],
-                    "intrinsics": K, "pose_context": poses})
+        s = {"idx": i, "filename": f"s{i}", "rgb": img(), "rgb_context": [img() for _ in range(n_ctx)],
+             "intrinsics": K, "pose_context": poses}
+        if depth:
+            # sparse LiDAR-like depth (KITTI velodyne projection: ~5 % valid)
+            dmap = lambda: (rng.uniform(1, 80, (h0, w0)) * (rng.random((h0, w0)) < 0.05)).astype(np.float32)
+            s["depth"] = dmap()
+            s["depth_context"] = [dmap()[..., None] for _ in range(n_ctx)]
+        out.append(s)
     return out
+
+
+def test_resize_depth_nearest_matches_cv2_restatement():
+    """The gather used on the GPU (run here on CPU tensors) == the oracle's
+    OpenCV INTER_NEAREST restatement, for KITTI raw sizes -> 192x640 and an
+    upscaling case."""
+    from oracle import dro_oracle as O
+    from dro_sfm_amd.datasets.gpu_loader import resize_depth_nearest
+    rng = np.random.default_rng(3)
+    for (h, w), shape in [((375, 1242), (192, 640)), ((370, 1226), (192, 640)), ((7, 9), (16, 20))]:
+        d = rng.uniform(0, 80, (2, h, w)).astype(np.float32)
+        got = resize_depth_nearest(torch.from_numpy(d), shape)
+        assert got.shape == (2, 1) + shape
+        for b in range(2):
+            want = O.resize_depth_cv2_nearest(d[b], shape)[..., 0]
+            assert np.array_equal(got[b, 0].numpy(), want)
 
 
 def test_collate_decoded_layout():
@@ -36,6 +58,9 @@ def test_collate_decoded_layout():
     assert b["intrinsics"].shape == (3, 3, 3) and b["intrinsics"].dtype == torch.float32
     assert len(b["pose_context"]) == 2 and b["pose_context"][1].shape == (3, 4, 4)
     assert b["idx"] == [0, 1, 2] and b["filename"][2] == "s2"
+    d = collate_decoded(_samples([(12, 20), (10, 18)], depth=True))
+    assert [t.shape for t in d["depth"]] == [(12, 20), (10, 18)] and d["depth"][0].dtype == torch.float32
+    assert len(d["depth_context"]) == 2 and d["depth_context"][1][1].shape == (10, 18)
 
 
 @pytest.mark.gpu
@@ -70,3 +95,25 @@ def test_gpu_pipeline_matches_reference_chain():
         K[1] *= H / h0
         assert torch.allclose(out["intrinsics"][n].cpu(), K, rtol=0, atol=1e-4)
     assert out["pose_context"][1].is_cuda and out["pose_context"][1].shape == (3, 4, 4)
+
+
+@pytest.mark.gpu
+def test_gpu_pipeline_depth_two_raw_sizes():
+    """Supervised batches: 'depth' and 'depth_context' of samples
+    from two KITTI drives (375x1242, 370x1226) come out [B, 1, 192, 640] on the
+    device, each sample equal to resize_depth (cv2 INTER_NEAREST restated in
+    the oracle) + ToTensor -- the resolution SupervisedDepthPoseLoss needs."""
+    from oracle import dro_oracle as O
+    from dro_sfm_amd.datasets.gpu_loader import GPUTrainPipeline, collate_decoded
+    H, W = 192, 640
+    sizes = [(375, 1242), (370, 1226), (370, 1226)]
+    s = _samples(sizes, depth=True)
+    out = GPUTrainPipeline((H, W), JIT, generator=torch.Generator().manual_seed(5))(collate_decoded(s))
+    assert out["depth"].shape == (3, 1, H, W) and out["depth"].is_cuda
+    assert len(out["depth_context"]) == 2 and out["depth_context"][0].shape == (3, 1, H, W)
+    for n in range(3):
+        want = O.resize_depth_cv2_nearest(s[n]["depth"], (H, W))[..., 0]
+        assert np.array_equal(out["depth"][n, 0].cpu().numpy(), want), n
+        for j in range(2):
+            want = O.resize_depth_cv2_nearest(s[n]["depth_context"][j], (H, W))[..., 0]
+            assert np.array_equal(out["depth_context"][j][n, 0].cpu().numpy(), want), (n, j)
