@@ -446,27 +446,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
-    ap.add_argument("--no-miopen", action="store_true",
-                    help="run the remaining library convolutions on PyTorch's native kernels")
-    ap.add_argument("--conv-backend", choices=("hip", "miopen"), default="hip",
-                    help="update-block convolutions: native f32-MFMA engine or MIOpen (A/B only)")
-    ap.add_argument("--wgrad-side-stream", action="store_true",
-                    help="per-call weight-gradient kernels on a side stream (A/B; eager only)")
-    ap.add_argument("--no-direct-wgrad", action="store_true",
-                    help="weight gradients through autograd instead of in place on a side stream (A/B)")
-    ap.add_argument("--depth-encoder-main", action="store_true",
-                    help="cnet_depth on the main stream instead of the pose block's stream (A/B)")
-    ap.add_argument("--concurrent-encoders", action="store_true",
-                    help="context encoders on side streams beside fnet (A/B; slower, DESIGN.md)")
-    ap.add_argument("--pose-encoder-main", action="store_true",
-                    help="A/B: cnet_pose on the main stream (default: on the pose block's stream)")
-    ap.add_argument("--serial-blocks", action="store_true",
-                    help="A/B: pose update block after the depth block on one stream (default: the "
-                         "pose block on a side stream beside the depth block)")
-    ap.add_argument("--no-grad-sinks", action="store_true",
-                    help="autograd's per-use gradient sums instead of in-place gradient sinks (A/B)")
-    ap.add_argument("--aten-maxpool", action="store_true",
-                    help="A/B: the ResNet stem max pooling through ATen instead of hip.maxpool3x3s2")
     ap.add_argument("--pipeline", choices=("resident", "gpu"), default="resident",
                     help="resident: float batches already in HBM (the metric's contract); gpu: every step "
                          "starts from decoded uint8 KITTI raw frames (375x1242) in pinned host memory and "
@@ -476,13 +455,6 @@ def main():
                     help="A/B: the encoders' stride-2 convs on the HIP engine instead of MIOpen")
     ap.add_argument("--miopen-encoder-convs", action="store_true",
                     help="A/B: the encoders' stride-1 3x3 convolutions on MIOpen instead of the HIP engine")
-    ap.add_argument("--no-fused-bn", action="store_true",
-                    help="encoder BatchNorm+ReLU through PyTorch's kernels (A/B)")
-    ap.add_argument("--miopen-find", choices=("on", "off"), default="off",
-                    help="torch.backends.cudnn.benchmark (MIOpen Find for the library convs; the "
-                         "reference sets it, horovod_trainer.py:34)")
-    ap.add_argument("--split-engine", choices=("off", "all", "3x3fwd"), default="off",
-                    help="split-bf16 MFMA conv engine (csrc/xconv.hip) for the halo convs (A/B)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel loop (for rocprofv3 --stats / --pmc runs)")
     ap.add_argument("--roofline-iters", type=int, default=50)
@@ -493,31 +465,14 @@ def main():
     set_workload(args.workload)
     if args.batch is None:
         args.batch = WL["batch"]
-    torch.backends.cudnn.enabled = not args.no_miopen
-    torch.backends.cudnn.benchmark = args.miopen_find == "on"
     if args.roofline_only:
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         torch.cuda.set_device(dev)
         print(json.dumps({"roofline": roofline_conv(dev, args.roofline_iters, TRAFFIC_FILE)}), flush=True)
         return
-    import dro_sfm_amd.hip.conv as _hconv
-    _hconv.set_direct_weight_grads(not args.no_direct_wgrad)
-    _hconv.set_weight_grad_stream(args.wgrad_side_stream)
-    _hconv.set_split_engine(args.split_engine != "off", args.split_engine)
-    from dro_sfm_amd.networks.optim import update as _update
-    _update.set_conv_backend(args.conv_backend)
-    from dro_sfm_amd.networks.depth_pose import DepthPoseNet as _dpn
-    _dpn.set_concurrent_encoders(args.concurrent_encoders)
-    _dpn.set_concurrent_blocks(not args.serial_blocks)
-    _dpn.set_pose_encoder_stream(not args.pose_encoder_main)
-    _dpn.set_depth_encoder_pose_stream(not args.depth_encoder_main)
     from dro_sfm_amd.networks.optim import extractor as _extractor
-    _extractor.set_fused_batchnorm(not args.no_fused_bn)
-    _extractor.set_native_maxpool(not args.aten_maxpool)
     _extractor.set_native_convs(not args.miopen_encoder_convs)
     _extractor.set_native_strided_convs(args.native_strided_convs)
-    from dro_sfm_amd.hip import ops as _hops
-    _hops.set_grad_sinks(not args.no_grad_sinks)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -590,20 +545,9 @@ def main():
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch, "ref_frames": NREF,
                    "image": [H, W], "parallelism": f"dp{world}", "flip_lr_prob": args.flip_prob,
                    "optimizer": "Adam lr 2e-4", "execution": mode,
-                   "update_convs": args.conv_backend,
-                   "encoders": "concurrent streams" if args.concurrent_encoders else "serial",
-                   "update_blocks": "serial" if args.serial_blocks else "concurrent streams",
-                   "pose_encoder": "main stream" if (args.pose_encoder_main or args.serial_blocks) else "pose-block stream",
-                   "depth_encoder": "main stream" if (args.depth_encoder_main or args.pose_encoder_main
-                                                      or args.serial_blocks) else "pose-block stream, first",
-                   "grad_sinks": not args.no_grad_sinks,
-                   "split_engine": args.split_engine,
-                   "encoder_bn": "pytorch" if args.no_fused_bn else "fused hip",
+                   "update_blocks": "depth block + pose block (side stream, with both context encoders)",
                    "encoder_3x3_s1": "miopen" if args.miopen_encoder_convs else "hip",
-                   "encoder_strided": "hip" if args.native_strided_convs else "miopen",
-                   "stem_pool": "aten" if args.aten_maxpool else "hip",
-                   "weight_grads": "autograd" if args.no_direct_wgrad else
-                   ("in place, side stream" if args.wgrad_side_stream else "in place")},
+                   "encoder_strided": "hip" if args.native_strided_convs else "miopen"},
         "final_loss": round(float(loss), 6),
     }
     if rank == 0 and not args.no_roofline:

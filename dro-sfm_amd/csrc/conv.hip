@@ -1167,239 +1167,6 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
   }
 }
 
-// ------------------------------------------------------------------ weight gradient v3
-// Same GEMM and partial layout as wgrad2_kernel ([split][tap][o][c], bias
-// [split][o], wgrad2_finish_kernel), with SMALLER channel tiles: BO (32 or 64)
-// output x 32 input channels x all taps per block, 8 waves (2 per SIMD) that
-// split the pixels of each tile (wave w: o half w / NPG, pixel group w % NPG),
-// every wave holding all T tap accumulators.  At a fixed block count the
-// smaller tile needs 2-4x fewer pixel splits: the split partials -- written
-// once and read back by the finish, 35 MB each way for the fnet layer1 3x3 at
-// 240 splits of 64x64 -- shrink by that factor, and each block runs 2-4x more
-// pixel tiles behind its one exposed prologue.  The pixel groups are summed
-// through LDS in a fixed order at the end (RT taps per round).  1-D grid,
-// XCD-aware: the channel-tile blocks of a split (which stage the same pixels)
-// and neighbouring splits share an XCD's L2.
-// compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1 (register
-// arrays indexed by i stay in VGPRs; a runtime index put them in scratch)
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (N > 0) {
-    static_for<N - 1>(f);
-    f(std::integral_constant<int, N - 1>{});
-  }
-}
-
-template <int KH, int KW, int BO>
-struct HaloShapeW3 {
-  static constexpr int T = KH * KW;
-  static constexpr int TH = HaloShape<32, KH, KW>::TH, TW = 64 / TH;
-  static constexpr int HWd = TW + KW - 1;
-  static constexpr int HALO = (TH + KH - 1) * HWd;
-  static constexpr int HPAD = HALO;
-  static constexpr int NJ = (HALO + 63) / 64;
-  static constexpr int NT = 2;                          // pixel tiles per stage
-  static constexpr int XSTR = (NT * HPAD) | 1;          // odd channel stride (conflict-free B reads)
-  static constexpr int BC = 32, GPAD = BO + 1;
-  static constexpr int NWO = BO / 32, NPG = 8 / NWO;   // o halves, pixel groups
-  static constexpr int KSW = 32 / NPG;                 // k-steps (pixel pairs) per wave per tile
-  static constexpr int GPW = BO / 8, XPW = BC / 8;      // G rows / X channels staged per wave
-  static constexpr int STAGE = NT * 64 * GPAD + BC * XSTR;
-  static constexpr int RT = T < 3 ? T : 3;              // taps per reduction round
-  static constexpr int RED = RT * 8 * 16 * 64;
-  static constexpr int LDS = 2 * STAGE > RED ? 2 * STAGE : RED;
-  static_assert(NJ <= 2 && TW % 2 == 0 && (BO == 32 || BO == 64), "wgrad3 shape");
-};
-
-template <int KH, int KW, int GACT, bool MULTI, int BO>
-__global__ __launch_bounds__(512) void wgrad3_kernel(typename WgParam<MULTI>::T P) {
-  const IgArgs& a = WgParam<MULTI>::ig(P);
-  using S = HaloShapeW3<KH, KW, BO>;
-  constexpr int T = S::T, TH = S::TH, TW = S::TW, HWd = S::HWd, HALO = S::HALO, HPAD = S::HPAD;
-  constexpr int NJ = S::NJ, NT = S::NT, XSTR = S::XSTR, BC = S::BC, GPAD = S::GPAD, STAGE = S::STAGE;
-  constexpr int NPG = S::NPG, KSW = S::KSW, GPW = S::GPW, XPW = S::XPW, RT = S::RT;
-  constexpr int PH = KH / 2, PW = KW / 2;
-  __shared__ float smem[S::LDS];
-  const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
-  const int H = a.g.H, W = a.g.W, Cin = a.g.Cin, Cout = a.g.Cout;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..7
-  const int noc = a.otiles * ((Cin + BC - 1) / BC);
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = L / noc, t = L - split * noc;
-  const int ot = t % a.otiles, ct = t / a.otiles;
-  const int o0 = ot * BO, c0 = ct * BC;
-  const unsigned HWu = (unsigned)H * (unsigned)W;
-  int ntiles = a.g.B * a.tiles_img;
-  if constexpr (MULTI) ntiles = P.use_tiles * P.nuse;
-  const int tbeg = split * a.chunks_per_split;
-  const int tend = min(ntiles, tbeg + a.chunks_per_split);
-  const int nst = (tend - tbeg + NT - 1) / NT;         // stages of NT tiles
-  const bool do_bias = a.gbias && ct == 0;
-  const float galpha = a.galpha;
-  float gr[NT][GPW], yr[NT][GACT ? GPW : 1], xr[NT][XPW * NJ], bsum[GPW];
-  unsigned gmask[NT], xmask[NT];
-#pragma unroll
-  for (int j = 0; j < GPW; ++j) bsum[j] = 0.f;
-  auto load1 = [&](auto uc, int tile) __attribute__((always_inline)) {
-    constexpr int u = decltype(uc)::value;
-    const bool tv = tile < tend;                       // scalar: past the split's tiles -> zeros
-    tile = tv ? tile : tbeg;
-    const float* __restrict__ Gp = a.G;
-    const float* __restrict__ Yp = a.gy;
-    KSlice sbase = kernarg_srcs();
-    if constexpr (MULTI) {
-      const int uu = tile / P.use_tiles;
-      tile -= uu * P.use_tiles;
-      Gp = *(KFPtr)(kernarg_base() + offsetof(WgMulti, uG) + uu * sizeof(FPtr));
-      if (GACT) Yp = *(KFPtr)(kernarg_base() + offsetof(WgMulti, uy) + uu * sizeof(FPtr));
-      sbase = (KSlice)(kernarg_base() + offsetof(WgMulti, usrc)) + uu * kMaxSrc;
-    }
-    const int b = tile / a.tiles_img, trem = tile - b * a.tiles_img;
-    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
-    // G tile: lane = pixel of the tile, wave w -> output channels o0 + GPW w + j
-    const int qy = lane / TW, qx = lane - qy * TW;
-    const int oy = ty0 + qy, ox = tx0 + qx;
-    const bool pin = tv && oy < H && ox < W;
-    const unsigned pix = pin ? (unsigned)(oy * W + ox) : 0u;
-    unsigned gm = 0;
-#pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      const int o = o0 + wave * GPW + j;        // scalar
-      const bool ok = pin && o < Cout;
-      gm |= ok ? (1u << j) : 0u;
-      const unsigned off = ok ? ((unsigned)b * Cout + o) * HWu + pix : 0u;
-      gr[u][j] = Gp[off];
-      if (GACT) yr[u][j] = Yp[off];
-    }
-    gmask[u] = gm;
-    // X patch: wave w -> channels c0 + XPW w + i, lanes over the halo
-    RowDesc ds[XPW];
-    bool real[XPW];
-#pragma unroll
-    for (int i = 0; i < XPW; ++i) {
-      const int ch = c0 + wave * XPW + i;       // scalar
-      real[i] = tv && ch < Cin;
-      ds[i] = row_desc_at(sbase, cb1, cb2, cb3, ch < Cin ? ch : 0, HWu);
-    }
-    unsigned xm = 0;
-#pragma unroll
-    for (int i = 0; i < XPW; ++i) {
-      const unsigned xbase = (unsigned)b * ds[i].A + ds[i].Bc;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int e = lane + 64 * j;
-        const int hy = e / HWd, hx = e - hy * HWd;
-        const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
-        const bool ok = real[i] && e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        xm |= ok ? (1u << (i * NJ + j)) : 0u;
-        xr[u][i * NJ + j] = ds[i].p[ok ? xbase + (ds[i].M ? (unsigned)(yy * W + xx) : 0u) : 0u];
-      }
-    }
-    xmask[u] = xm;
-  };
-  auto load = [&](int st) __attribute__((always_inline)) {
-    static_for<NT>([&](auto uc) __attribute__((always_inline)) { load1(uc, tbeg + st * NT + decltype(uc)::value); });
-  };
-  auto store = [&](int buf) __attribute__((always_inline)) {
-    float* Gs = smem + buf * STAGE;
-    float* Xs = Gs + NT * 64 * GPAD;
-    static_for<NT>([&](auto uc) __attribute__((always_inline)) {
-      constexpr int u = decltype(uc)::value;
-#pragma unroll
-      for (int j = 0; j < GPW; ++j) {
-        float g = (gmask[u] >> j) & 1u ? galpha * gr[u][j] : 0.f;
-        if (GACT) g *= act_bwd(yr[u][j], GACT);
-        Gs[(u * 64 + lane) * GPAD + wave * GPW + j] = g;
-        if (do_bias) bsum[j] += g;
-      }
-#pragma unroll
-      for (int i = 0; i < XPW; ++i) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int e = lane + 64 * j;
-          if (e < HPAD)
-            Xs[(wave * XPW + i) * XSTR + u * HPAD + e] = (xmask[u] >> (i * NJ + j)) & 1u ? xr[u][i * NJ + j] : 0.f;
-        }
-      }
-    });
-  };
-
-  const int wo = wave / NPG, pg = wave - wo * NPG;
-  const int hi = lane >> 5;
-  f32x16 acc[T];
-#pragma unroll
-  for (int tp = 0; tp < T; ++tp)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[tp][r] = 0.f;
-
-  if (nst > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    const bool more = st + 1 < nst;
-    if (more) load(st + 1);
-    const float* Gs = smem + buf * STAGE;
-    const float* Xs = Gs + NT * 64 * GPAD;
-#pragma unroll
-    for (int u = 0; u < NT; ++u) {
-      const float* ga = Gs + (u * 64 + hi) * GPAD + wo * 32 + (lane & 31);
-      const float* xb = Xs + (lane & 31) * XSTR + u * HPAD + hi;
-#pragma unroll
-      for (int s = 0; s < KSW; ++s) {
-        const int pp = 2 * (pg * KSW + s);          // even pixel of this k-step
-        const float av = ga[pp * GPAD];
-        const int poff = (pp / TW) * HWd + (pp % TW);
-#pragma unroll
-        for (int k = 0; k < T; ++k) {
-          const int ty = k / KW, tx = k - ty * KW;
-          acc[k] = mfma32(av, xb[poff + ty * HWd + tx], acc[k]);
-        }
-      }
-    }
-    if (more) store(buf ^ 1);
-    __syncthreads();
-  }
-  // sum the pixel groups RT taps at a time (fixed order pg = 0..NPG-1) and
-  // write the split partials: lanes along c (128-B row segments)
-  float* wpart = a.part + (size_t)split * Cout * Cin * T;
-  const size_t tstride = (size_t)Cout * Cin;
-  float* red = smem;   // [RT][8 waves][16][64]
-#pragma unroll
-  for (int t0 = 0; t0 < T; t0 += RT) {
-#pragma unroll
-    for (int tt = 0; tt < RT; ++tt) {
-      if (t0 + tt < T) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) red[((tt * 8 + wave) * 16 + r) * 64 + lane] = acc[t0 + tt][r];
-      }
-    }
-    __syncthreads();
-    for (int e = tid; e < RT * BO * BC; e += 512) {
-      const int tt = e / (BO * BC), rem = e - tt * (BO * BC);
-      const int ol = rem / BC, c = rem - ol * BC;
-      const int wq = ol / 32, om = ol - wq * 32;
-      const int r = (om & 3) + 4 * (om >> 3), ln = c + 32 * ((om >> 2) & 1);
-      float v = 0.f;
-#pragma unroll
-      for (int g = 0; g < NPG; ++g) v += red[((tt * 8 + wq * NPG + g) * 16 + r) * 64 + ln];
-      const int o = o0 + ol, cc = c0 + c;
-      if (t0 + tt < T && o < Cout && cc < Cin) wpart[(t0 + tt) * tstride + (size_t)o * Cin + cc] = v;
-    }
-    __syncthreads();
-  }
-  if (do_bias) {
-#pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      const float v = wave_sum(bsum[j]);
-      const int o = o0 + wave * GPW + j;
-      if (lane == 0 && o < Cout) a.bpart[(size_t)split * Cout + o] = v;
-    }
-  }
-}
 
 // wgrad2 partials: dW[o][c][tap] = sum_s part[s][tap][o][c]; db[o] = sum_s bpart[s][o].
 // Threads walk the partials' coalesced (tap, o, c) order.  The reduction is
@@ -1742,55 +1509,6 @@ WhPlan plan_wgrad2(int Cin, int Cout, int KH, int KW, int ntiles_total, int B, i
   return pl;
 }
 
-// weight gradient v3 (wgrad3_kernel): BO x 32 channel tiles; BO = 64 when the
-// output channels alone give enough tiles (Cout >= 128), else 32.  Splits fill
-// ~`target` blocks.  Opt-in (DRO_WG3=1; DRO_WG3_BO forces BO): measured slower
-// than wgrad2 (fnet layer1 roofline call 52.4 vs 57.7 TF/s; step weight-gradient
-// kernels + finish 5.4 vs 4.35 ms) -- the smaller tile's extra staging per MFMA
-// costs more than its 4x smaller split partials save.
-bool wgrad_v3() {
-  static const bool v3 = [] {
-    const char* e = getenv("DRO_WG3");
-    return e && atoi(e) == 1;
-  }();
-  return v3;
-}
-
-WhPlan plan_wgrad3(int Cin, int Cout, int KH, int KW, int ntiles_total, int B, int H, int W, int* bo_out) {
-  WhPlan pl = {};
-  pl.ok = (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3) || (KH == 1 && KW == 1);
-  if (!pl.ok) return pl;
-  const int TH = (KW == 1 || (KH == 3 && KW == 3)) ? 8 : 4, TW = 64 / TH;
-  pl.tiles_x = (W + TW - 1) / TW;
-  pl.tiles_img = ((H + TH - 1) / TH) * pl.tiles_x;
-  const int ntiles = ntiles_total > 0 ? ntiles_total : B * pl.tiles_img;
-  static const int bo_env = [] {
-    const char* e = getenv("DRO_WG3_BO");
-    const int v = e ? atoi(e) : 0;
-    return v == 32 || v == 64 ? v : 0;
-  }();
-  const int BO = bo_env ? bo_env : (Cout >= 128 ? 64 : 32);
-  if (bo_out) *bo_out = BO;
-  pl.otiles = (Cout + BO - 1) / BO;
-  pl.ctiles = (Cin + 31) / 32;
-  pl.tgroups = 1;
-  const int blocks = pl.otiles * pl.ctiles;
-  static const int target = [] {   // tuning override: DRO_WG3_TARGET_BLOCKS (default 256)
-    const char* e = getenv("DRO_WG3_TARGET_BLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 256;
-  }();
-  int sp = (target + blocks - 1) / blocks;
-  if (sp > 256) sp = 256;
-  if (sp > ntiles) sp = ntiles;
-  if (sp < 1) sp = 1;
-  pl.tiles_per_split = ((ntiles + sp - 1) / sp + 1) / 2 * 2;   // whole stages of 2 tiles
-  pl.splits = (ntiles + pl.tiles_per_split - 1) / pl.tiles_per_split;
-  pl.part_bytes = align256((size_t)pl.splits * Cout * Cin * KH * KW * sizeof(float)) +
-                  align256((size_t)pl.splits * Cout * sizeof(float));
-  return pl;
-}
-
 size_t fwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
   return std::max(plan_igemm(Cout, Cin, KH, KW, B, H, W).part_bytes,
                   xconv_part_bytes(Cout, Cin, KH, KW, B, H, W));
@@ -1804,8 +1522,7 @@ size_t bwd_workspace(int B, int H, int W, int Cin, int Cout, int KH, int KW) {
                   xconv_part_bytes(Cin, Cout, KH, KW, B, H, W)) +
          std::max(std::max(plan_wgrad(Cin, Cout, T, P).part_bytes,  // weight-gradient partials
                            plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).part_bytes),
-                  std::max(plan_wgrad2(Cin, Cout, KH, KW, 0, B, H, W).part_bytes,
-                           plan_wgrad3(Cin, Cout, KH, KW, 0, B, H, W, nullptr).part_bytes));
+                  plan_wgrad2(Cin, Cout, KH, KW, 0, B, H, W).part_bytes);
 }
 
 bool too_big(long long B, long long C, long long HW) { return B * C * HW >= (1LL << 30); }
@@ -2446,30 +2163,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     DRO_ACT_SWITCH(gact, st = (launch_igemm<1, A_, 0>(a, P, ws_ig, s)));
     if (st) return st;
   }
-  if (grad_weight && wh.ok && !wgrad_v1() && wgrad_v3()) {
-    int BO = 32;
-    const WhPlan w3 = plan_wgrad3(a.g.Cin, Cout, KH, KW, 0, B, H, W, &BO);
-    a.otiles = w3.otiles;
-    a.tiles_x = w3.tiles_x;
-    a.tiles_img = w3.tiles_img;
-    a.chunks_per_split = w3.tiles_per_split;
-    a.part = reinterpret_cast<float*>(ws_wg);
-    a.bpart = reinterpret_cast<float*>(ws_wg + align256((size_t)w3.splits * Cout * a.g.Cin * T * sizeof(float)));
-    const dim3 grid((unsigned)(w3.otiles * w3.ctiles * w3.splits));
-    const int gact = fold ? act : 0;
-    conv_logf(2.0 * Cout * a.g.Cin * T * (double)P, "wgrad3_kernel<%d, %d, %d, false, %d>", KH, KW, gact, BO);
-#define DRO_WG3(KH_, KW_, BO_) DRO_ACT_SWITCH(gact, hipLaunchKernelGGL((wgrad3_kernel<KH_, KW_, A_, false, BO_>), grid, dim3(512), 0, s, a))
-#define DRO_WG3B(KH_, KW_) if (BO == 64) { DRO_WG3(KH_, KW_, 64); } else { DRO_WG3(KH_, KW_, 32); }
-    if (KH == 1 && KW == 1) { DRO_WG3B(1, 1); }
-    else if (KH == 1) { DRO_WG3B(1, 5); }
-    else if (KW == 1) { DRO_WG3B(5, 1); }
-    else { DRO_WG3B(3, 3); }
-#undef DRO_WG3B
-#undef DRO_WG3
-    if ((st = launch_status("wgrad3_kernel launch failed"))) return st;
-    launch_wgrad2_finish(a, w3.splits, s);
-    if ((st = launch_status("wgrad2_finish_kernel launch failed"))) return st;
-  } else if (grad_weight && wh.ok && !wgrad_v1()) {
+  if (grad_weight && wh.ok && !wgrad_v1()) {
     const WhPlan w2 = plan_wgrad2(a.g.Cin, Cout, KH, KW, 0, B, H, W);
     a.otiles = w2.otiles;
     a.tiles_x = w2.tiles_x;
@@ -2728,7 +2422,6 @@ extern "C" size_t dro_conv2d_weight_grad_multi_workspace_bytes(int nuse, int B, 
   if (nuse < 1) nuse = 1;
   if (!wgrad_v1()) {
     const WhPlan t = plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W);
-    if (wgrad_v3()) return plan_wgrad3(Cin, Cout, KH, KW, nuse * B * t.tiles_img, B, H, W, nullptr).part_bytes;
     return plan_wgrad2(Cin, Cout, KH, KW, nuse * B * t.tiles_img, B, H, W).part_bytes;
   }
   return plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W).part_bytes;
@@ -2774,12 +2467,9 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
   }
   const int Cin = m.a.g.Cin, T = KH * KW;
   const bool v2 = !wgrad_v1();
-  const bool v3 = v2 && wgrad_v3();
-  int BO = 32;
   const int ntiles_all = nuse * B * plan_wgrad_halo(Cin, Cout, KH, KW, B, H, W).tiles_img;
-  const WhPlan wh = v3   ? plan_wgrad3(Cin, Cout, KH, KW, ntiles_all, B, H, W, &BO)
-                    : v2 ? plan_wgrad2(Cin, Cout, KH, KW, ntiles_all, B, H, W)
-                         : plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W);
+  const WhPlan wh = v2 ? plan_wgrad2(Cin, Cout, KH, KW, ntiles_all, B, H, W)
+                       : plan_wgrad_multi(Cin, Cout, KH, KW, nuse, B, H, W);
   if (!wh.ok) {
     set_error("conv2d_weight_grad_multi: kernel shape not supported (1x1, 1x5, 5x1, 3x3)");
     return DRO_E_SHAPE;
@@ -2810,22 +2500,6 @@ extern "C" int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse,
   hipStream_t s = (hipStream_t)stream;
   const int tgroups = v2 ? wh.tgroups : 1;
   const dim3 grid((unsigned)(wh.otiles * wh.ctiles * tgroups), (unsigned)wh.splits);
-  if (v3) {
-    conv_logf(2.0 * Cout * Cin * T * (double)B * H * W * nuse, "wgrad3_kernel<%d, %d, %d, true, %d>", KH, KW, act,
-              BO);
-    const dim3 grid1((unsigned)(wh.otiles * wh.ctiles * wh.splits));
-#define DRO_WG3M(KH_, KW_, BO_) DRO_ACT_SWITCH(act, hipLaunchKernelGGL((wgrad3_kernel<KH_, KW_, A_, true, BO_>), grid1, dim3(512), 0, s, m))
-#define DRO_WG3MB(KH_, KW_) if (BO == 64) { DRO_WG3M(KH_, KW_, 64); } else { DRO_WG3M(KH_, KW_, 32); }
-    if (KH == 1 && KW == 1) { DRO_WG3MB(1, 1); }
-    else if (KH == 1) { DRO_WG3MB(1, 5); }
-    else if (KW == 1) { DRO_WG3MB(5, 1); }
-    else { DRO_WG3MB(3, 3); }
-#undef DRO_WG3MB
-#undef DRO_WG3M
-    if ((st = launch_status("wgrad3_kernel<multi> launch failed"))) return st;
-    launch_wgrad2_finish(a, wh.splits, s);
-    return launch_status("wgrad2_finish_kernel launch failed");
-  }
   if (v2)
     conv_logf(2.0 * Cout * Cin * T * (double)B * H * W * nuse, "wgrad2_kernel<%d, %d, %d, true, %d>", KH, KW,
               act, tgroups);

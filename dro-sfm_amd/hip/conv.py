@@ -17,11 +17,12 @@ Direct weight gradients (the trainer's path): when the parameters a conv reads
 are flagged `_dro_direct` and their `.grad` tensors are back-to-back views of
 one flat buffer (trainers/dp_trainer.GradBuckets lays fused groups out
 adjacently), the weight/bias gradient kernels accumulate straight into those
-views (in stream order by default, or on a side HIP stream concurrently with
-the data-gradient chain: set_weight_grad_stream); autograd receives None for
-the parameters, and a side stream is joined into the caller's stream at the end
-of backward (engine final callback).  Fused weights (z|r gates, shared-input heads) are then
-views of the flat parameter buffer instead of per-forward concatenations.
+views, in stream order; autograd receives None for the parameters.  Fused
+weights (z|r gates, shared-input heads) are then views of the flat parameter
+buffer instead of per-forward concatenations.  (Round 3 measured two
+side-stream variants -- per-call weight gradients forked onto a side stream,
+and the batched flushes on a stream of their own -- both slower under hipGraph
+replay; they were removed in round 4.)
 
 Batched weight gradients (direct path, default on): the recurrent update
 blocks apply every weight once per iteration, so instead of one weight-gradient
@@ -42,7 +43,6 @@ afresh) and the split buffers are saved for the backward.
 """
 import contextlib
 import ctypes
-import os
 
 import torch
 
@@ -216,89 +216,6 @@ def _mark_direct(params):
         p._dro_direct_used = True
 
 
-_SIDE = {}
-_JOINS = {}          # forking stream -> its side stream, joined at the end of this backward
-_USE_SIDE = [False]
-_FORK_ROLES = {}     # stream id of a persistent model stream -> its own side-stream key
-
-
-def register_fork_stream(stream):
-    """A persistent stream of the model (DepthPoseNet's pose-block stream)
-    whose backward work forks weight gradients onto a side stream of its own.
-    Every other stream (the main chain: a warm-up stream, then torch's
-    capture stream) shares one side stream, created before capture."""
-    _FORK_ROLES[stream.stream_id] = ("model", stream.stream_id)
-
-
-def set_weight_grad_stream(side):
-    """Run the per-call (non-batched) direct weight-gradient kernels on a side
-    stream (True) or in order on the current stream (False, default: measured
-    faster under hipGraph replay, where cross-stream edges add ~4 us bubbles
-    per fork).  Eager only: GraphedTrainStep refuses to capture with it on
-    (round 3: side-stream weight gradients crashed capture_end)."""
-    _USE_SIDE[0] = bool(side)
-
-
-def weight_grad_stream_enabled():
-    return _USE_SIDE[0]
-
-
-def _fork_side(main=None):
-    """The weight-gradient stream: `main` (default: the current stream), or a
-    side stream forked from it; every side stream forked during a backward pass
-    is joined back into its forking stream by one engine final callback."""
-    main = torch.cuda.current_stream() if main is None else main
-    if not _USE_SIDE[0]:
-        return main
-    # keyed by role, not by stream: the main chain runs on a different stream
-    # in the eager warm-up than under capture, and a stream created during
-    # capture crashed the captured step
-    key = (main.device, _FORK_ROLES.get(main.stream_id, "main"))
-    side = _SIDE.get(key)
-    if side is None:
-        side = _SIDE[key] = torch.cuda.Stream(device=main.device)
-    side.wait_stream(main)
-    if not _JOINS:
-        def join():
-            # into the forking stream AND the stream the backward returns on
-            # (the engine may already have synchronised the forking stream
-            # with it; work forked after that point would be left unjoined)
-            cur = torch.cuda.current_stream()
-            for m, sd in list(_JOINS.values()):
-                m.wait_stream(sd)
-                if cur != m:
-                    cur.wait_stream(sd)
-            _JOINS.clear()
-        torch.autograd.Variable._execution_engine.queue_callback(join)
-    _JOINS[key] = (main, side)
-    return side
-
-
-def join_weight_grad_streams():
-    """Make the CURRENT stream wait for every weight-gradient side stream used
-    since the last join.  Call on the thread that ran backward(), right after
-    it: the engine's final callback may run on an autograd worker thread whose
-    current stream is not the caller's (under graph capture that left the side
-    stream unjoined and capture_end crashed)."""
-    cur = torch.cuda.current_stream()
-    for (dev, _), sd in _SIDE.items():
-        if dev == cur.device:
-            cur.wait_stream(sd)
-    _JOINS.clear()
-    fl = _FLUSH.get(cur.device)
-    if fl is not None:
-        cur.wait_stream(fl)
-    _INFLIGHT.clear()
-
-
-def _on_side(side, tensors):
-    if not _USE_SIDE[0]:
-        return
-    for t in tensors:
-        if t is not None:
-            t.record_stream(side)
-
-
 def _grad_buffers(scope, key, weight, nbias, device):
     """(gw, gb, accumulate, first) for one backward call."""
     if scope is None:
@@ -371,7 +288,7 @@ def flush_param_grads(param):
     if not keys:
         return None
     items = [_PENDING.pop(k) for k in keys]
-    return _launch_weight_grads(items, _flush_stream(items[0][2][0]))
+    return _launch_weight_grads(items, items[0][2][0])
 
 
 def flush_weight_grads(stream=None):
@@ -385,40 +302,6 @@ def flush_weight_grads(stream=None):
     _launch_weight_grads(items, stream or torch.cuda.current_stream())
 
 
-_FLUSH = {}          # device -> the weight-gradient flush stream (set_flush_stream)
-_USE_FLUSH = [os.environ.get("DRO_WGRAD_FLUSH_STREAM", "0") == "1"]
-_INFLIGHT = []       # uses launched on the flush stream, released at the join
-
-
-def set_flush_stream(enabled):
-    """Batched weight gradients (flushed from the parameter hooks as the last
-    use of a weight is back-propagated) on their own stream, so the
-    data-gradient chain -- iteration 0 of the update blocks, the heads, the
-    encoders -- does not wait for them (profiles/r3_step_timeline.txt:
-    iteration 0's backward 3.7 ms against 1.4 ms for iteration 1, the
-    difference being these launches).  Their operands stay referenced until
-    join_weight_grad_streams() (no record_stream).  Off by default
-    (DRO_WGRAD_FLUSH_STREAM=1): captured and replayed it is correct (graph,
-    DP and metric-config parity tests green) but slower, 19.7-19.9 vs
-    16.3-16.4 ms/step A/B on one box -- the weight-gradient kernels (240-block
-    grids) then share the chip with both update-block chains and the
-    encoders' data gradients, and the pose chain's iteration-1 backward
-    stretched from 1.5 to 5.1 ms (profiles/r3_step_timeline_flush_stream.txt)."""
-    _USE_FLUSH[0] = bool(enabled)
-
-
-def _flush_stream(use_stream):
-    if not _USE_FLUSH[0]:
-        return use_stream
-    dev = use_stream.device
-    st = _FLUSH.get(dev)
-    if st is None:
-        if torch.cuda.is_current_stream_capturing():
-            return use_stream            # never create a stream inside a capture
-        st = _FLUSH[dev] = torch.cuda.Stream(device=dev)
-    return st
-
-
 def _launch_weight_grads(items, stream):
     lib = _lib.load()
     side = any(s != stream for _, _, streams in items for s in streams)
@@ -426,9 +309,7 @@ def _launch_weight_grads(items, stream):
         for s in streams:
             if s != stream:
                 stream.wait_stream(s)
-    if side and stream in _FLUSH.values():
-        _INFLIGHT.append(items)          # operands live until the join
-    elif side:
+    if side:
         for _, uses, streams in items:
             for srcs, dout, y in uses:
                 for x in (*srcs, dout, y):
@@ -528,15 +409,12 @@ class _Conv2d(torch.autograd.Function):
                                               ptr(ws), nws, stream_of(gout)), "dro_conv2d_backward(data)")
             if _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None):
                 return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
-            side = _fork_side()
-            _on_side(side, [gout, y, weight, *srcs])
-            with torch.cuda.stream(side):
-                ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
-                check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
-                                              act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                              ptr(gout), None, None, None, None, ptr(gw),
-                                              ptr(gb) if has_bias else None, 1, None, ptr(ws), nws,
-                                              stream_of(gout)), "dro_conv2d_backward(weight)")
+            ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
+            check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
+                                          act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
+                                          ptr(gout), None, None, None, None, ptr(gw),
+                                          ptr(gb) if has_bias else None, 1, None, ptr(ws), nws,
+                                          stream_of(gout)), "dro_conv2d_backward(weight)")
             return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
         want_w = need[0] or (has_bias and need[1])
         if want_w:
@@ -748,15 +626,14 @@ class _SepGRUHalf(torch.autograd.Function):
 
     @staticmethod
     def _backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs, tg, qacc0):
-        """Data-gradient chain on the current stream; dWq/dbq and dWz|r/dbz|r
-        accumulate into the flat .grad views on the side stream."""
+        """Data-gradient chain and, when not batched, dWq/dbq and dWz|r/dbz|r
+        (accumulated into the flat .grad views) on the current stream."""
         B, hd, H, W = h.shape
         KH, KW = wq.shape[2:]
         cin = wq.shape[1]
         st = stream_of(h)
         n = 1 + len(xs)
         (_, _), (gwzr, gbzr), (gwq, gbq) = ctx.direct
-        main = torch.cuda.current_stream()
         drh = torch.empty_like(h)
         ptrs, ctot, coff = _grad_targets([drh, *tg])
         acc = (ctypes.c_int * n)(*qacc0)
@@ -765,16 +642,12 @@ class _SepGRUHalf(torch.autograd.Function):
                                       0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
                                       None, None, 0, ptr(ctx.wsplit[1]), ptr(ws), nws, st),
               "dro_conv2d_backward(q data)")
-        batched = _queue_weight_grad([rh, *xs], wq.shape, 0, 1.0, dq, None, gwq, gbq)
-        side = main if batched else _fork_side()  # dq and r*h are final here
-        _on_side(side, [] if batched else [dq, rh, wq, *xs])
-        with torch.cuda.stream(side) if not batched else contextlib.nullcontext():
-            if not batched:
-                wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-                check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
-                                              0, ctypes.c_float(1.0), None, ptr(dq), None, None, None,
-                                              None, ptr(gwq), ptr(gbq), 1, None, ptr(wsw), nwsw, stream_of(h)),
-                      "dro_conv2d_backward(q weight)")
+        if not _queue_weight_grad([rh, *xs], wq.shape, 0, 1.0, dq, None, gwq, gbq):
+            wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
+            check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
+                                          0, ctypes.c_float(1.0), None, ptr(dq), None, None, None,
+                                          None, ptr(gwq), ptr(gbq), 1, None, ptr(wsw), nwsw, st),
+                  "dro_conv2d_backward(q weight)")
         check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
                                         ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
         ptrs, ctot, coff = _grad_targets([dh, *tg])
@@ -787,15 +660,11 @@ class _SepGRUHalf(torch.autograd.Function):
         if _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
             need = ctx.needs_input_grad
             return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
-        if side is not main:
-            side.wait_stream(main)                # dz|dr are final after stage 2
-        _on_side(side, [dzr, h, wzr])
-        with torch.cuda.stream(side):
-            wsw, nwsw = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-            check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
-                                          0, ctypes.c_float(1.0), None, ptr(dzr), None, None, None, None,
-                                          ptr(gwzr), ptr(gbzr), 1, None, ptr(wsw), nwsw, stream_of(h)),
-                  "dro_conv2d_backward(zr weight)")
+        wsw, nwsw = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
+        check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
+                                      0, ctypes.c_float(1.0), None, ptr(dzr), None, None, None, None,
+                                      ptr(gwzr), ptr(gbzr), 1, None, ptr(wsw), nwsw, st),
+              "dro_conv2d_backward(zr weight)")
         need = ctx.needs_input_grad
         return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
 

@@ -14,16 +14,15 @@ Execution plan (what changes versus the reference, never the math):
     and the whole pose update block (cost, encoder, GRU, head) run once over
     N*B samples instead of N Python iterations;
   * convex upsampling is one HIP launch (hip.convex_upsample);
-  * optionally (set_concurrent_encoders(True)) the two context encoders
-    (cnet_depth, cnet_pose) run on two side HIP streams beside the feature
-    encoder; autograd runs their backward on the same streams and a hipGraph
-    capture records the fork/join as parallel branches.  Measured slower on
-    MI355X (24.7 vs 23.7 ms/step: the cross-stream edges cost more than the
-    overlap of three MIOpen-bound trunks gains), so serial is the default;
-  * tensors read by every iteration (feature maps, context features) can carry
-    a gradient sink (hip.grad_sink, off by default -- measured neutral): the
-    cost and GRU backward kernels then add into it in place instead of autograd
-    summing one gradient per use;
+  * the pose update block runs on a side HIP stream beside the depth update
+    block (they read only each other's detached state of the previous outer
+    iteration), and the two context encoders run on that stream too, beside
+    the feature encoder (cnet_depth first; the depth block waits for it
+    through an event); autograd runs their backward on the same streams and a
+    hipGraph capture records the fork/join as parallel branches;
+  * tensors read by every iteration (feature maps, context features) carry a
+    gradient sink (hip.grad_sink): the cost and GRU backward kernels add into
+    it in place instead of autograd summing one gradient per use;
   * no host synchronisation anywhere: the step can be captured in a hipGraph.
 """
 import contextlib
@@ -54,7 +53,6 @@ def parse_version(version):
             "out_norm": "out" in version, "inter": "inter" in version}
 
 
-_CONCURRENT = [False]
 _SIDE_STREAMS = {}
 
 
@@ -77,11 +75,6 @@ def set_upsample_many(enabled):
     """All kept predictions upsampled in one launch each way after the
     recurrence (default), or one upsample launch per prediction (A/B)."""
     _UPSAMPLE_MANY[0] = bool(enabled)
-
-
-def set_concurrent_encoders(enabled):
-    """Run cnet_depth / cnet_pose on side streams beside fnet (default False)."""
-    _CONCURRENT[0] = bool(enabled)
 
 
 _CONCURRENT_BLOCKS = [True]
@@ -107,13 +100,13 @@ def set_pose_encoder_stream(enabled):
     _POSE_ENCODER_SIDE[0] = bool(enabled)
 
 
-def _side_streams(device):
-    ss = _SIDE_STREAMS.get(device)
-    if ss is None:
-        ss = _SIDE_STREAMS[device] = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
-        for st in ss:
-            hip.conv.register_fork_stream(st)
-    return ss
+def _pose_stream(device):
+    """The pose block's persistent side stream (created once, never during a
+    capture: the eager warm-up steps create it)."""
+    st = _SIDE_STREAMS.get(device)
+    if st is None:
+        st = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+    return st
 
 
 class DepthPoseNet(nn.Module):
@@ -198,24 +191,17 @@ class DepthPoseNet(nn.Module):
         cuda = target_image.is_cuda
         pside = None
         if self.iters > 0 and _CONCURRENT_BLOCKS[0] and cuda:
-            pside = _side_streams(target_image.device)[1]
-        # cnet_depth: beside fnet when set_concurrent_encoders (joined before the
-        # depth block); cnet_pose: on the pose block's stream (no join needed),
-        # or beside fnet without concurrent blocks
+            pside = _pose_stream(target_image.device)
+        # cnet_pose on the pose block's stream (no join needed); cnet_depth
+        # first on that stream too (its backward then runs there, beside
+        # fnet's); the depth block waits for cnet_depth only, through an event
         d_stream = p_stream = None
         d_event = None
         if self.iters > 0 and cuda:
-            if _CONCURRENT[0]:
-                d_stream = _side_streams(target_image.device)[0]
             if pside is not None and _POSE_ENCODER_SIDE[0]:
                 p_stream = pside
                 if _DEPTH_ENCODER_POSE_STREAM[0]:
-                    # cnet_depth first on the pose block's stream (its backward
-                    # then runs there too, beside fnet's); the depth block
-                    # waits for cnet_depth only, through an event
                     d_stream = pside
-            elif _CONCURRENT[0]:
-                p_stream = _side_streams(target_image.device)[1]
             main = torch.cuda.current_stream(target_image.device)
             for st in {d_stream, p_stream} - {None}:
                 st.wait_stream(main)

@@ -531,9 +531,6 @@ class DataParallelTrainer:
         loss = out["loss"]
         stamp("fwd:loss")
         stamp_grad(loss, "bwd:begin").sum().backward()
-        if self.grads.flat.is_cuda:
-            from ..hip.conv import join_weight_grad_streams
-            join_weight_grad_streams()              # weight-gradient side streams, if any
         stamp("bwd:end")
         self.grads.finish()
         if isinstance(self.optimizer, FlatAdam) and self.optimizer.active is None \
@@ -603,10 +600,6 @@ class GraphedTrainStep:
 
     def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True,
                  reduce_in_graph=False):
-        from ..hip.conv import weight_grad_stream_enabled
-        if weight_grad_stream_enabled():
-            raise RuntimeError("GraphedTrainStep: weight-gradient side streams (hip.conv.set_weight_grad_stream) "
-                               "are eager-only")
         self.tr = trainer
         # collectives outside the graph when there is an exchange at all
         self.outside = trainer.grads.reduce and not reduce_in_graph

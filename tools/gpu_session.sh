@@ -25,59 +25,35 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
-    testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
+    tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
+    testsall) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
     bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    benchmi) run bench_miopen 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --conv-backend miopen ;;
-    benchnd) run bench_nodirect 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-direct-wgrad ;;
-    benchside) run bench_side 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
-    benchnosink) run bench_nosink 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-grad-sinks ;;
-    benchsf) run bench_splitfinish 600 env DRO_SPLIT_FINISH=1 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
-    benche) run bench_eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --eager ;;
-    benchn) run bench_native 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-miopen ;;
-    prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
-    roof) run roofline_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/roof" -o run -- python bench.py --roofline-only ;;
-    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python bench.py --roofline-only &&
-         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python bench.py --roofline-only &&
-         run pmc_traffic 60 python tools/pmc_traffic.py "$OUT" ;;
-    w:*) wl=${step#w:}; run "bench_$wl" 900 python bench.py --workload "$wl" --steps 10 --warmup 3 ;;
-    benchnowrw) run bench_nowrwnhwc 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
-    benchnoig) run bench_noigemm 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
-    benchsink) run bench_sink 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --grad-sinks ;;
     benchab) run bench_a 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
-    benchnobn) run bench_nofusedbn 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-fused-bn ;;
-    benchconc) run bench_conc 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --concurrent-encoders ;;
-    convkin) for k in 1 2 4; do run "bench_conv_kin$k" 300 env DRO_CONV_KIN=$k python tools/bench_conv.py --iters 30; done ;;
-    stampkin) for k in 1 2 4; do run "conv_stamps_kin$k" 300 env DRO_CONV_KIN=$k python tools/conv_stamps.py; done ;;
-    kinthr) for t in 512 1024 2048; do run "bench_kin2_below$t" 600 env DRO_CONV_KIN2_BELOW=$t python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline; done ;;
-    stampdbg) run conv_stamps_dbg 300 env STAMP_DBG=${STAMP_DBG:-0,1,2,4,3,5} python tools/conv_stamps.py ;;
-    tprof) run torch_prof 600 python tools/torch_prof.py ;;
+    benche) run bench_eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --eager ;;
+    benchns) run bench_native_strided 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --native-strided-convs ;;
+    benchpipe) run bench_pipeline 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pipeline gpu ;;
+    dp2) run bench_dp2_gloo_onegpu 600 env DRO_DIST_BACKEND=gloo DRO_BENCH_DEVICE=0 python bench.py --gpus 2 --steps 10 --warmup 3 --no-roofline ;;
+    prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
+    profns) run rocprof_ns 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profns" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --native-strided-convs ;;
+    roof) run roofline_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/roof" -o run -- python bench.py --roofline-only ;;
+    roofonly) run roofonly 300 python bench.py --roofline-only ;;
+    pmc) run pmc_fetch 600 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python bench.py --roofline-only &&
+         run pmc_write 600 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python bench.py --roofline-only &&
+         run pmc_traffic 60 python tools/pmc_traffic.py "$OUT" ;;
     pmcsq) run pmc_sq 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python bench.py --roofline-only ;;
     croof) run croof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/croof" -o run -- python tools/conv_roofline.py run "$OUT/croof" &&
          run croof_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/croof_fetch" -o run -- python tools/conv_roofline.py run "$OUT/croof_fetch" &&
          run croof_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/croof_write" -o run -- python tools/conv_roofline.py run "$OUT/croof_write" &&
          run croof_mfma 300 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/croof_mfma" -o run -- python tools/conv_roofline.py run "$OUT/croof_mfma" &&
          run croof_table 60 python tools/conv_roofline.py table "$OUT/croof" --pmc-dirs "$OUT/croof_fetch" "$OUT/croof_write" "$OUT/croof_mfma" ;;
-    v5iso) run py_view5iso 600 python tools/diag_train_steps.py view5iso ;;
-    dp2) run bench_dp2_gloo_onegpu 600 env DRO_DIST_BACKEND=gloo DRO_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 10 --warmup 3 --no-roofline ;;
-    sidediag) run side_eager 300 env PYTHONFAULTHANDLER=1 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --wgrad-side-stream --eager &&
-              run side_graph 300 env PYTHONFAULTHANDLER=1 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --wgrad-side-stream ;;
-    profns) run rocprof_ns 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profns" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --native-strided-convs ;;
-    tlcd) run step_timeline_cnetd 300 env DRO_CNET_DEPTH_POSE_STREAM=1 python tools/step_timeline.py ;;
-    roofonly) run roofonly 300 python bench.py --roofline-only ;;
+    tl) run step_timeline 300 python tools/step_timeline.py ;;
+    photo) run photo_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/photo" -o run -- python tools/bench_photo.py --iters 20 ;;
+    w:*) wl=${step#w:}; run "bench_$wl" 900 python bench.py --workload "$wl" --steps 10 --warmup 3 ;;
     envr:*) kv=${step#envr:}; run "roof_${kv%%=*}_${kv#*=}" 300 env "$kv" python bench.py --roofline-only ;;
     envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
-    benchmienc) run bench_miopen_enc 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --miopen-encoder-convs ;;
-    photo) run photo_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/photo" -o run -- python tools/bench_photo.py --iters 20 ;;
-    benchsb) run bench_serialblocks 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --serial-blocks ;;
-    benche20) run bench_eager20 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --eager ;;
-    benchpipe) run bench_pipeline 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pipeline gpu ;;
-    benchpem) run bench_pose_enc_main 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pose-encoder-main ;;
-    benchns) run bench_native_strided 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --native-strided-convs ;;
-    benchab20) run bench_ab 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
-    k:*) kk=${step#k:}; run "pytest_k_${kk//[^a-zA-Z0-9]/_}" 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider -k "$kk" ;;
-    t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -m pytest "$f" -m gpu -q --timeout=600 -p no:cacheprovider ;;
+    k:*) kk=${step#k:}; run "pytest_k_${kk//[^a-zA-Z0-9]/_}" 900 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider -k "$kk" ;;
+    t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -u -m pytest "$f" -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
   esac
