@@ -318,6 +318,19 @@ __device__ __forceinline__ void bilinear_taps(float ix, float iy, int h, int w, 
   T.idx[3] = T.idx[2] + 1;
 }
 
+// Test hook (parity tests): the bilinear cell (floor(ix), floor(iy)) a kernel
+// took, packed as ((y0 + 32768) << 16) | (x0 + 32768) with each coordinate
+// clamped to [-32767, 32766] (cells that far out have no in-image tap either
+// way); -1 (0xffffffff) is never produced and marks "not recorded".  A
+// coordinate within rounding of an integer is where grid_sample's derivative
+// jumps between two cells: the oracle takes the recorded cell so that fp32
+// and fp64 evaluations are compared on the same branch.
+__device__ __forceinline__ int pack_cell(float ix, float iy) {
+  const float fx = fminf(fmaxf(floorf(ix), -32767.f), 32766.f);
+  const float fy = fminf(fmaxf(floorf(iy), -32767.f), 32766.f);
+  return (int)(((unsigned)((int)fy + 32768) << 16) | (unsigned)((int)fx + 32768));
+}
+
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

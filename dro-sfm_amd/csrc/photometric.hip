@@ -61,6 +61,7 @@ struct PhotoArgs {
   float* part_ph;   // [n,B,tiles]
   float* part_sm;   // [n,B,tiles,2]
   double* part_pose; // [N,n,B,tiles,12] fp64 (block_sum_d)
+  int* cells;        // backward test hook: bilinear cell per (j, i, b, pixel) (pack_cell), or NULL
 };
 
 __device__ __forceinline__ int reflect_idx(int y, int H) {
@@ -141,7 +142,8 @@ __device__ __forceinline__ void stage_warp_bwd(const PhotoArgs& a, const float* 
                                                const float* __restrict__ invt, const float ki[9],
                                                const float kr[9], const float R[9], const float t[3],
                                                int x0, int y0, float* __restrict__ est,
-                                               float (&dxc)[kPxPerThread][3], float (&dyc)[kPxPerThread][3]) {
+                                               float (&dxc)[kPxPerThread][3], float (&dyc)[kPxPerThread][3],
+                                               int* __restrict__ cells) {
   constexpr int PW = W2, PL = H2 * W2, HALO = 2;
   constexpr int NRING = PL - TH * TW;
   constexpr int NR = (NRING + kThreads - 1) / kThreads;
@@ -170,6 +172,9 @@ __device__ __forceinline__ void stage_warp_bwd(const PhotoArgs& a, const float* 
       Proj q;
       project(ki, kr, R, t, (float)gx, (float)gy, depth, a.H, a.W, q);
       bilinear_taps(q.ix, q.iy, a.H, a.W, T[u]);
+      // the cell of an interior pixel is the one its derivative terms use
+      if (interior && cells && y0 + k / PW - HALO < a.H && x0 + k % PW - HALO < a.W)
+        cells[(size_t)gy * a.W + gx] = pack_cell(q.ix, q.iy);
     }
     float v[U][3][4];
 #pragma unroll
@@ -604,7 +609,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     // terms of the thread's own pixels (the projection is recomputed for the
     // chain rule in (3))
     float dxc[kPxPerThread][3], dyc[kPxPerThread][3];
-    stage_warp_bwd(a, ctx, invt, ki, kr, R, t, x0, y0, est, dxc, dyc);
+    stage_warp_bwd(a, ctx, invt, ki, kr, R, t, x0, y0, est, dxc, dyc,
+                   a.cells ? a.cells + ((size_t)(j * a.n + i) * a.B + b) * HW : nullptr);
     __syncthreads();
     float gix[kPxPerThread], giy[kPxPerThread];
 #pragma unroll
@@ -845,6 +851,7 @@ int photo_setup(PhotoArgs& a, const float* image, const float* context, const fl
   a.part_ph = (float*)(ws + L.part_ph);
   a.part_sm = (float*)(ws + L.part_sm);
   a.part_pose = (double*)(ws + L.part_pose);
+  a.cells = nullptr;
   return DRO_OK;
 }
 }  // namespace
@@ -884,7 +891,7 @@ extern "C" int dro_photometric_backward(const float* image, const float* context
                                         int B, int N, int n, int H, int W, float ssim_w, float C1,
                                         float C2, float smooth_w, int automask, int reduce_min,
                                         const float* grad_out, float* grad_inv_depths,
-                                        float* grad_pose, void* workspace, void* stream) {
+                                        float* grad_pose, void* workspace, int* cells, void* stream) {
   PhotoArgs a;
   int st = photo_setup(a, image, context, inv_depths, K, ref_K, pose, pose_mode, B, N, n, H, W,
                        ssim_w, C1, C2, smooth_w, automask, reduce_min, workspace);
@@ -894,6 +901,7 @@ extern "C" int dro_photometric_backward(const float* image, const float* context
     return DRO_E_NULL;
   }
   if (!grad_pose) a.part_pose = nullptr;
+  a.cells = cells;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(photo_bwd_kernel, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a,
                      grad_out, grad_inv_depths);

@@ -42,6 +42,7 @@ struct WarpArgs {
   int B, N, C, h, w;
   int reduce_mean;
   int acc_fmap;      // backward: add into grad_fmap
+  int* cells;        // backward test hook: bilinear cell per (n, b, p) (pack_cell), or NULL
 };
 
 __device__ __forceinline__ void cams(const WarpArgs& a, int b, float ki[9], float kr[9]) {
@@ -52,6 +53,10 @@ __device__ __forceinline__ void cams(const WarpArgs& a, int b, float ki[9], floa
 }
 
 // ------------------------------------------------------------------ forward
+// SAMPLE = false: cost = (fmap - warped)^2 (mean over refs with reduce_mean);
+// SAMPLE = true: the warped map itself (view_synthesis, camera_utils.py:23-56;
+// fmap unused, out [N,B,C,h,w]).
+template <bool SAMPLE>
 __global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* __restrict__ cost) {
   const int P = a.h * a.w;
   const int p = blockIdx.x * kWave + (threadIdx.x & 63);
@@ -67,10 +72,10 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* _
   const float u = (float)(p % a.w), v = (float)(p / a.w);
 
   float f[kCPT], acc[kCPT];
-  const float* fm = a.fmap + ((size_t)b * a.C + c0) * P + p;
+  const float* fm = SAMPLE ? nullptr : a.fmap + ((size_t)b * a.C + c0) * P + p;
 #pragma unroll
   for (int c = 0; c < kCPT; ++c) {
-    f[c] = (c < cn) ? fm[(size_t)c * P] : 0.f;
+    f[c] = (!SAMPLE && c < cn) ? fm[(size_t)c * P] : 0.f;
     acc[c] = 0.f;
   }
   const int ps = pose_stride(a.pose_mode);
@@ -91,6 +96,10 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* _
         if (T.ok[1]) val += pl[T.idx[1]] * T.wgt[1];
         if (T.ok[2]) val += pl[T.idx[2]] * T.wgt[2];
         if (T.ok[3]) val += pl[T.idx[3]] * T.wgt[3];
+        if (SAMPLE) {
+          cost[(((size_t)n * a.B + b) * a.C + c0 + c) * P + p] = val;
+          continue;
+        }
         const float d = f[c] - val;
         if (a.reduce_mean) {
           acc[c] += d * d;
@@ -100,7 +109,7 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* _
       }
     }
   }
-  if (a.reduce_mean) {
+  if (!SAMPLE && a.reduce_mean) {
     float* out = cost + ((size_t)b * a.C + c0) * P + p;
     const float invN = (float)a.N;
 #pragma unroll
@@ -112,6 +121,8 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_kernel(WarpArgs a, float* _
 // ------------------------------------------------------------------ backward: feature side
 // d/dfmap, d/dfmap_ref (bilinear scatter, fp32 atomics) and the per-pixel
 // sampling-position gradient gxy[n,b,p] = sum_c dL/dwarped * dwarped/d(ix,iy).
+// SAMPLE: gcost is dL/dwarped [N,B,C,h,w] (view synthesis), no fmap.
+template <bool SAMPLE>
 __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
     WarpArgs a, const float* __restrict__ gcost, float* __restrict__ gfmap,
     float* __restrict__ gfref, float* __restrict__ gxy) {
@@ -137,20 +148,20 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
   const float scaleN = a.reduce_mean ? 1.f / (float)a.N : 1.f;
 
   float f[kCPT], gf[kCPT], g[kCPT];
-  const float* fm = a.fmap + ((size_t)b * a.C + cb) * P + pp;
+  const float* fm = SAMPLE ? nullptr : a.fmap + ((size_t)b * a.C + cb) * P + pp;
 #pragma unroll
   for (int c = 0; c < kCPT; ++c) {
-    f[c] = (c < cn) ? fm[(size_t)c * P] : 0.f;
+    f[c] = (!SAMPLE && c < cn) ? fm[(size_t)c * P] : 0.f;
     gf[c] = 0.f;
   }
-  if (a.reduce_mean) {
+  if (!SAMPLE && a.reduce_mean) {
     const float* gp = gcost + ((size_t)b * a.C + cb) * P + pp;
 #pragma unroll
     for (int c = 0; c < kCPT; ++c) g[c] = (c < cn) ? gp[(size_t)c * P] * scaleN : 0.f;
   }
   const int ps = pose_stride(a.pose_mode);
   for (int n = 0; n < a.N; ++n) {
-    if (!a.reduce_mean) {
+    if (SAMPLE || !a.reduce_mean) {
       const float* gp = gcost + (((size_t)n * a.B + b) * a.C + cb) * P + pp;
 #pragma unroll
       for (int c = 0; c < kCPT; ++c) g[c] = (c < cn) ? gp[(size_t)c * P] : 0.f;
@@ -161,6 +172,8 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
     project(ki, kr, R, t, u, v, depth, a.h, a.w, q);
     Taps T;
     bilinear_taps(q.ix, q.iy, a.h, a.w, T);
+    if (a.cells && blockIdx.y == 0 && wave == 0 && active)
+      a.cells[(size_t)(n * a.B + b) * P + p] = pack_cell(q.ix, q.iy);
     const float* fr = a.fmap_ref + (((size_t)n * a.B + b) * a.C + cb) * P;
     float* gr = gfref ? gfref + (((size_t)n * a.B + b) * a.C + cb) * P : nullptr;
     const float omy = 1.f - T.ty, omx = 1.f - T.tx;
@@ -174,9 +187,9 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
         const float v2 = T.ok[2] ? pl[T.idx[2]] : 0.f;
         const float v3 = T.ok[3] ? pl[T.idx[3]] : 0.f;
         const float val = v0 * T.wgt[0] + v1 * T.wgt[1] + v2 * T.wgt[2] + v3 * T.wgt[3];
-        const float gd = 2.f * (f[c] - val) * g[c];  // d cost / d fmap
+        const float gd = SAMPLE ? 0.f : 2.f * (f[c] - val) * g[c];  // d cost / d fmap
         gf[c] += gd;
-        const float gw = -gd;                         // d cost / d warped
+        const float gw = SAMPLE ? g[c] : -gd;         // d loss / d warped
         if (gr) {
           float* gpl = gr + (size_t)c * P;
           if (T.ok[0]) atomicAdd(gpl + T.idx[0], gw * T.wgt[0]);
@@ -206,7 +219,7 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
       __syncthreads();
     }
   }
-  if (gfmap) {
+  if (!SAMPLE && gfmap) {
     float* out = gfmap + ((size_t)b * a.C + cb) * P + pp;
 #pragma unroll
     for (int c = 0; c < kCPT; ++c)
@@ -388,6 +401,7 @@ static WarpArgs make_args(const float* fmap, const float* fmap_ref, const float*
                           int N, int C, int h, int w, int reduce_mean) {
   WarpArgs a;
   a.acc_fmap = 0;
+  a.cells = nullptr;
   a.fmap = fmap;
   a.fmap_ref = fmap_ref;
   a.depth = depth;
@@ -439,37 +453,28 @@ extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, c
                          pose, pose_mode, B, N, C, h, w, reduce_mean);
   const int P = h * w;
   dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
-  hipLaunchKernelGGL(warp_cost_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, cost);
+  hipLaunchKernelGGL(warp_cost_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a, cost);
   return launch_status("warp_cost_fwd_kernel launch failed");
 }
 
-extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float* depth,
-                                      int depth_mode, float min_disp, float max_disp,
-                                      const float* K, const float* ref_K, float scale,
-                                      const float* pose, int pose_mode, int B, int N, int C,
-                                      int h, int w, int reduce_mean, const float* grad_cost,
-                                      float* grad_fmap, float* grad_fmap_ref, float* grad_depth,
-                                      float* grad_pose, int accumulate, void* workspace,
-                                      void* stream) {
-  int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, N, C, h, w);
-  if (st) return st;
-  if (!depth || !grad_cost) {
-    set_error("warp_cost_backward: NULL depth/grad_cost");
-    return DRO_E_NULL;
-  }
+// shared backward of the cost (SAMPLE = false) and of view synthesis (true)
+template <bool SAMPLE>
+static int warp_backward(WarpArgs a, const float* grad_out, float* grad_fmap, float* grad_fmap_ref,
+                         float* grad_depth, float* grad_pose, int accumulate, void* workspace, int* cells,
+                         hipStream_t s) {
+  const int B = a.B, N = a.N, C = a.C, h = a.h, w = a.w;
   const bool geo = grad_depth || grad_pose;
   if (geo && !workspace) {
-    set_error("warp_cost_backward: workspace required for depth/pose gradients");
+    set_error("warp backward: workspace required for depth/pose gradients");
     return DRO_E_NULL;
   }
-  hipStream_t s = (hipStream_t)stream;
-  WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
-                         pose, pose_mode, B, N, C, h, w, reduce_mean);
   if (accumulate < 0 || accumulate > 3) {
-    set_error("warp_cost_backward: accumulate must be 0..3");
+    set_error("warp backward: accumulate must be 0..3");
     return DRO_E_MODE;
   }
+  int st;
   a.acc_fmap = accumulate & 1;
+  a.cells = cells;
   const int P = h * w;
   float* gxy = geo ? (float*)workspace : nullptr;
   const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
@@ -478,9 +483,9 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
       (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s)))
     return st;
   if (gxy && (st = launch_zero(gxy, (size_t)N * B * P * 2, s))) return st;
-  if (grad_fmap || grad_fmap_ref || gxy) {
+  if (grad_fmap || grad_fmap_ref || gxy || cells) {
     dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
-    hipLaunchKernelGGL(warp_cost_bwd_feat_kernel, grid, dim3(256), 0, s, a, grad_cost, grad_fmap,
+    hipLaunchKernelGGL(warp_cost_bwd_feat_kernel<SAMPLE>, grid, dim3(256), 0, s, a, grad_out, grad_fmap,
                        grad_fmap_ref, gxy);
     if ((st = launch_status("warp_cost_bwd_feat_kernel launch failed"))) return st;
   }
@@ -490,9 +495,70 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
     if ((st = launch_status("warp_cost_bwd_geo_kernel launch failed"))) return st;
   }
   if (grad_pose) {
-    if ((st = launch_pose_finalize(partial, nblk, N * B, pose, pose_mode, grad_pose, s))) return st;
+    if ((st = launch_pose_finalize(partial, nblk, N * B, a.pose, a.pose_mode, grad_pose, s))) return st;
   }
   return DRO_OK;
+}
+
+extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float* depth,
+                                      int depth_mode, float min_disp, float max_disp,
+                                      const float* K, const float* ref_K, float scale,
+                                      const float* pose, int pose_mode, int B, int N, int C,
+                                      int h, int w, int reduce_mean, const float* grad_cost,
+                                      float* grad_fmap, float* grad_fmap_ref, float* grad_depth,
+                                      float* grad_pose, int accumulate, void* workspace, int* cells,
+                                      void* stream) {
+  int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, N, C, h, w);
+  if (st) return st;
+  if (!depth || !grad_cost) {
+    set_error("warp_cost_backward: NULL depth/grad_cost");
+    return DRO_E_NULL;
+  }
+  WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
+                         pose, pose_mode, B, N, C, h, w, reduce_mean);
+  return warp_backward<false>(a, grad_cost, grad_fmap, grad_fmap_ref, grad_depth, grad_pose, accumulate,
+                              workspace, cells, (hipStream_t)stream);
+}
+
+extern "C" int dro_view_synthesis_forward(const float* ref_image, const float* depth, int depth_mode,
+                                          float min_disp, float max_disp, const float* K, const float* ref_K,
+                                          float scale, const float* pose, int pose_mode, int B, int N, int C,
+                                          int H, int W, float* warped, void* stream) {
+  // check_common wants a non-NULL fmap: view synthesis has none (ref_image stands in)
+  int st = check_common(ref_image, ref_image, K, ref_K, pose, pose_mode, B, N, C, H, W);
+  if (st) return st;
+  if (!depth || !warped) {
+    set_error("view_synthesis_forward: NULL depth/warped");
+    return DRO_E_NULL;
+  }
+  if (depth_mode < DRO_DEPTH_METRIC || depth_mode > DRO_DEPTH_DISP) {
+    set_error("view_synthesis_forward: unknown depth_mode");
+    return DRO_E_MODE;
+  }
+  WarpArgs a = make_args(nullptr, ref_image, depth, depth_mode, min_disp, max_disp, K, ref_K, scale, pose,
+                         pose_mode, B, N, C, H, W, 0);
+  const int P = H * W;
+  dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
+  hipLaunchKernelGGL(warp_cost_fwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a, warped);
+  return launch_status("warp_cost_fwd_kernel<sample> launch failed");
+}
+
+extern "C" int dro_view_synthesis_backward(const float* ref_image, const float* depth, int depth_mode,
+                                           float min_disp, float max_disp, const float* K, const float* ref_K,
+                                           float scale, const float* pose, int pose_mode, int B, int N, int C,
+                                           int H, int W, const float* grad_warped, float* grad_ref_image,
+                                           float* grad_depth, float* grad_pose, void* workspace, int* cells,
+                                           void* stream) {
+  int st = check_common(ref_image, ref_image, K, ref_K, pose, pose_mode, B, N, C, H, W);
+  if (st) return st;
+  if (!depth || !grad_warped) {
+    set_error("view_synthesis_backward: NULL depth/grad_warped");
+    return DRO_E_NULL;
+  }
+  WarpArgs a = make_args(nullptr, ref_image, depth, depth_mode, min_disp, max_disp, K, ref_K, scale, pose,
+                         pose_mode, B, N, C, H, W, 0);
+  return warp_backward<true>(a, grad_warped, nullptr, grad_ref_image, grad_depth, grad_pose, 0, workspace,
+                             cells, (hipStream_t)stream);
 }
 
 extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref, const float* disp,

@@ -4,6 +4,7 @@ Each Function checks dtype/device/shape up front (RuntimeError, as the
 reference's ATen ops would raise), allocates outputs through the caching
 allocator, and launches on the current stream.
 """
+import contextlib
 import ctypes
 
 import torch
@@ -115,10 +116,49 @@ def _sink_of(t):
     return getattr(t, "_dro_gsink", None)
 
 
+# ------------------------------------------------------------------------- bilinear-cell record
+class CellRecord:
+    """Test hook (parity tests only): the bilinear cell every warp's backward
+    used per pixel -- grid_sample's derivative is piecewise constant in the
+    sampling position and jumps where a coordinate crosses an integer, so an
+    fp32 and an fp64 evaluation can land on different branches.  Each op call
+    made inside record_bilinear_cells() allocates an int32 map (-1 = not
+    recorded) that its backward kernel fills (pack_cell, csrc/dro_common.hpp);
+    `calls` holds (tag, map) in forward call order."""
+
+    def __init__(self):
+        self.calls = []
+
+    def new(self, tag, shape, device):
+        cells = torch.full(shape, -1, dtype=torch.int32, device=device)
+        self.calls.append((tag, cells))
+        return cells
+
+
+_CELLS = [None]
+
+
+@contextlib.contextmanager
+def record_bilinear_cells():
+    """Record the bilinear cells of every warp_cost / photometric_loss /
+    view_synthesis backward run for ops called inside the block."""
+    prev = _CELLS[0]
+    _CELLS[0] = rec = CellRecord()
+    try:
+        yield rec
+    finally:
+        _CELLS[0] = prev
+
+
+def _cell_map(tag, shape, device):
+    rec = _CELLS[0]
+    return rec.new(tag, shape, device) if rec is not None and torch.is_grad_enabled() else None
+
+
 class _WarpCost(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale,
-                reduce_mean):
+                reduce_mean, tag):
         lib = _lib.load()
         require_device(fmap, fmap_ref, depth, K, ref_K, what="warp_cost")
         B, C, h, w = fmap.shape
@@ -141,6 +181,7 @@ class _WarpCost(torch.autograd.Function):
         ctx.sinks = sinks
         ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode, int(reduce_mean))
         ctx.restore = restore
+        ctx.cells = _cell_map(tag, (N, B, h, w), fmap.device)
         return cost
 
     @staticmethod
@@ -170,31 +211,33 @@ class _WarpCost(torch.autograd.Function):
         g_d = torch.empty_like(depth) if need[2] else None
         g_p = torch.empty_like(pose_flat) if need[3] else None
         ws = None
-        if g_d is not None or g_p is not None:
+        if g_d is not None or g_p is not None or ctx.cells is not None:
             nbytes = lib.dro_warp_cost_workspace_bytes(B, N, h, w)
             ws = torch.empty(nbytes // 4 + 1, device=fmap.device, dtype=torch.float32)
         check(lib.dro_warp_cost_backward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode,
                                          min_disp, max_disp, ptr(K), ptr(ref_K), scale,
                                          ptr(pose_flat), pose_mode, B, N, C, h, w, reduce_mean,
                                          ptr(gcost), ptr(g_f), ptr(g_r), ptr(g_d), ptr(g_p),
-                                         accumulate, ptr(ws), stream_of(fmap)), "dro_warp_cost_backward")
+                                         accumulate, ptr(ws), ptr(ctx.cells), stream_of(fmap)),
+              "dro_warp_cost_backward")
         if g_p is not None:
             g_p = ctx.restore(g_p)
         if sf is not None:
             g_f = None
         if sr is not None:
             g_r = None
-        return g_f, g_r, g_d, g_p, None, None, None, None, None, None, None
+        return g_f, g_r, g_d, g_p, None, None, None, None, None, None, None, None
 
 
 def warp_cost(fmap, fmap_ref, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_METRIC,
-              min_depth=None, max_depth=None, scale=1.0 / 8, reduce_mean=True):
+              min_depth=None, max_depth=None, scale=1.0 / 8, reduce_mean=True, tag=None):
     """Fused get_cost_each / depth_cost_calc (DepthPoseNet.py:76-105).
 
     fmap [B,C,h,w]; fmap_ref [N,B,C,h,w]; depth [B,1,h,w] encoded per depth_mode
     (DEPTH_DISP applies disp_to_depth(min_depth, max_depth) then inv2depth);
     pose [N,B,6] euler vectors or [N,B,3|4,4] matrices; K/ref_K full-res [B,3,3].
     Returns the mean cost over refs [B,C,h,w] (reduce_mean) or [N,B,C,h,w].
+    `tag` names the call in a record_bilinear_cells() record (tests).
     """
     if fmap_ref.dim() == 4:
         fmap_ref = fmap_ref.unsqueeze(0)
@@ -203,7 +246,65 @@ def warp_cost(fmap, fmap_ref, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_ME
     if depth_mode == DEPTH_DISP and (min_depth is None or max_depth is None):
         raise RuntimeError("warp_cost: DEPTH_DISP needs min_depth and max_depth")
     return _WarpCost.apply(fmap, fmap_ref, depth, pose, K, K if ref_K is None else ref_K,
-                           depth_mode, float(min_disp), float(max_disp), float(scale), reduce_mean)
+                           depth_mode, float(min_disp), float(max_disp), float(scale), reduce_mean, tag)
+
+
+class _ViewSynthesis(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ref_image, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale):
+        lib = _lib.load()
+        require_device(ref_image, depth, K, ref_K, what="view_synthesis")
+        N, B, C, H, W = ref_image.shape
+        if depth.shape != (B, 1, H, W) or K.shape != (B, 3, 3) or ref_K.shape != (B, 3, 3):
+            raise RuntimeError("view_synthesis: ref_image [N,B,C,H,W], depth [B,1,H,W], K/ref_K [B,3,3]")
+        pose_flat, pose_mode, restore = _pose_layout(pose, (N, B))
+        require_device(pose_flat, what="view_synthesis")
+        ref_image, depth, K, ref_K = ref_image.contiguous(), depth.contiguous(), K.contiguous(), ref_K.contiguous()
+        warped = torch.empty_like(ref_image)
+        check(lib.dro_view_synthesis_forward(ptr(ref_image), ptr(depth), depth_mode, min_disp, max_disp, ptr(K),
+                                             ptr(ref_K), scale, ptr(pose_flat), pose_mode, B, N, C, H, W,
+                                             ptr(warped), stream_of(ref_image)), "dro_view_synthesis_forward")
+        ctx.save_for_backward(ref_image, depth, pose_flat, K, ref_K)
+        ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode)
+        ctx.restore = restore
+        ctx.cells = _cell_map("view_synthesis", (N, B, H, W), ref_image.device)
+        return warped
+
+    @staticmethod
+    def backward(ctx, gw):
+        lib = _lib.load()
+        ref_image, depth, pose_flat, K, ref_K = ctx.saved_tensors
+        depth_mode, min_disp, max_disp, scale, pose_mode = ctx.cfg
+        N, B, C, H, W = ref_image.shape
+        need = ctx.needs_input_grad
+        g_r = torch.empty_like(ref_image) if need[0] else None
+        g_d = torch.empty_like(depth) if need[1] else None
+        g_p = torch.empty_like(pose_flat) if need[2] else None
+        ws = torch.empty(lib.dro_warp_cost_workspace_bytes(B, N, H, W) // 4 + 1, device=depth.device)
+        check(lib.dro_view_synthesis_backward(ptr(ref_image), ptr(depth), depth_mode, min_disp, max_disp, ptr(K),
+                                              ptr(ref_K), scale, ptr(pose_flat), pose_mode, B, N, C, H, W,
+                                              ptr(gw.contiguous()), ptr(g_r), ptr(g_d), ptr(g_p), ptr(ws),
+                                              ptr(ctx.cells), stream_of(depth)), "dro_view_synthesis_backward")
+        return g_r, g_d, (ctx.restore(g_p) if g_p is not None else None), None, None, None, None, None, None
+
+
+def view_synthesis(ref_image, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_METRIC, min_depth=None,
+                   max_depth=None, scale=1.0):
+    """view_synthesis (geometry/camera_utils.py:23-56) of N reference images in one
+    launch: ref_image [N,B,C,H,W] (or [B,C,H,W] for one view), depth [B,1,H,W]
+    in `depth_mode`, pose [N,B,6] euler vectors or [N,B,3|4,4] matrices (target
+    -> reference, Camera(ref_K, Tcw=pose)), K/ref_K [B,3,3] scaled by `scale`
+    (scale_intrinsics).  Returns the warped references, same shape as ref_image.
+    The kernels are the cost's (warp_cost_fwd/bwd_feat/bwd_geo in SAMPLE mode)."""
+    single = ref_image.dim() == 4
+    if single:
+        ref_image, pose = ref_image.unsqueeze(0), pose.unsqueeze(0)
+    if depth_mode == DEPTH_DISP and (min_depth is None or max_depth is None):
+        raise RuntimeError("view_synthesis: DEPTH_DISP needs min_depth and max_depth")
+    min_disp, max_disp = _disp_range(min_depth, max_depth)
+    out = _ViewSynthesis.apply(ref_image, depth, pose, K, K if ref_K is None else ref_K, depth_mode,
+                               float(min_disp), float(max_disp), float(scale))
+    return out[0] if single else out
 
 
 def plane_sweep_cost(fmap, fmap_ref, disp, pose, K, ref_K=None, *, min_depth, max_depth,
@@ -252,6 +353,7 @@ class _Photometric(torch.autograd.Function):
         ctx.save_for_backward(image, context, inv_depths, pose_flat, K, ref_K, ws)
         ctx.cfg = (pose_mode, opts)
         ctx.restore = restore
+        ctx.cells = _cell_map("photo", (N, n, B, H, W), image.device)
         metrics = out[1:].detach()
         # per-pixel argmin over the candidate maps (uint8 [n,B,H,W], the first
         # region of the workspace); exposed for parity tests
@@ -272,7 +374,7 @@ class _Photometric(torch.autograd.Function):
         check(lib.dro_photometric_backward(ptr(image), ptr(context), ptr(inv_depths), ptr(K),
                                            ptr(ref_K), ptr(pose_flat), pose_mode, B, N, n, H, W,
                                            ssim_w, C1, C2, smooth_w, automask, reduce_min,
-                                           ptr(gloss), ptr(g_inv), ptr(g_pose), ptr(ws),
+                                           ptr(gloss), ptr(g_inv), ptr(g_pose), ptr(ws), ptr(ctx.cells),
                                            stream_of(image)), "dro_photometric_backward")
         if g_pose is not None:
             g_pose = ctx.restore(g_pose)

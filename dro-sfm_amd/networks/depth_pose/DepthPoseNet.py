@@ -170,10 +170,10 @@ class DepthPoseNet(nn.Module):
         disps, masks = zip(*pairs)
         return list(hip.convex_upsample_many(list(disps), list(masks), ratio, affine=affine).unbind(0))
 
-    def _cost(self, fmap1, frefs, disp, poses, K, reduce_mean):
+    def _cost(self, fmap1, frefs, disp, poses, K, reduce_mean, tag=None):
         return hip.warp_cost(fmap1, frefs, disp, poses, K, depth_mode=self.depth_mode,
                              min_depth=self.min_depth, max_depth=self.max_depth,
-                             scale=1.0 / self.feat_ratio, reduce_mean=reduce_mean)
+                             scale=1.0 / self.feat_ratio, reduce_mean=reduce_mean, tag=tag)
 
     # ------------------------------------------------------------------ forward
     def forward(self, target_image, ref_imgs, intrinsics):
@@ -282,7 +282,7 @@ class DepthPoseNet(nn.Module):
             frozen_poses, frozen_disp = poses, disp
 
             def depth_block(h_d):
-                depth_cost = lambda d: self._cost(fmap1, frefs, d, frozen_poses, K, True)
+                depth_cost = lambda d: self._cost(fmap1, frefs, d, frozen_poses, K, True, ("depth", it))
                 h_d, masks, disps = self.update_block_depth(h_d, depth_cost, frozen_disp, x_d,
                                                             seq_len=self.seq_len)
                 keep = range(self.seq_len) if self.inter_sup else [self.seq_len - 1]
@@ -294,7 +294,7 @@ class DepthPoseNet(nn.Module):
             def pose_block(h_p):
                 # pose block over all N refs at once; depth frozen at this outer step
                 pose_cost = lambda q: self._cost(fmap1_p, frefs_p, frozen_disp, q.view(N, B, 6), K,
-                                                 False).view(N * B, C, h, w)
+                                                 False, ("pose", it)).view(N * B, C, h, w)
                 h_p, seq = self.update_block_pose(h_p, pose_cost, frozen_poses.reshape(N * B, 6), x_p,
                                                   seq_len=self.seq_len)
                 seq = seq if self.inter_sup else [seq[-1]]

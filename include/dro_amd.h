@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -84,7 +84,11 @@ size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w);
  * dro_warp_cost_workspace_bytes() bytes when grad_depth or grad_pose is set.
  * accumulate: bit 0 adds into grad_fmap, bit 1 into grad_fmap_ref (otherwise
  * they are overwritten) -- the feature maps are shared by every cost call of a
- * step, so their gradients can be summed in place (hip.grad_sink). */
+ * step, so their gradients can be summed in place (hip.grad_sink).
+ * cells (test hook, NULL in production): int32 [N,B,h,w] receives the bilinear
+ * cell each pixel's sampling position fell in, packed ((y0 + 32768) << 16) |
+ * (x0 + 32768) -- the branch of grid_sample's piecewise-linear derivative this
+ * backward took (parity tests hand it to the fp64 oracle). */
 int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float* depth,
                            int depth_mode, float min_disp, float max_disp,
                            const float* K, const float* ref_K, float scale,
@@ -92,7 +96,27 @@ int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float
                            int B, int N, int C, int h, int w, int reduce_mean,
                            const float* grad_cost, float* grad_fmap, float* grad_fmap_ref,
                            float* grad_depth, float* grad_pose, int accumulate, void* workspace,
-                           void* stream);
+                           int* cells, void* stream);
+
+/* View synthesis (geometry/camera_utils.py:23-56): the reference maps warped
+ * into the target view, warped[n,b] = grid_sample(ref_image[n,b],
+ * Camera(ref_K, Tcw=pose[n,b]).scaled(scale).project(Camera(K).scaled(scale)
+ * .reconstruct(depth[b]))), bilinear, zeros padding, align_corners=True.
+ *   ref_image [N,B,C,H,W]; depth [B,1,H,W] (depth_mode); pose [N,B,6|12];
+ *   warped [N,B,C,H,W].  The same kernels as the cost (one launch for all N).
+ * Backward: grad_ref_image (bilinear scatter, fp32 atomics), grad_depth (summed
+ * over the N views), grad_pose; any may be NULL.  workspace as
+ * dro_warp_cost_workspace_bytes(B, N, H, W); cells as in dro_warp_cost_backward. */
+int dro_view_synthesis_forward(const float* ref_image, const float* depth, int depth_mode,
+                               float min_disp, float max_disp, const float* K, const float* ref_K,
+                               float scale, const float* pose, int pose_mode, int B, int N, int C,
+                               int H, int W, float* warped, void* stream);
+int dro_view_synthesis_backward(const float* ref_image, const float* depth, int depth_mode,
+                                float min_disp, float max_disp, const float* K, const float* ref_K,
+                                float scale, const float* pose, int pose_mode, int B, int N, int C,
+                                int H, int W, const float* grad_warped, float* grad_ref_image,
+                                float* grad_depth, float* grad_pose, void* workspace, int* cells,
+                                void* stream);
 
 /* D fronto-parallel hypothesis planes (SURVEY.md §8(d) measurement extension):
  * for each plane d, depth = inv2depth(disp_to_depth(disp[d])) everywhere and
@@ -125,14 +149,18 @@ int dro_photometric_forward(const float* image, const float* context, const floa
                             float* out, void* workspace, void* stream);
 
 /* grad_out: device pointer to d(total)/d(loss) (1 float).  Writes
- * grad_inv_depths [n,B,1,H,W] and (if non-NULL) grad_pose [N,n,B,6|12]. */
+ * grad_inv_depths [n,B,1,H,W] and (if non-NULL) grad_pose [N,n,B,6|12].
+ * cells (test hook, NULL in production): int32 [N,n,B,H,W], the bilinear cell
+ * of every pixel's warp whose derivative this backward used (packed as in
+ * dro_warp_cost_backward; pixels of a (ref, tile) with no selected candidate
+ * are skipped and left as they were). */
 int dro_photometric_backward(const float* image, const float* context, const float* inv_depths,
                              const float* K, const float* ref_K, const float* pose, int pose_mode,
                              int B, int N, int n, int H, int W,
                              float ssim_w, float C1, float C2, float smooth_w,
                              int automask, int reduce_min,
                              const float* grad_out, float* grad_inv_depths, float* grad_pose,
-                             void* workspace, void* stream);
+                             void* workspace, int* cells, void* stream);
 
 /* ------------------------------------------------------------------------
  * Supervised depth + pose loss (sparse-l1).

@@ -107,23 +107,89 @@ def sample_grid(depth, K, ref_K, pose, scale):
     return torch.stack([u, v], -1).reshape(B, h, w, 2)
 
 
-def get_cost_each(pose, fmap, fmap_ref, depth, K, ref_K, scale):
+class Cells:
+    """Bilinear cells of a step's warps (test hook).  grid_sample's value is
+    continuous in the sampling position but its derivative jumps where a
+    coordinate crosses an integer: two evaluations of one step whose rounding
+    puts a coordinate on either side of a cell edge take different branches of
+    the (exact) piecewise-linear function.  `forced` maps a call key to an
+    int64 [B,h,w] tensor of packed cells ((y0 + 32768) << 16 | (x0 + 32768);
+    -1 = take the natural cell) that the sampler then uses, so the oracle is
+    evaluated on the branch another implementation took (the HIP kernels
+    record theirs: hip.record_bilinear_cells); with record=True the natural
+    cells of every call are kept in `recorded`.  Keys: ("depth", it, s, j),
+    ("pose", it, s, j), ("photo", j, i)."""
+
+    def __init__(self, forced=None, record=False):
+        self.forced = forced or {}
+        self.recorded = {} if record else None
+
+    def sample(self, img, grid, key):
+        return grid_sample_cells(img, grid, self.forced.get(key), self, key)
+
+
+def pack_cells(x0, y0):
+    """pack_cell (csrc/dro_common.hpp) of floor coordinates, int64."""
+    x0 = x0.clamp(-32767, 32766).long()
+    y0 = y0.clamp(-32767, 32766).long()
+    return ((y0 + 32768) << 16) | (x0 + 32768)
+
+
+def grid_sample_cells(img, grid, cells=None, book=None, key=None):
+    """F.grid_sample(img, grid, 'bilinear', 'zeros', align_corners=True), with
+    the bilinear cell of each output taken from `cells` where given (see
+    Cells).  Same unnormalisation as ATen (((g + 1) / 2) * (size - 1)), same
+    corner weights; out-of-image corners contribute zero."""
+    if cells is None and (book is None or book.recorded is None):
+        return F.grid_sample(img, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+    B, C, Hi, Wi = img.shape
+    ix = ((grid[..., 0] + 1) / 2) * (Wi - 1)
+    iy = ((grid[..., 1] + 1) / 2) * (Hi - 1)
+    x0, y0 = torch.floor(ix.detach()), torch.floor(iy.detach())
+    if book is not None and book.recorded is not None:
+        book.recorded[key] = pack_cells(x0, y0)
+    if cells is not None:
+        c = cells.to(torch.int64).reshape(x0.shape)
+        forced = c != -1
+        x0 = torch.where(forced, ((c & 0xFFFF) - 32768).to(x0.dtype), x0)
+        y0 = torch.where(forced, (((c >> 16) & 0xFFFF) - 32768).to(y0.dtype), y0)
+    tx, ty = ix - x0, iy - y0
+    flat = img.reshape(B, C, Hi * Wi)
+    out = 0.0
+    for dy, dx, wgt in ((0, 0, (1 - tx) * (1 - ty)), (0, 1, tx * (1 - ty)), (1, 0, (1 - tx) * ty),
+                        (1, 1, tx * ty)):
+        xx, yy = x0 + dx, y0 + dy
+        ok = (xx >= 0) & (xx <= Wi - 1) & (yy >= 0) & (yy <= Hi - 1)
+        idx = torch.where(ok, yy * Wi + xx, torch.zeros_like(xx)).long().reshape(B, 1, -1)
+        v = torch.gather(flat, 2, idx.expand(B, C, idx.shape[-1])).reshape(B, C, *ix.shape[1:])
+        out = out + v * (wgt * ok.to(wgt.dtype)).unsqueeze(1)
+    return out
+
+
+def get_cost_each(pose, fmap, fmap_ref, depth, K, ref_K, scale, cells=None, key=None):
     """DepthPoseNet.get_cost_each (networks/depth_pose/DepthPoseNet.py:76-96)."""
     grid = sample_grid(depth, K, ref_K, pose, scale)
-    warped = F.grid_sample(fmap_ref, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+    if cells is not None:
+        warped = cells.sample(fmap_ref, grid, key)
+    else:
+        warped = F.grid_sample(fmap_ref, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
     return (fmap - warped) ** 2
 
 
-def depth_cost_calc(inv_scaled, fmap, fmaps_ref, poses, K, ref_K, scale):
-    """DepthPoseNet.depth_cost_calc (DepthPoseNet.py:98-105): mean over refs."""
+def depth_cost_calc(inv_scaled, fmap, fmaps_ref, poses, K, ref_K, scale, cells=None, key=None):
+    """DepthPoseNet.depth_cost_calc (DepthPoseNet.py:98-105): mean over refs.
+    key (with `cells`): the call's key prefix, ref j appended."""
     depth = inv2depth(inv_scaled)
-    costs = [get_cost_each(p, fmap, f, depth, K, ref_K, scale) for p, f in zip(poses, fmaps_ref)]
+    costs = [get_cost_each(p, fmap, f, depth, K, ref_K, scale, cells, key + (j,) if key else None)
+             for j, (p, f) in enumerate(zip(poses, fmaps_ref))]
     return torch.stack(costs, 1).mean(1)
 
 
-def view_synthesis(ref_image, depth, pose, K, ref_K):
+def view_synthesis(ref_image, depth, pose, K, ref_K, cells=None, key=None):
     """geometry/camera_utils.py:23-56 at full resolution (scale 1)."""
     grid = sample_grid(depth, K, ref_K, pose, 1.0)
+    if cells is not None:
+        return cells.sample(ref_image, grid, key)
     return F.grid_sample(ref_image, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
 
 
@@ -175,17 +241,18 @@ def smoothness(inv_depths, image, smooth_w):
 
 def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_w=0.85, C1=1e-4,
                            C2=9e-4, smooth_w=0.001, automask=True, reduce="min",
-                           forced_selection=None):
+                           forced_selection=None, cells=None):
     """MultiViewPhotometricDecayLoss.forward (multiview_photometric_loss_mf.py:303-361).
 
     context: list of N [B,3,H,W]; inv_depths: list of n [B,1,H,W] (full res);
     poses[j][i]: euler [B,6] or transform [B,4,4] for ref j, prediction i.
+    cells: a Cells book (keys ("photo", j, i)) -- test hook.
     """
     n = len(inv_depths)
     per_pred = [[] for _ in range(n)]
     for j, ref in enumerate(context):
         for i in range(n):
-            est = view_synthesis(ref, inv2depth(inv_depths[i]), poses[j][i], K, ref_K)
+            est = view_synthesis(ref, inv2depth(inv_depths[i]), poses[j][i], K, ref_K, cells, ("photo", j, i))
             per_pred[i].append(photometric_map(est, image, ssim_w, C1, C2))
         if automask:
             unwarped = photometric_map(ref, image, ssim_w, C1, C2)
@@ -369,8 +436,10 @@ def parse_version(version):
                 out_norm="out" in version, inter="inter" in version)
 
 
-def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=True):
-    """DepthPoseNet.forward (DepthPoseNet.py:107-205)."""
+def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=True, cells=None):
+    """DepthPoseNet.forward (DepthPoseNet.py:107-205).  cells: a Cells book for
+    the cost warps (keys ("depth", it, s, j), ("pose", it, s, j)) -- test hook."""
+    import itertools
     cfg = parse_version(version)
     hd, cd, S = cfg["hdim"], 32, cfg["seq"]
     scale = (lambda x: disp_to_depth(x, min_depth, max_depth)) if cfg["out_norm"] else (lambda x: x)
@@ -388,11 +457,13 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
                            training)
     h_p = [torch.tanh(ctx_p[B * j:B * (j + 1), :hd]) for j in range(N)]
     x_p = [torch.relu(ctx_p[B * j:B * (j + 1), hd:hd + cd]) for j in range(N)]
-    for _ in range(cfg["outer"]):
+    for it in range(cfg["outer"]):
         inv = inv.detach()
         poses = [q.detach() for q in poses]
         depth_fixed = inv2depth(scale(inv))
-        cost_d = lambda x, ps=poses: depth_cost_calc(x, fmap1, frefs, ps, K, K, 1.0 / 8)
+        sd = itertools.count()
+        cost_d = lambda x, ps=poses, it=it, sd=sd: depth_cost_calc(x, fmap1, frefs, ps, K, K, 1.0 / 8, cells,
+                                                                  ("depth", it, next(sd)))
         h_d, masks, invs = update_block_depth(p, "update_block_depth.", h_d, cost_d, inv, x_d, S,
                                               scale)
         sel = range(S) if cfg["inter"] else [S - 1]
@@ -401,7 +472,9 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
         inv = invs[-1]
         new_poses = []
         for j in range(N):
-            cost_p = lambda q, j=j: get_cost_each(q, fmap1, frefs[j], depth_fixed, K, K, 1.0 / 8)
+            sp = itertools.count()
+            cost_p = lambda q, j=j, it=it, sp=sp: get_cost_each(q, fmap1, frefs[j], depth_fixed, K, K, 1.0 / 8,
+                                                                cells, ("pose", it, next(sp), j))
             h_p[j], seqs = update_block_pose(p, "update_block_pose.", h_p[j], cost_p, poses[j],
                                              x_p[j], S)
             new_poses.append(seqs if cfg["inter"] else [seqs[-1]])
@@ -423,7 +496,7 @@ def flip_lr_intr(K, width):
 
 
 def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", loss_kw=None,
-                    forced_selection=None, flip=False, pred_perturb=None):
+                    forced_selection=None, flip=False, pred_perturb=None, cells=None):
     """SelfSupModelMF / SupModelMF .forward in training mode
     (models/SfmModelMF.py:106-189, SelfSupModelMF.py:63-99, SupModelMF.py:78-119).
 
@@ -445,7 +518,7 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
     if flip:
         K = flip_lr_intr(K, img.shape[3])
         img, refs = img.flip(3), [r.flip(3) for r in refs]
-    invs, pvec = depth_pose_net(p, version, min_depth, max_depth, img, refs, K, training=True)
+    invs, pvec = depth_pose_net(p, version, min_depth, max_depth, img, refs, K, training=True, cells=cells)
     if flip:
         invs = [d.flip(3) for d in invs]
     if pred_perturb is not None:
@@ -458,7 +531,7 @@ def train_step_loss(p, version, min_depth, max_depth, batch, kind="selfsup", los
     poses = [[pvec[:, j, i] for i in range(n)] for j in range(N)]
     if kind == "selfsup":
         out = photometric_decay_loss(batch["rgb_original"], batch["rgb_context_original"], invs, K,
-                                     K, poses, forced_selection=forced_selection, **loss_kw)
+                                     K, poses, forced_selection=forced_selection, cells=cells, **loss_kw)
     else:
         gt_inv = torch.where(batch["depth"] <= 0, torch.zeros_like(batch["depth"]),
                              1.0 / batch["depth"].clamp(min=1e-6))

@@ -158,10 +158,72 @@ def test_warp_cost_rejects_bad_input(hip):
         hip.warp_cost(d["fmap"].double(), d["fmap_ref"], d["depth"], d["pose"], d["K"])
 
 
+# ------------------------------------------------------------------ view synthesis (warped images)
+def test_view_synthesis_golden(hip):
+    """view_synthesis (geometry/camera_utils.py:23-56) -- the warped reference
+    image the photometric loss compares -- on the reference's fixture (B=2,
+    48x160): the warped image at 1e-4 against the reference's own output;
+    gradients of sum(warped * G) w.r.t. depth and pose at 1e-4 against the
+    fp64 oracle on the kernel's bilinear cells, and against the reference's
+    within 1e-4 max|ref| + |ref - x64| per element."""
+    d = fx("view_synthesis")
+    depth, pose = d["depth"].clone().requires_grad_(True), d["pose"].clone().requires_grad_(True)
+    with hip.record_bilinear_cells() as rec:
+        warped = hip.view_synthesis(d["ref"], depth, pose, d["K"])
+        (warped * d["G"]).sum().backward()
+    assert warped.shape == d["warped"].shape
+    assert rel(warped, d["warped"]) < TOL
+    (tag, cells), = rec.calls
+    assert tag == "view_synthesis" and bool((cells != -1).all())
+    c64 = {k: d[k].cpu().double() for k in ("ref", "depth", "pose", "K", "G")}
+    dd, pp = c64["depth"].clone().requires_grad_(True), c64["pose"].clone().requires_grad_(True)
+    out = O.view_synthesis(c64["ref"], dd, pp, c64["K"], c64["K"], O.Cells(forced={"v": cells[0].cpu().long()}), "v")
+    assert rel(warped.double(), out) < TOL
+    (out * c64["G"]).sum().backward()
+    assert rel(depth.grad.double(), dd.grad) < TOL
+    assert rel(pose.grad.double(), pp.grad) < TOL
+    for got, x64, ref in ((depth.grad, dd.grad, d["g_depth"]), (pose.grad, pp.grad, d["g_pose"])):
+        got, ref = got.double().cpu(), ref.double().cpu()
+        bound = TOL * ref.abs().max() + (ref - x64).abs()
+        assert bool(((got - ref).abs() <= bound).all()), float(((got - ref).abs() - bound).max())
+
+
+def test_view_synthesis_kitti_size_vs_oracle(hip):
+    """Metric-config warp: B=2, 192x640, N=2 reference images in one launch,
+    inverse-depth input (the photometric loss's encoding, inv2depth in-kernel),
+    euler poses.  Warped images 1e-4 against the fp64 oracle; gradients of
+    sum(warped * G) w.r.t. the inverse depth (summed over both views), the
+    poses and the reference images 1e-4 against the fp64 oracle on the
+    kernel's bilinear cells."""
+    g = torch.Generator().manual_seed(21)
+    B, N, H, W = 2, 2, 192, 640
+    K = kitti_K(B)
+    refs = torch.stack([smooth_images(B, H, W, 61 + j, detail=0.3) for j in range(N)])
+    inv = torch.nn.functional.interpolate(0.02 + 0.3 * torch.rand(B, 1, H // 8, W // 8, generator=g),
+                                          size=(H, W), mode="bilinear", align_corners=False)
+    vec = torch.cat([0.1 * torch.randn(N, B, 3, generator=g), 0.02 * torch.randn(N, B, 3, generator=g)], 2)
+    G = torch.randn(N, B, 3, H, W, generator=g)
+    rg, ig, vg = (t.to(DEV).requires_grad_(True) for t in (refs, inv, vec))
+    with hip.record_bilinear_cells() as rec:
+        warped = hip.view_synthesis(rg, ig, vg, K.to(DEV), depth_mode=hip.DEPTH_INV)
+        (warped * G.to(DEV)).sum().backward()
+    cells = rec.calls[0][1].cpu().long()
+    r64, i64, v64 = (t.double().requires_grad_(True) for t in (refs, inv, vec))
+    outs = [O.view_synthesis(r64[j], O.inv2depth(i64), v64[j], K.double(), K.double(),
+                             O.Cells(forced={j: cells[j]}), j) for j in range(N)]
+    out64 = torch.stack(outs)
+    assert rel(warped.double(), out64) < TOL
+    (out64 * G.double()).sum().backward()
+    assert rel(ig.grad.double(), i64.grad) < TOL
+    assert rel(vg.grad.double(), v64.grad) < TOL
+    assert rel(rg.grad.double(), r64.grad) < TOL
+
+
 # ------------------------------------------------------------------ photometric loss
-def _oracle_photometric(d, dt, forced_selection=None):
+def _oracle_photometric(d, dt, forced_selection=None, cells=None):
     """Oracle loss and gradients on the fixture inputs in dtype dt; with
-    forced_selection the min reduction takes the given candidates."""
+    forced_selection the min reduction takes the given candidates, with cells
+    (cells_from_record) the warps take the given bilinear cells."""
     invs = [i.cpu().to(dt).requires_grad_(True) for i in d["inv_depths"]]
     vecs = d["poses"].cpu().to(dt).requires_grad_(True)
     N, n = vecs.shape[1], vecs.shape[2]
@@ -170,7 +232,8 @@ def _oracle_photometric(d, dt, forced_selection=None):
                                    d["K"].cpu().to(dt), d["K"].cpu().to(dt), poses,
                                    automask=bool(int(d["automask"])),
                                    reduce="min" if int(d["reduce_min"]) else "mean",
-                                   forced_selection=forced_selection)
+                                   forced_selection=forced_selection,
+                                   cells=O.Cells(forced=cells) if cells is not None else None)
     out["loss"].sum().backward()
     return torch.stack([i.grad for i in invs]).double(), vecs.grad.double(), out["loss"].detach().double()
 
@@ -182,58 +245,57 @@ def test_photometric_loss_golden(hip, name):
     smoothness: 1e-4.  Gradients: EVERY element of the reference's
     g_inv_depths and g_poses, nothing excluded:
 
-        |hip - ref| <= 1e-4 max|ref| + |ref - x64| + kink
-                       (+ 2 |x32 - x64| for g_inv)
+        |hip - ref| <= 1e-4 max|ref| + |ref - x64|   (+ 2 |x32 - x64| for g_inv)
 
-    x64 / x32: the oracle in fp64 / fp32 taking the kernel's min-selection.
-    |ref - x64| is the reference's own measured distance from the exact
-    gradient of that selection (its fp32 rounding, plus -- where the kernel
-    resolved a near-tied min differently -- the exact effect of that choice;
-    the selection may differ from the fp64 minimum only where the loss moves by
-    <= 1e-9 relative, asserted).  `kink` (tests/photo_kinks.py) bounds the
-    pixels whose warp coordinate lies within fp32 rounding (2x the fixture's
-    measured coordinate error) of a grid line, where the bilinear derivative
-    jumps: found as the cause of the round-2 photo_loss_mean and round-3
-    photo_loss_noauto pose deviations (reproduced to 1 %).  The inverse-depth
-    map also gets twice the fp32 oracle's own per-pixel error: SSIM's
-    E[x^2]-E[x]^2 on smooth 3x3 windows cancels in any fp32 evaluation."""
-    import photo_kinks
+    x64 / x32: the oracle in fp64 / fp32 on the kernel's branch -- its
+    min-selection and the bilinear cell of every warped pixel the backward
+    used (hip.record_bilinear_cells): at a coordinate within rounding of a
+    grid line grid_sample's derivative jumps, and fp32/fp64 evaluations can
+    land on either side.  |ref - x64| is the reference's own distance from
+    the exact gradient on that branch (its fp32 rounding, and the exact effect
+    of a different cell or near-tied selection; the selection may differ from
+    the fp64 minimum only where the loss moves by <= 1e-9 relative, asserted).
+    The inverse-depth map also gets twice the fp32 oracle's own per-pixel
+    error: SSIM's E[x^2]-E[x]^2 on smooth 3x3 windows cancels in any fp32
+    evaluation.  And the kernel against the exact gradient of its own branch:
+    pose 1e-4 of max|x64|."""
     d = fx(name)
     invs = d["inv_depths"].clone().requires_grad_(True)           # [n,B,1,H,W]
     vec = d["poses"].clone().requires_grad_(True)                 # [B,N,n,6]
     pose = vec.permute(1, 2, 0, 3)                                # [N,n,B,6]
-    loss, metrics, sel = hip.photometric_loss(d["image"], d["context"], invs, pose, d["K"],
-                                              automask=bool(int(d["automask"])),
-                                              reduce_min=bool(int(d["reduce_min"])),
-                                              return_selection=True)
+    with hip.record_bilinear_cells() as rec:
+        loss, metrics, sel = hip.photometric_loss(d["image"], d["context"], invs, pose, d["K"],
+                                                  automask=bool(int(d["automask"])),
+                                                  reduce_min=bool(int(d["reduce_min"])),
+                                                  return_selection=True)
+        loss.sum().backward()
+    cells = cells_from_record(rec)
     assert rel(loss, d["loss"]) < TOL
     assert rel(metrics[1], d["smoothness_loss"]) < TOL
-    loss.sum().backward()
     forced = None
     if int(d["reduce_min"]):
         forced = sel.cpu().unsqueeze(2)
         _, _, l64_free = _oracle_photometric(d, torch.float64)
         _, _, l64_forced = _oracle_photometric(d, torch.float64, forced)
         assert float(l64_forced - l64_free) <= 1e-9 * float(l64_free), "selection differs beyond near-ties"
-    gi64, gp64, _ = _oracle_photometric(d, torch.float64, forced)
-    gi32, _, _ = _oracle_photometric(d, torch.float32, forced)
-    kink_p, kink_i, _, _ = photo_kinks.gridline_allowance(d, forced)
+    gi64, gp64, _ = _oracle_photometric(d, torch.float64, forced, cells)
+    gi32, _, _ = _oracle_photometric(d, torch.float32, forced, cells)
     ref_i, ref_p = d["g_inv_depths"].double().cpu(), d["g_poses"].double().cpu()
     got_i, got_p = invs.grad.double().cpu(), vec.grad.double().cpu()
-    bound_p = TOL * ref_p.abs().max() + (ref_p - gp64).abs() + kink_p
-    bound_i = TOL * ref_i.abs().max() + (ref_i - gi64).abs() + 2 * (gi32 - gi64).abs() + kink_i
+    bound_p = TOL * ref_p.abs().max() + (ref_p - gp64).abs()
+    bound_i = TOL * ref_i.abs().max() + (ref_i - gi64).abs() + 2 * (gi32 - gi64).abs()
     ep, ei = (got_p - ref_p).abs(), (got_i - ref_i).abs()
     assert bool((ep <= bound_p).all()), ("pose", float((ep - bound_p).max()), float(ep.max() / ref_p.abs().max()))
     assert bool((ei <= bound_i).all()), ("inv", float((ei - bound_i).max()), int((ei > bound_i).sum()))
-    # and the kernel against the exact gradient of its own selection
-    assert bool(((got_p - gp64).abs() <= TOL * gp64.abs().max() + kink_p).all())
+    assert rel(got_p, gp64) <= TOL, rel(got_p, gp64)
 
 
 def test_photometric_loss_kitti_size_vs_oracle(hip):
     """Metric-config loss: B=2, 192x640, n_pred=9, N=2, automask + min.
 
-    The oracle takes the kernel's per-pixel min selection (forced_selection),
-    so near-tied pixels cannot pick different candidates in two fp32 orders.
+    The oracle takes the kernel's per-pixel min selection (forced_selection)
+    and bilinear cells (record_bilinear_cells), so near-tied pixels and
+    coordinates at grid lines cannot take different branches.
     Loss scalar: 1e-4.  Gradients: relative L2 1e-4 against the fp64 oracle,
     and max-rel within 4x the oracle's own fp32 max-rel: SSIM's E[x^2]-E[x]^2
     on smooth 3x3 windows cancels, so the reference algorithm itself is
@@ -246,9 +308,11 @@ def test_photometric_loss_kitti_size_vs_oracle(hip):
     invs = 0.02 + 0.3 * torch.rand(n, B, 1, H, W, generator=g)
     vec = torch.cat([0.1 * torch.randn(B, N, n, 3, generator=g), 0.02 * torch.randn(B, N, n, 3, generator=g)], 3)
     ig, vg = invs.to(DEV).requires_grad_(True), vec.to(DEV).requires_grad_(True)
-    loss, metrics, sel = hip.photometric_loss(image.to(DEV), ctx.to(DEV), ig, vg.permute(1, 2, 0, 3),
-                                              K.to(DEV), return_selection=True)
-    loss.sum().backward()
+    with hip.record_bilinear_cells() as rec:
+        loss, metrics, sel = hip.photometric_loss(image.to(DEV), ctx.to(DEV), ig, vg.permute(1, 2, 0, 3),
+                                                  K.to(DEV), return_selection=True)
+        loss.sum().backward()
+    book = lambda: O.Cells(forced=cells_from_record(rec))
     free = O.photometric_decay_loss(image, list(ctx), list(invs), K, K,
                                     [[vec[:, j, i] for i in range(n)] for j in range(N)])
     assert rel(loss, free["loss"]) < TOL                     # un-forced oracle: same scalar
@@ -258,7 +322,7 @@ def test_photometric_loss_kitti_size_vs_oracle(hip):
         vc = vec.to(dt).detach().clone().requires_grad_(True)
         out = O.photometric_decay_loss(image.to(dt), list(ctx.to(dt)), list(ic), K.to(dt), K.to(dt),
                                        [[vc[:, j, i] for i in range(n)] for j in range(N)],
-                                       forced_selection=sel.cpu().unsqueeze(2))
+                                       forced_selection=sel.cpu().unsqueeze(2), cells=book())
         out["loss"].sum().backward()
         ref[dt] = (out, ic.grad.double(), vc.grad.double())
     out64, gi64, gv64 = ref[torch.float64]
@@ -386,30 +450,39 @@ def test_depth_pose_net_golden(hip, tag, version):
         assert rel(pose_e, d["poses_eval"]) < 1e-3
 
 
-def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=False, perturb=False,
-                  want_preds=False, seed=99, pred_perturb=None):
+def cells_from_record(rec):
+    """hip.record_bilinear_cells() record -> the oracle's Cells keys:
+    ("depth", it, s, j) / ("pose", it, s, j) -> [B,h,w], ("photo", j, i) ->
+    [B,H,W] (int64 on the CPU).  The product calls each tag once per inner
+    step s, in order; one call covers every reference view j."""
+    out, steps = {}, {}
+    for tag, cells in rec.calls:
+        c = cells.cpu().to(torch.int64)
+        if tag == "photo":
+            for j in range(c.shape[0]):
+                for i in range(c.shape[1]):
+                    out[("photo", j, i)] = c[j, i]
+        elif isinstance(tag, tuple):
+            s_ = steps.get(tag, 0)
+            steps[tag] = s_ + 1
+            for j in range(c.shape[0]):
+                out[(tag[0], tag[1], s_, j)] = c[j]
+    return out
+
+
+def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=False, cells=None,
+                  want_preds=False):
     """Oracle loss and parameter gradients (and, want_preds, the net's
-    predictions (inv_depths [n,B,1,H,W], poses [B,N,n,6])).  perturb (True =
-    1e-7, or a relative scale): the images and K moved by a seeded relative
-    Gaussian -- the gradient's change under it measures how far an fp32
-    evaluation of this step may land from another at that distance (kinks of
-    the loss: min selection, L1 signs, bilinear cell edges, smoothness signs;
-    amplified by the recurrence)."""
+    predictions (inv_depths [n,B,1,H,W], poses [B,N,n,6])), on the branch
+    given by the min-selection `forced` and the bilinear cells `cells` (a dict
+    of cells_from_record, or None for the natural ones)."""
     p = params_from_spec(spec)
     p = {k: (v.to(dt).requires_grad_(True) if v.is_floating_point() and "running" not in k
              else (v.to(dt) if v.is_floating_point() else v)) for k, v in p.items()}
     b = {k: (v.to(dt) if torch.is_tensor(v) and v.is_floating_point() else
              ([t.to(dt) for t in v] if isinstance(v, list) else v)) for k, v in batch.items()}
-    if perturb:
-        s = 1e-7 if perturb is True else float(perturb)
-        g = torch.Generator().manual_seed(seed)
-        jig = lambda t: t * (1 + s * torch.randn(t.shape, generator=g, dtype=t.dtype))
-        for key in ("rgb", "rgb_original", "intrinsics"):
-            b[key] = jig(b[key])
-        for key in ("rgb_context", "rgb_context_original"):
-            b[key] = [jig(t) for t in b[key]]
-    out = O.train_step_loss(p, version, mind, maxd, b, kind=kind, forced_selection=forced, flip=flip,
-                            pred_perturb=pred_perturb)
+    book = O.Cells(forced=cells) if cells is not None else None
+    out = O.train_step_loss(p, version, mind, maxd, b, kind=kind, forced_selection=forced, flip=flip, cells=book)
     out["loss"].sum().backward()
     grads = {k: v.grad for k, v in p.items() if getattr(v, "grad", None) is not None}
     if want_preds:
@@ -421,129 +494,53 @@ def _l2(a, b):
     return float((a.double().cpu() - b.double().cpu()).norm() / b.double().cpu().norm())
 
 
-def _matched_sensitivity(model, out, preds64, oracle_args, cap=1e-5, seeds=(99, 100, 101)):
-    """The fp64 gradient's change between two points as far apart as THIS
-    evaluation's forward pass is from fp64.
-
-    The photometric loss has derivative jumps (bilinear cell edges where a
-    warped coordinate crosses an integer, L1 and smoothness signs): the
-    gradient is piecewise smooth, and on small images a few pixels crossing a
-    cell edge move a pose gradient by percents (view5 fixture, fp64 oracle:
-    input perturbation 1e-7 -> gradient L2 change 2.3e-5; 1e-6 -> 4.3e-3, dL/dpose
-    of one ref by 11 %).  Where an fp32 forward lands within that band is
-    rounding, not parity.  So: measure the forward distance d_hip of the HIP
-    predictions (inverse depths and poses, relative L2) from the fp64 oracle's,
-    measure the fp64 oracle's own prediction move d0 under a 1e-7 input
-    perturbation, and evaluate the fp64 gradient at a perturbation scaled to
-    1e-7 * d_hip / d0 (capped at `cap`, which also bounds what this allowance
-    can ever absorb), once per seed: each sample crosses a different set of
-    kinks, and the checks take the largest change per tensor.  An input
-    perturbation moves every activation smoothly; an fp32 forward's rounding
-    does not, so three more samples evaluate the loss at the fp64
-    predictions moved by relative noise of HIP's measured prediction distance
-    (inverse depths and poses separately), backpropagated through the exact
-    net (oracle train_step_loss pred_perturb).  Returns ([gsens...], info)."""
-    inv_h = torch.stack([d.detach() for d in out["inv_depths"]]).double().cpu()
-    pv = getattr(out.get("poses"), "vec", None)
-    pose_h = pv.detach().double().cpu() if pv is not None else None
-    args, kw = oracle_args
-    _, _, (inv_p, pose_p) = _oracle_grads(*args, perturb=1e-7, want_preds=True, **kw)
-    d_inv = _l2(inv_h, preds64[0])
-    d_pose = _l2(pose_h, preds64[1]) if pose_h is not None else 0.0
-    d_hip = max(d_inv, d_pose)
-    d0 = max(_l2(inv_p, preds64[0]), _l2(pose_p, preds64[1]) if pose_h is not None else 0.0)
-    scale = min(cap, 1e-7 * max(1.0, d_hip / max(d0, 1e-30)))
-    gs = [_oracle_grads(*args, perturb=scale, seed=sd, **kw)[1] for sd in seeds]
-    # the loss evaluated at predictions moved as far as HIP's are from fp64
-    # (straight-through to the exact net): the loss's own derivative jumps
-    pp = (min(cap, d_inv), min(cap, d_pose))
-    gs += [_oracle_grads(*args, pred_perturb=(pp[0], pp[1], sd), **kw)[1] for sd in seeds]
-    return gs, {"d_hip": d_hip, "d_inv": d_inv, "d_pose": d_pose, "d0_1e-7": d0, "scale": scale}
+# Train-step gradient bounds (round 4): fixed, against the fp64 oracle evaluated
+# on the SAME branch of the loss as the kernels -- the min-reprojection
+# selection (forced_selection) and every warp's bilinear cells
+# (hip.record_bilinear_cells -> O.Cells) -- so that fp32-vs-fp64 rounding
+# across a cell edge or a near-tie cannot move the reference gradient.  No term
+# depends on the product's own run-to-run spread or on the fp32 oracle.
+GRAD_TENSOR_TOL = 1e-3     # per tensor: max|hip - fp64| / max|fp64|
+GRAD_L2_TOL = 1e-4         # the whole gradient: relative L2
 
 
-def _hip_spread(model, batch, flip=None, runs=2):
-    """Per-tensor max relative difference between the parameter gradients of
-    this step (already back-propagated into `model`) and those of `runs`
-    re-runs of the SAME step (same parameters, a fresh copy of the same batch).
-    MIOpen's forward convolutions (the encoders' stride-2 entries) are not
-    run-to-run deterministic (1.9e-6 forward spread, tools/diag_determinism2.py),
-    and at the fixtures' bilinear cell-edge kinks that spread alone moved one
-    tensor of the flipped it8 step by 4 % in one of three runs -- a property
-    of this point of the function under fp32 rounding, measured on the product
-    itself.  Re-runs whose min-reprojection selection differs from the first
-    run's (the oracle is pinned to that one) are not compared.  Returns
-    {name: spread}."""
-    named = [(k, p) for k, p in model.depth_net.named_parameters() if p.grad is not None]
-    g0 = {k: p.grad.detach().clone() for k, p in named}
-    loss_mod = getattr(model, "_photometric_loss", None)
-    sel0 = loss_mod.last_selection.clone() if loss_mod is not None and loss_mod.last_selection is not None else None
-    spread = {k: 0.0 for k in g0}
-    for _ in range(runs):
-        b = {k: (v.clone() if torch.is_tensor(v) else [t.clone() for t in v]) for k, v in batch.items()}
-        for _, p in named:
-            p.grad = None
-        out = model(b, flip=flip) if flip is not None else model(b)
-        out["loss"].sum().backward()
-        if sel0 is not None and not torch.equal(loss_mod.last_selection, sel0):
-            continue
-        for k, p in named:
-            spread[k] = max(spread[k], rel(p.grad, g0[k]))
-    for k, p in named:                      # leave the first run's gradients in place
-        p.grad = g0[k]
-    return spread
+def _grad_check(model, g64, tensor_tol=GRAD_TENSOR_TOL, l2_tol=GRAD_L2_TOL):
+    """Every parameter gradient within tensor_tol (max-rel over its elements) of
+    the fp64 oracle on the kernels' branch, and the whole gradient within
+    l2_tol in relative L2.  Returns (offenders, l2)."""
+    named = [(k, v.grad) for k, v in model.depth_net.named_parameters() if k in g64 and v.grad is not None]
+    den = sum(float(g64[k].double().pow(2).sum()) for k, _ in named)
+    num = sum(float((g.double().cpu() - g64[k].double()).pow(2).sum()) for k, g in named)
+    l2 = (num / den) ** 0.5
+    bad = [(k, e) for k, g in named for e in [rel(g, g64[k])] if e > tensor_tol]
+    if l2 > l2_tol:
+        bad.append(("<global L2>", l2))
+    return sorted(bad, key=lambda t: -t[1]), l2
 
 
-def _grad_check(model, g64, g32, floor_mult=16.0, abs_floor=2e-3, gsens=None, spread=None):
-    """Every parameter gradient within max(abs_floor, floor_mult x the fp32
-    oracle's own distance to fp64 for that tensor, 4 x the fp32 oracle's
-    global relative L2 distance, 4 x the fp64 gradient's largest change under
-    the input perturbations gsens (_matched_sensitivity)) of the fp64 oracle (per tensor, max-rel over
-    every element); the global relative L2 error of the whole gradient within
-    max(abs_floor, 8x the fp32 oracle's, 4x the perturbation's).  The global
-    term matters where the step is ill-conditioned in fp32 (the flipped it8
-    fixture: the fp32 oracle itself is 2e-3 off fp64 in L2, its error sitting
-    on other tensors than any other fp32 evaluation's).
-    Returns (offenders, ok_global, info)."""
-    names = [k for k, v in model.depth_net.named_parameters() if k in g64 and v.grad is not None]
-    grads = dict(model.depth_net.named_parameters())
-    den = sum(float(g64[k].double().pow(2).sum()) for k in names)
-    num = sum(float((grads[k].grad.double().cpu() - g64[k].double()).pow(2).sum()) for k in names)
-    num32 = sum(float((g32[k].double() - g64[k].double()).pow(2).sum()) for k in names)
-    l2, l2_32 = (num / den) ** 0.5, (num32 / den) ** 0.5
-    gsens = [] if gsens is None else (gsens if isinstance(gsens, list) else [gsens])
-    l2_s = max([(sum(float((g[k].double() - g64[k].double()).pow(2).sum()) for k in names) / den) ** 0.5
-                for g in gsens] or [0.0])
-    bad = []
-    for k in names:
-        e = rel(grads[k].grad, g64[k])
-        tol = max(abs_floor, floor_mult * rel(g32[k], g64[k]), 4 * l2_32,
-                  *[4 * rel(g[k], g64[k]) for g in gsens], 4 * (spread or {}).get(k, 0.0))
-        if e > tol:
-            bad.append((k, e, tol))
-    return bad, l2 <= max(abs_floor, 8.0 * l2_32, 4.0 * l2_s), (l2, l2_32, l2_s)
-
-
-def _fixture_check(model, fixture, g64, g32, floor_mult=16.0, abs_floor=2e-3, gsens=None, spread=None):
+def _fixture_check(model, fixture, g64, tensor_tol=GRAD_TENSOR_TOL):
     """Per tensor, over the reference fixture's stored elements (whole tensors
     or a fixed 2048-entry sample): max|HIP - reference| / max|reference| within
-    the distance of the reference to the fp64 oracle (same min-selection as
-    HIP) plus max(abs_floor, floor_mult x the fp32 oracle's own max-rel) -- the
-    reference is compared directly, and may differ only by what its own fp32
-    rounding and this build's bound explain."""
+    tensor_tol plus the fp64 oracle's own distance to the reference on the
+    kernels' branch (the exact function differs from the reference's fp32 run
+    where that run's cells or selection differ: a computed quantity, not a
+    measured spread)."""
     named = [(k, v.grad) for k, v in model.depth_net.named_parameters() if v.grad is not None]
-    den = sum(float(g64[k].double().pow(2).sum()) for k, _ in named if k in g64)
-    l2_32 = (sum(float((g32[k].double() - g64[k].double()).pow(2).sum()) for k, _ in named if k in g64)
-             / den) ** 0.5
     e_hip = grad_errors(named, fixture)
     e_ref = grad_errors(list(g64.items()), fixture)        # reference vs exact
-    gsens = [] if gsens is None else (gsens if isinstance(gsens, list) else [gsens])
-    bad = []
-    for k, e in e_hip.items():
-        tol = e_ref[k] + max(abs_floor, floor_mult * rel(g32[k], g64[k]), 4 * l2_32,
-                             *[4 * rel(g[k], g64[k]) for g in gsens], 4 * (spread or {}).get(k, 0.0))
-        if e > tol:
-            bad.append((k, e, tol))
-    return bad, e_hip
+    bad = [(k, e, e_ref[k] + tensor_tol) for k, e in e_hip.items() if e > e_ref[k] + tensor_tol]
+    return bad, e_hip, e_ref
+
+
+def _run_step(model, batch, flip=None):
+    """One training forward + backward of the product with its bilinear cells
+    recorded; returns (out, cells dict)."""
+    import dro_sfm_amd.hip as H
+    with H.record_bilinear_cells() as rec:
+        out = model(batch, flip=flip) if flip is not None else model(batch)
+        out["loss"].sum().backward()
+    torch.cuda.synchronize()
+    return out, cells_from_record(rec)
 
 
 def _selfsup_model(mind, maxd, tag, version):
@@ -570,13 +567,12 @@ def test_train_step_golden(hip, tag, version, kind, flip):
     """SelfSupModelMF / SupModelMF training step on the reference's golden inputs,
     without and with the left-right flip forced (SfmModelMF.py:110-119: the
     net sees flipped images and the flipped K, the loss the flipped K).
-    Loss scalar: 1e-4 vs the reference.  Parameter gradients, per element:
-    (1) vs the fp64 oracle taking the kernel's min-selection, per tensor
-    within max(2e-3, 16x the fp32 oracle's own error), global L2 within
-    max(2e-3, 8x); (2) directly vs the reference's per-element fixture
-    (_fixture_check).  The factor covers fp32 convolution rounding amplified
-    by the recurrent loop; the allowance also holds the step's own
-    run-to-run spread (_hip_spread: MIOpen's forward is not deterministic)."""
+    Loss scalar: 1e-4 vs the reference.  Predictions within 1e-4 (relative L2)
+    of the fp64 oracle's.  Parameter gradients, per element: (1) vs the fp64
+    oracle on the kernels' branch (their min-selection and bilinear cells),
+    every tensor within GRAD_TENSOR_TOL and the whole gradient within
+    GRAD_L2_TOL -- fixed bounds; (2) directly vs the reference's per-element
+    fixture (_fixture_check)."""
     d = fx(f"train_step_{tag}")
     f = fx(f"train_step_{tag}_{'flip' if flip else 'grads'}")
     dn = fx(f"depthposenet_{tag}")
@@ -588,27 +584,21 @@ def test_train_step_golden(hip, tag, version, kind, flip):
              "depth": d["gt_depth"], "pose_context": [d["gt_poses"][:, j] for j in range(N)]}
     cpu_batch = {k: (v.cpu().clone() if torch.is_tensor(v) else [t.cpu() for t in v]) for k, v in batch.items()}
     model = (_selfsup_model if kind == "selfsup" else _sup_model)(mind, maxd, tag, version)
-    out = model(batch, flip=flip)
+    out, cells = _run_step(model, batch, flip)
     assert rel(out["loss"], f["loss"]) < TOL
     if flip:
         assert torch.equal(batch["intrinsics"].cpu(), f["K_after"].cpu())   # mutated in place
-    out["loss"].sum().backward()
     forced = None
     if kind == "selfsup":
         forced = model._photometric_loss.last_selection.cpu().unsqueeze(2)
-    b0 = {k: (v.clone() if torch.is_tensor(v) else [t.clone() for t in v]) for k, v in cpu_batch.items()}
-    spread = _hip_spread(model, {k: (v.to(DEV) if torch.is_tensor(v) else [t.to(DEV) for t in v])
-                                 for k, v in b0.items()}, flip)
-    args = (spec, version, mind, maxd, cpu_batch, kind, torch.float64, forced, flip)
-    _, g64, p64 = _oracle_grads(*args, want_preds=True)
-    _, g32, p32 = _oracle_grads(*args[:6], torch.float32, forced, flip, want_preds=True)
-    gs, sinfo = _matched_sensitivity(model, out, p64, (args, {}))
-    sinfo["d_o32"] = _l2(p32[0], p64[0])
-    assert sinfo["d_hip"] < 1e-4, sinfo                   # the forward itself: fp32-close
-    bad, ok, info = _grad_check(model, g64, g32, gsens=gs, spread=spread)
-    assert not bad and ok, (bad[:5], info, sinfo)
-    fbad, _ = _fixture_check(model, {k: v.cpu() for k, v in f.items()}, g64, g32, gsens=gs, spread=spread)
-    assert not fbad, (fbad[:5], sinfo)
+    _, g64, p64 = _oracle_grads(spec, version, mind, maxd, cpu_batch, kind, torch.float64, forced, flip, cells,
+                                want_preds=True)
+    d_hip = _l2(torch.stack([d.detach() for d in out["inv_depths"]]), p64[0])
+    assert d_hip < 1e-4, d_hip                               # the forward itself: fp32-close
+    bad, l2 = _grad_check(model, g64)
+    assert not bad, (bad[:5], l2)
+    fbad, _, _ = _fixture_check(model, {k: v.cpu() for k, v in f.items()}, g64)
+    assert not fbad, fbad[:5]
 
 
 def _scannet_K(B, W=320, H=240):
@@ -630,20 +620,17 @@ def test_train_step_view5_n4_golden(hip):
              "rgb_context_original": list(f["refs"]), "intrinsics": f["K"].clone()}
     cpu_batch = {k: (v.cpu().clone() if torch.is_tensor(v) else [t.cpu() for t in v]) for k, v in batch.items()}
     model = _selfsup_model(mind, maxd, "it12h", "it12-h-out")
-    out = model(batch)
+    out, cells = _run_step(model, batch)
     assert rel(out["loss"], f["loss"]) < TOL
-    out["loss"].sum().backward()
     forced = model._photometric_loss.last_selection.cpu().unsqueeze(2)
-    args = (spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float64, forced)
-    _, g64, p64 = _oracle_grads(*args, want_preds=True)
-    _, g32, p32 = _oracle_grads(*args[:6], torch.float32, forced, want_preds=True)
-    gs, sinfo = _matched_sensitivity(model, out, p64, (args, {}))
-    sinfo["d_o32"] = _l2(p32[0], p64[0])
-    assert sinfo["d_hip"] < 1e-4, sinfo
-    bad, ok, info = _grad_check(model, g64, g32, gsens=gs)
-    assert not bad and ok, (bad[:5], info, sinfo)
-    fbad, _ = _fixture_check(model, {k: v.cpu() for k, v in f.items()}, g64, g32, gsens=gs)
-    assert not fbad, (fbad[:5], sinfo)
+    _, g64, p64 = _oracle_grads(spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float64, forced,
+                                False, cells, want_preds=True)
+    d_hip = _l2(torch.stack([d.detach() for d in out["inv_depths"]]), p64[0])
+    assert d_hip < 1e-4, d_hip
+    bad, l2 = _grad_check(model, g64)
+    assert not bad, (bad[:5], l2)
+    fbad, _, _ = _fixture_check(model, {k: v.cpu() for k, v in f.items()}, g64)
+    assert not fbad, fbad[:5]
 
 
 @pytest.mark.parametrize("kind", ["selfsup_view5", "sup_view3"])
@@ -671,18 +658,13 @@ def test_train_step_scannet_size_vs_oracle(hip, kind):
                                  for _ in range(N)]
     model = (_selfsup_model if kind == "selfsup_view5" else _sup_model)(mind, maxd, "it12h", "it12-h-out")
     gb = {k: (v.to(DEV) if torch.is_tensor(v) else [t.to(DEV) for t in v]) for k, v in batch.items()}
-    out = model(gb)
-    out["loss"].sum().backward()
+    out, cells = _run_step(model, gb)
     forced = model._photometric_loss.last_selection.cpu().unsqueeze(2) if kind == "selfsup_view5" else None
     okind = "selfsup" if kind == "selfsup_view5" else "sup"
-    loss64, g64 = _oracle_grads(spec, "it12-h-out", mind, maxd, batch, okind, torch.float64, forced)
-    loss32, g32 = _oracle_grads(spec, "it12-h-out", mind, maxd, batch, okind, torch.float32, forced)
-    # the untrained it12-h recurrence at 240x320 is ill-conditioned in fp32: the
-    # fp32 oracle's own loss sits ~3.5e-4 from fp64 (sup_view3), so the loss
-    # bound is max(1e-4, 4x that measured distance)
-    assert rel(out["loss"], loss64) < max(TOL, 4 * rel(loss32, loss64))
-    bad, ok, info = _grad_check(model, g64, g32)
-    assert not bad and ok, (bad[:5], info)
+    loss64, g64 = _oracle_grads(spec, "it12-h-out", mind, maxd, batch, okind, torch.float64, forced, False, cells)
+    assert rel(out["loss"], loss64) < TOL
+    bad, l2 = _grad_check(model, g64)
+    assert not bad, (bad[:5], l2)
 
 
 def test_train_step_kitti_metric_config(hip):
@@ -699,11 +681,10 @@ def test_train_step_kitti_metric_config(hip):
              "intrinsics": K}
     model = _selfsup_model(0.5, 80.0, "it8", "it8-seq4-inter-out")
     gb = {k: (v.to(DEV) if torch.is_tensor(v) else [t.to(DEV) for t in v]) for k, v in batch.items()}
-    out = model(gb)
-    out["loss"].sum().backward()
+    out, cells = _run_step(model, gb)
     forced = model._photometric_loss.last_selection.cpu().unsqueeze(2)
-    loss64, g64 = _oracle_grads(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", torch.float64, forced)
-    _, g32 = _oracle_grads(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", torch.float32, forced)
+    loss64, g64 = _oracle_grads(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", torch.float64, forced,
+                                False, cells)
     assert rel(out["loss"], loss64) < TOL
-    bad, ok, info = _grad_check(model, g64, g32)
-    assert not bad and ok, (bad[:5], info)
+    bad, l2 = _grad_check(model, g64)
+    assert not bad, (bad[:5], l2)

@@ -335,3 +335,40 @@ def test_pose_metrics():
     d = load_fixture(os.path.join(G, "metrics_pose.npz"))
     for k in range(d["gt"].shape[0]):
         assert torch.equal(O.pose_metrics(d["gt"][k], d["pred"][k]), d["metrics"][k]), k
+
+
+def test_grid_sample_cells_matches_aten():
+    """The oracle's forced-cell bilinear sampler (O.Cells, the parity tests'
+    branch pinning): with the natural cells recorded and forced back it equals
+    F.grid_sample (bilinear, zeros, align_corners=True) in value and in both
+    gradients; at a sampling coordinate exactly on a grid line, forcing the
+    cell to the left neighbour keeps the value and switches the x-derivative
+    to the left cell's slope."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(0)
+    img = torch.randn(2, 5, 12, 20, generator=g, dtype=torch.float64)
+    grid = torch.rand(2, 12, 20, 2, generator=g, dtype=torch.float64) * 2.4 - 1.2
+    rec = O.Cells(record=True)
+    ga, gb = grid.clone().requires_grad_(True), grid.clone().requires_grad_(True)
+    ia, ib = img.clone().requires_grad_(True), img.clone().requires_grad_(True)
+    a = F.grid_sample(ia, ga, mode="bilinear", padding_mode="zeros", align_corners=True)
+    assert torch.allclose(rec.sample(img, grid, "k"), a, atol=1e-12)
+    b = O.Cells(forced={"k": rec.recorded["k"]}).sample(ib, gb, "k")
+    assert torch.allclose(a, b, atol=1e-12)
+    a.sum().backward()
+    b.sum().backward()
+    assert torch.allclose(ga.grad, gb.grad, atol=1e-10) and torch.allclose(ia.grad, ib.grad, atol=1e-12)
+    # one output exactly on the grid line x = 7: natural cell x0 = 7, forced x0 = 6
+    one = img[:1, :1]
+    gx = torch.tensor([[[[2 * 7 / 19 - 1, 2 * 4.25 / 11 - 1]]]], dtype=torch.float64, requires_grad=True)
+    nat = O.Cells(record=True)
+    v_nat = nat.sample(one, gx, "p")
+    c = nat.recorded["p"].clone()
+    c = c - 1                                           # x0 + 32768 - 1: the left cell
+    v_left = O.Cells(forced={"p": c}).sample(one, gx, "p")
+    assert torch.allclose(v_nat, v_left, atol=1e-12)
+    d_nat = torch.autograd.grad(nat.sample(one, gx, "p").sum(), gx)[0][..., 0]
+    d_left = torch.autograd.grad(O.Cells(forced={"p": c}).sample(one, gx, "p").sum(), gx)[0][..., 0]
+    r = one[0, 0, 4] * 0.75 + one[0, 0, 5] * 0.25      # the row interpolated at y = 4.25
+    assert torch.allclose(d_nat, (r[8] - r[7]) * 19 / 2, atol=1e-10)
+    assert torch.allclose(d_left, (r[7] - r[6]) * 19 / 2, atol=1e-10)
