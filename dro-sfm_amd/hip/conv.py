@@ -43,6 +43,7 @@ afresh) and the split buffers are saved for the backward.
 """
 import contextlib
 import ctypes
+from typing import Optional
 
 import torch
 
@@ -353,89 +354,140 @@ def _dense_out(srcs, C):
     return torch.empty(B, C, H, W, device=srcs[0].device, dtype=torch.float32)
 
 
-class _Conv2d(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, weight, bias, act, alpha, scope, direct, nsrc, *rest):
-        lib = _lib.load()
-        srcs = rest[:nsrc]
-        require_device(weight, bias, *srcs, what="conv2d")
-        Cout, Cin, KH, KW = weight.shape
-        if sum(s.shape[1] for s in srcs) != Cin:
-            raise RuntimeError("conv2d: source channels do not add up to the weight's Cin")
-        B, _, H, W = srcs[0].shape
-        weight = weight.contiguous()
-        out = _dense_out(srcs, Cout)
-        ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, out.device)
-        wf, wb = _wsplit(weight)
-        check(lib.dro_conv2d_forward(_slices(srcs), len(srcs), ptr(weight), ptr(bias), B, H, W, Cout, KH, KW,
-                                     act, ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(wf), ptr(ws), nws,
-                                     stream_of(out)), "dro_conv2d_forward")
-        ctx.wsplit = wb
-        ctx.save_for_backward(weight, out if act else None, *srcs)
-        ctx.sinks = [_sink_of(x) for x in srcs]
-        ctx.meta = (act, alpha, bias is not None)
-        ctx.scope = scope
-        ctx.direct = direct
-        ctx.nrest = len(rest) - nsrc
-        return out
+Tensor = torch.Tensor
+_LAST_WSPLIT = []   # split-bf16 backward copy of the weight a forward op made (xconv engine), for its setup
 
-    @staticmethod
-    def backward(ctx, gout):
-        lib = _lib.load()
-        weight, y, *srcs = ctx.saved_tensors
-        act, alpha, has_bias = ctx.meta
-        Cout, Cin, KH, KW = weight.shape
-        B, _, H, W = srcs[0].shape
-        need = ctx.needs_input_grad
-        gout = gout.contiguous()
-        # sources with a gradient sink are written in place (and get None)
-        sinks = [s if need[7 + i] else None for i, s in enumerate(ctx.sinks)]
-        gsrc = [torch.empty(B, s.shape[1], H, W, device=gout.device) if need[7 + i] and sinks[i] is None
-                else None for i, s in enumerate(srcs)]
-        sk = [s.target() if s is not None else (None, 0) for s in sinks]
-        tgt = [t if s is not None else g for (t, _), s, g in zip(sk, sinks, gsrc)]
-        dacc = [a for _, a in sk]
-        ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
-        if ctx.direct is not None:
-            # data gradients here, weight gradients on the side stream into .grad
-            gw, gb = ctx.direct[2], ctx.direct[3]
-            ptrs, ctot, coff = _grad_targets(tgt)
-            acc = (ctypes.c_int * len(srcs))(*dacc)
-            if any(g is not None for g in tgt):
-                ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
-                check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
-                                              act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                              ptr(gout), ptrs, ctot, coff, acc, None, None, 0, ptr(ctx.wsplit),
-                                              ptr(ws), nws, stream_of(gout)), "dro_conv2d_backward(data)")
-            if _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None):
-                return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
-            ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
-            check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
-                                          act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                          ptr(gout), None, None, None, None, ptr(gw),
-                                          ptr(gb) if has_bias else None, 1, None, ptr(ws), nws,
-                                          stream_of(gout)), "dro_conv2d_backward(weight)")
-            return (None, None, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
-        want_w = need[0] or (has_bias and need[1])
-        if want_w:
-            gw, gb, wacc, first = _grad_buffers(ctx.scope, ("conv", weight.data_ptr(), Cout),
-                                                weight, Cout if has_bias else 0, gout.device)
-        else:
-            gw, gb, wacc, first = None, None, 0, False
-        ptrs, ctot, coff = _grad_targets(tgt)
-        acc = (ctypes.c_int * len(srcs))(*dacc)
-        ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, gout.device)
-        check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW,
-                                      act, ctypes.c_float(alpha), ctypes.byref(ys) if ys else None,
-                                      ptr(gout), ptrs, ctot, coff, acc, ptr(gw), ptr(gb), wacc, ptr(ctx.wsplit),
-                                      ptr(ws), nws, stream_of(gout)), "dro_conv2d_backward")
-        rw = gw if (first and need[0]) else None
-        rb = gb if (first and has_bias and need[1]) else None
-        return (rw, rb, None, None, None, None, None, *gsrc, *([None] * ctx.nrest))
+
+def _placeholder(t, device):
+    return t if t is not None else torch.empty(0, device=device)
+
+
+# ------------------------------------------------------------------ dro::conv2d_backward (data + weight gradients)
+@torch.library.custom_op("dro::conv2d_backward", mutates_args=("grad_srcs", "grad_weight", "grad_bias"))
+def _conv2d_bwd_op(srcs: list[Tensor], weight: Tensor, y: Optional[Tensor], grad_out: Tensor, act: int,
+                   alpha: float, grad_srcs: list[Tensor], accumulate: list[int], grad_weight: Optional[Tensor],
+                   grad_bias: Optional[Tensor], weight_accumulate: int, wsplit: Optional[Tensor]) -> None:
+    """Gradients of act(conv(cat(srcs), weight) + b) * alpha: the data gradient of
+    source i into grad_srcs[i] (empty = not wanted; accumulate[i] = 1 adds),
+    the weight (+ bias) gradient into grad_weight / grad_bias (added when
+    weight_accumulate).  y: the saved output when act != none (its derivative
+    is folded into the staging).  One launch per gradient kind."""
+    lib = _lib.load()
+    Cout, Cin, KH, KW = weight.shape
+    B, _, H, W = srcs[0].shape
+    tgt = [g if g.numel() else None for g in grad_srcs]
+    ys = DroSlice(y.data_ptr(), Cout, Cout, 0, 0) if y is not None else None
+    ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, grad_out.device)
+    ptrs, ctot, coff = _grad_targets(tgt) if any(t is not None for t in tgt) else (None, None, None)
+    acc = (ctypes.c_int * len(srcs))(*accumulate) if ptrs is not None else None
+    if ptrs is None and grad_weight is None:
+        return
+    check(lib.dro_conv2d_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, Cout, KH, KW, act,
+                                  ctypes.c_float(alpha), ctypes.byref(ys) if ys else None, ptr(grad_out.contiguous()),
+                                  ptrs, ctot, coff, acc, ptr(grad_weight), ptr(grad_bias), weight_accumulate,
+                                  ptr(wsplit), ptr(ws), nws, stream_of(grad_out)), "dro_conv2d_backward")
+
+
+@_conv2d_bwd_op.register_fake
+def _(srcs, weight, y, grad_out, act, alpha, grad_srcs, accumulate, grad_weight, grad_bias, weight_accumulate,
+      wsplit):
+    return None
+
+
+def _conv_bwd(srcs, weight, y, gout, act, alpha, tgt, dacc, gw=None, gb=None, wacc=0, wsplit=None):
+    dev = gout.device
+    torch.ops.dro.conv2d_backward(list(srcs), weight, y, gout, act, float(alpha),
+                                  [_placeholder(t, dev) for t in tgt], [int(a) for a in dacc], gw, gb, int(wacc),
+                                  wsplit)
+
+
+# ------------------------------------------------------------------ dro::conv2d
+@torch.library.custom_op("dro::conv2d", mutates_args=())
+def _conv2d_op(srcs: list[Tensor], weight: Tensor, bias: Optional[Tensor], act: int, alpha: float,
+               params: list[Tensor], nweight: int) -> Tensor:
+    """act(conv2d(cat(srcs, 1), weight, bias, stride 1, padding k//2)) * alpha
+    without materialising the concatenation (each source: NCHW, a channel
+    slice of one, or a [B,C,1,1] map expanded over H x W).  params: the
+    parameters weight/bias are the fused flat-buffer views of when the
+    trainer's in-place weight gradients apply (params[:nweight] weights,
+    the rest biases), else empty."""
+    lib = _lib.load()
+    require_device(weight, bias, *srcs, what="conv2d")
+    Cout, Cin, KH, KW = weight.shape
+    if sum(t.shape[1] for t in srcs) != Cin:
+        raise RuntimeError("conv2d: source channels do not add up to the weight's Cin")
+    B, _, H, W = srcs[0].shape
+    weight = weight.contiguous()
+    out = _dense_out(srcs, Cout)
+    ws, nws = _workspace(B, H, W, Cin, Cout, KH, KW, out.device)
+    wf, wb = _wsplit(weight)
+    check(lib.dro_conv2d_forward(_slices(srcs), len(srcs), ptr(weight), ptr(bias), B, H, W, Cout, KH, KW, act,
+                                 ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(wf), ptr(ws), nws, stream_of(out)),
+          "dro_conv2d_forward")
+    _LAST_WSPLIT[:] = [wb]
+    return out
+
+
+@_conv2d_op.register_fake
+def _(srcs, weight, bias, act, alpha, params, nweight):
+    B, _, H, W = srcs[0].shape
+    return srcs[0].new_empty((B, weight.shape[0], H, W))
+
+
+def _conv2d_setup(ctx, inputs, output):
+    srcs, weight, bias, act, alpha, params, nweight = inputs
+    ctx.wsplit = _LAST_WSPLIT.pop() if _LAST_WSPLIT else None
+    ctx.save_for_backward(weight.contiguous(), output if act else None, *srcs)
+    ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in srcs]
+    ctx.need_src = [x.requires_grad for x in srcs]
+    ctx.meta = (act, alpha, bias is not None, weight.requires_grad, bias is not None and bias.requires_grad)
+    ctx.direct = _direct_targets(params[:nweight], params[nweight:], mark=False) if params else None
+    ctx.scope = None if params else current_scope()
+    ctx.nparams = len(params)
+
+
+def _conv2d_backward(ctx, gout):
+    weight, y, *srcs = ctx.saved_tensors
+    act, alpha, has_bias, need_w, need_b = ctx.meta
+    Cout, Cin, KH, KW = weight.shape
+    B, _, H, W = srcs[0].shape
+    gout = gout.contiguous()
+    # sources with a gradient sink are written in place (and get None)
+    sinks = ctx.sinks
+    gsrc = [torch.empty(B, x.shape[1], H, W, device=gout.device) if ctx.need_src[i] and sinks[i] is None
+            else None for i, x in enumerate(srcs)]
+    sk = [sn.target() if sn is not None else (None, 0) for sn in sinks]
+    tgt = [t if sn is not None else g for (t, _), sn, g in zip(sk, sinks, gsrc)]
+    dacc = [a for _, a in sk]
+    none_params = [None] * ctx.nparams
+    if ctx.direct is not None:
+        # data gradients here; the weight gradients in place into the flat .grad
+        # views, queued for one batched launch per weight (or launched now)
+        gw, gb = ctx.direct[2], ctx.direct[3]
+        if any(g is not None for g in tgt):
+            _conv_bwd(srcs, weight, y, gout, act, alpha, tgt, dacc, wsplit=ctx.wsplit)
+        if not _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None):
+            _conv_bwd(srcs, weight, y, gout, act, alpha, [None] * len(srcs), [0] * len(srcs), gw,
+                      gb if has_bias else None, 1)
+        return gsrc, None, None, None, None, none_params, None
+    want_w = need_w or (has_bias and need_b)
+    if want_w:
+        gw, gb, wacc, first = _grad_buffers(ctx.scope, ("conv", weight.data_ptr(), Cout),
+                                            weight, Cout if has_bias else 0, gout.device)
+    else:
+        gw, gb, wacc, first = None, None, 0, False
+    _conv_bwd(srcs, weight, y, gout, act, alpha, tgt, dacc, gw, gb, wacc, ctx.wsplit)
+    rw = gw if (first and need_w) else None
+    rb = gb if (first and has_bias and need_b) else None
+    return gsrc, rw, rb, None, None, none_params, None
+
+
+torch.library.register_autograd("dro::conv2d", _conv2d_backward, setup_context=_conv2d_setup)
 
 
 def conv2d(srcs, weight, bias=None, act=None, alpha=1.0, parts=None):
-    """act(conv2d(cat(srcs, 1), weight, bias, padding=k//2)) * alpha on f32 MFMA.
+    """act(conv2d(cat(srcs, 1), weight, bias, padding=k//2)) * alpha on f32 MFMA
+    (torch.ops.dro.conv2d).
 
     parts=(weights, biases): the weight/bias are the dim-0 concatenation of these
     parameters (weight/bias may then be None: built here, as a flat-buffer view
@@ -447,230 +499,241 @@ def conv2d(srcs, weight, bias=None, act=None, alpha=1.0, parts=None):
     wparts, bparts = parts
     direct = _direct_targets(wparts, bparts)
     if direct is not None:
-        params = [*wparts, *bparts]
-        return _Conv2d.apply(direct[0], direct[1], ACT[act], float(alpha), None, direct, len(srcs),
-                             *srcs, *params)
+        return torch.ops.dro.conv2d(list(srcs), direct[0], direct[1], ACT[act], float(alpha),
+                                    [*wparts, *bparts], len(wparts))
     if weight is None:
         key = ("cat",) + tuple(id(p) for p in wparts)
         weight, bias = cached_cat(key, lambda: (torch.cat(list(wparts), 0),
                                                 torch.cat(list(bparts), 0) if bparts else None))
-    return _Conv2d.apply(weight, bias, ACT[act], float(alpha), current_scope(), None, len(srcs), *srcs)
+    return torch.ops.dro.conv2d(list(srcs), weight, bias, ACT[act], float(alpha), [], 0)
 
 
-class _Conv2dStrided(torch.autograd.Function):
-    """act(conv2d(x, weight, bias, stride, padding)) on the flattened implicit
-    GEMM (csrc/conv.hip dro_conv2d_strided_*): the encoders' stride-2 (and any
-    non-'same') convolutions.  Backward supports act none only (BatchNorm
-    follows every such conv in the encoders)."""
+# ------------------------------------------------------------------ dro::conv2d_strided
+@torch.library.custom_op("dro::conv2d_strided", mutates_args=())
+def _conv2d_strided_op(x: Tensor, weight: Tensor, bias: Optional[Tensor], stride: int, pad: int,
+                       act: int) -> Tensor:
+    """act(F.conv2d(x, weight, bias, stride, pad)) on the flattened implicit GEMM
+    (csrc/conv.hip dro_conv2d_strided_*): the encoders' stride-2 convs."""
+    lib = _lib.load()
+    require_device(x, weight, bias, what="conv2d_strided")
+    B, Cin, Hi, Wi = x.shape
+    Cout, cin_w, KH, KW = weight.shape
+    if cin_w != Cin:
+        raise RuntimeError("conv2d_strided: input channels do not match the weight")
+    Ho, Wo = (Hi + 2 * pad - KH) // stride + 1, (Wi + 2 * pad - KW) // stride + 1
+    x, weight = x.contiguous(), weight.contiguous()
+    out = torch.empty(B, Cout, Ho, Wo, device=x.device, dtype=torch.float32)
+    nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
+    check(lib.dro_conv2d_strided_forward(ptr(x), ptr(weight), ptr(bias), B, Hi, Wi, Cin, Cout, KH, KW, stride, pad,
+                                         act, ptr(out), ptr(ws), nws, stream_of(out)), "dro_conv2d_strided_forward")
+    return out
 
-    @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, act, direct):
-        lib = _lib.load()
-        require_device(x, weight, bias, what="conv2d_strided")
-        B, Cin, Hi, Wi = x.shape
-        Cout, cin_w, KH, KW = weight.shape
-        if cin_w != Cin:
-            raise RuntimeError("conv2d_strided: input channels do not match the weight")
-        Ho, Wo = (Hi + 2 * pad - KH) // stride + 1, (Wi + 2 * pad - KW) // stride + 1
-        x, weight = x.contiguous(), weight.contiguous()
-        out = torch.empty(B, Cout, Ho, Wo, device=x.device, dtype=torch.float32)
-        nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
-        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
-        check(lib.dro_conv2d_strided_forward(ptr(x), ptr(weight), ptr(bias), B, Hi, Wi, Cin, Cout, KH, KW, stride,
-                                             pad, act, ptr(out), ptr(ws), nws, stream_of(out)),
-              "dro_conv2d_strided_forward")
-        ctx.save_for_backward(x, weight)
-        ctx.meta = (stride, pad, act, bias is not None, direct)
-        return out
 
-    @staticmethod
-    def backward(ctx, gout):
-        lib = _lib.load()
-        x, weight = ctx.saved_tensors
-        stride, pad, act, has_bias, direct = ctx.meta
-        if act:
-            raise RuntimeError("conv2d_strided: backward through a fused activation is not supported")
-        B, Cin, Hi, Wi = x.shape
-        Cout, _, KH, KW = weight.shape
-        need = ctx.needs_input_grad
-        gout = gout.contiguous()
-        gx = torch.empty_like(x) if need[0] else None
-        if direct is not None:                 # in place into the trainer's flat .grad views
-            gw, gb, wacc = direct[2], direct[3] if has_bias else None, 1
-        else:
-            gw = torch.empty_like(weight) if need[1] else None
-            gb = torch.empty(Cout, device=x.device) if (has_bias and need[2]) else None
-            wacc = 0
-        if gw is None and gb is not None:
-            gw = torch.empty_like(weight)
-        nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
-        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
-        check(lib.dro_conv2d_strided_backward(ptr(x), ptr(weight), ptr(gout), B, Hi, Wi, Cin, Cout, KH, KW, stride,
-                                              pad, ptr(gx), 0, ptr(gw), ptr(gb), wacc, ptr(ws), nws,
-                                              stream_of(gout)), "dro_conv2d_strided_backward")
-        if direct is not None:
-            return gx, None, None, None, None, None, None
-        return gx, (gw if need[1] else None), (gb if has_bias and need[2] else None), None, None, None, None
+@_conv2d_strided_op.register_fake
+def _(x, weight, bias, stride, pad, act):
+    B, _, Hi, Wi = x.shape
+    Cout, _, KH, KW = weight.shape
+    return x.new_empty((B, Cout, (Hi + 2 * pad - KH) // stride + 1, (Wi + 2 * pad - KW) // stride + 1))
+
+
+@torch.library.custom_op("dro::conv2d_strided_backward", mutates_args=("grad_x", "grad_weight", "grad_bias"))
+def _conv2d_strided_bwd_op(x: Tensor, weight: Tensor, grad_out: Tensor, stride: int, pad: int,
+                           grad_x: Optional[Tensor], grad_weight: Optional[Tensor], grad_bias: Optional[Tensor],
+                           weight_accumulate: int) -> None:
+    """Data gradient into grad_x, weight (+ bias) gradient into grad_weight /
+    grad_bias (added when weight_accumulate); act none only."""
+    lib = _lib.load()
+    B, Cin, Hi, Wi = x.shape
+    Cout, _, KH, KW = weight.shape
+    nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
+    check(lib.dro_conv2d_strided_backward(ptr(x.contiguous()), ptr(weight.contiguous()), ptr(grad_out.contiguous()),
+                                          B, Hi, Wi, Cin, Cout, KH, KW, stride, pad, ptr(grad_x), 0, ptr(grad_weight),
+                                          ptr(grad_bias), weight_accumulate, ptr(ws), nws, stream_of(grad_out)),
+          "dro_conv2d_strided_backward")
+
+
+@_conv2d_strided_bwd_op.register_fake
+def _(x, weight, grad_out, stride, pad, grad_x, grad_weight, grad_bias, weight_accumulate):
+    return None
+
+
+def _conv2d_strided_setup(ctx, inputs, output):
+    x, weight, bias, stride, pad, act = inputs
+    ctx.save_for_backward(x, weight)
+    has_bias = bias is not None
+    ctx.meta = (stride, pad, act, has_bias, x.requires_grad, weight.requires_grad,
+                has_bias and bias.requires_grad)
+    ctx.direct = _direct_targets((weight,), (bias,) if has_bias else (), mark=False)
+
+
+def _conv2d_strided_backward(ctx, gout):
+    x, weight = ctx.saved_tensors
+    stride, pad, act, has_bias, need_x, need_w, need_b = ctx.meta
+    if act:
+        raise RuntimeError("conv2d_strided: backward through a fused activation is not supported")
+    Cout = weight.shape[0]
+    gx = torch.empty_like(x) if need_x else None
+    direct = ctx.direct
+    if direct is not None:                 # in place into the trainer's flat .grad views
+        gw, gb, wacc = direct[2], direct[3] if has_bias else None, 1
+    else:
+        gw = torch.empty_like(weight) if need_w else None
+        gb = torch.empty(Cout, device=x.device) if (has_bias and need_b) else None
+        wacc = 0
+    if gw is None and gb is not None:
+        gw = torch.empty_like(weight)
+    torch.ops.dro.conv2d_strided_backward(x, weight, gout, stride, pad, gx, gw, gb, wacc)
+    if direct is not None:
+        return gx, None, None, None, None, None
+    return gx, (gw if need_w else None), (gb if has_bias and need_b else None), None, None, None
+
+
+torch.library.register_autograd("dro::conv2d_strided", _conv2d_strided_backward, setup_context=_conv2d_strided_setup)
 
 
 def conv2d_strided(x, weight, bias=None, stride=2, padding=1, act=None):
     """act(F.conv2d(x, weight, bias, stride, padding)) on the HIP conv engine
-    (stride 1 or 2, any kernel size, one dense input).  Weight gradients go in
-    place into the trainer's flat buffer when the parameters are flagged for it
-    (as hip.conv2d does)."""
-    direct = _direct_targets((weight,), (bias,) if bias is not None else ())
-    return _Conv2dStrided.apply(x, weight, bias, int(stride), int(padding), ACT[act], direct)
+    (stride 1 or 2, any kernel size, one dense input; torch.ops.dro.conv2d_strided).
+    Weight gradients go in place into the trainer's flat buffer when the
+    parameters are flagged for it (as hip.conv2d does)."""
+    _direct_targets((weight,), (bias,) if bias is not None else ())      # marks them as written in place
+    return torch.ops.dro.conv2d_strided(x, weight, bias, int(stride), int(padding), ACT[act])
 
 
-class _SepGRUHalf(torch.autograd.Function):
+# ------------------------------------------------------------------ dro::gru_backward_elem
+@torch.library.custom_op("dro::gru_backward_elem", mutates_args=("dq", "dzr", "dh"))
+def _gru_elem_op(stage: int, dhn: Optional[Tensor], zr: Tensor, q: Optional[Tensor], h: Tensor,
+                 drh: Optional[Tensor], dq: Optional[Tensor], dzr: Tensor, dh: Tensor) -> None:
+    """SepConvGRU elementwise backward (csrc/conv.hip gru_backward_elem):
+    stage 1 -- from dL/dh' the pre-activation gradients of q and z and
+    dh = dh' (1 - z); stage 2 -- the pre-activation gradient of r and dh +=
+    d(r*h) r."""
+    lib = _lib.load()
+    B, hd, H, W = h.shape
+    check(lib.dro_gru_backward_elem(stage, B, hd, H, W, ptr(dhn), ptr(zr), ptr(q), ptr(h), ptr(drh), ptr(dq),
+                                    ptr(dzr), ptr(dh), stream_of(h)), f"dro_gru_backward_elem({stage})")
+
+
+@_gru_elem_op.register_fake
+def _(stage, dhn, zr, q, h, drh, dq, dzr, dh):
+    return None
+
+
+# ------------------------------------------------------------------ dro::sepconvgru_half
+@torch.library.custom_op("dro::sepconvgru_half", mutates_args=())
+def _sepgru_op(h: Tensor, wz: Tensor, bz: Tensor, wr: Tensor, br: Tensor, wq: Tensor, bq: Tensor, xs: list[Tensor],
+               wzr: Optional[Tensor], bzr: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor, Tensor]:
     """One direction of SepConvGRU (update.py:59-70): z, r = sigmoid(conv([h; x]));
-    q = tanh(conv([r*h; x])); h' = (1-z) h + z q.  x given as sources.
-    Forward: 2 launches (gates + r*h; candidate + blend)."""
+    q = tanh(conv([r*h; x])); h' = (1-z) h + z q, x given as sources (virtual
+    concat).  wzr/bzr: the fused z|r weight/bias when the caller has them (a
+    flat-buffer view or a per-forward concatenation), else built here.
+    Returns (h', z|r, r*h, q); the last three are saved for the backward."""
+    lib = _lib.load()
+    require_device(h, wz, wq, *xs, what="sepconvgru")
+    h = h.contiguous()
+    B, hd, H, W = h.shape
+    KH, KW = wz.shape[2:]
+    cin = wz.shape[1]
+    if wzr is None:
+        wzr = torch.cat([wz, wr], 0).contiguous()
+        bzr = torch.cat([bz, br], 0).contiguous()
+    st = stream_of(h)
+    zr = torch.empty(B, 2 * hd, H, W, device=h.device)
+    rh = torch.empty_like(h)
+    ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
+    wq = wq.contiguous()
+    zf, zb = _wsplit(wzr)
+    qf, qb = _wsplit(wq)
+    check(lib.dro_convgru_gates_forward(_slices([h, *xs]), 1 + len(xs), ptr(wzr), ptr(bzr), B, H, W, hd,
+                                        KH, KW, ptr(zr), ptr(rh), ptr(zf), ptr(ws), nws, st),
+          "dro_convgru_gates_forward")
+    q = torch.empty_like(h)
+    hn = torch.empty_like(h)
+    z_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, 0, 0)
+    h_sl = DroSlice(h.data_ptr(), hd, hd, 0, 0)
+    wsq, nwsq = _workspace(B, H, W, cin, hd, KH, KW, h.device)
+    check(lib.dro_convgru_blend_forward(_slices([rh, *xs]), 1 + len(xs), ptr(wq), ptr(bq),
+                                        B, H, W, hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl),
+                                        ptr(q), ptr(hn), hd, 0, ptr(qf), ptr(wsq), nwsq, st),
+          "dro_convgru_blend_forward")
+    _LAST_WSPLIT[:] = [(zb, qb, wzr)]
+    return hn, zr, rh, q
 
-    @staticmethod
-    def forward(ctx, h, wz, bz, wr, br, wq, bq, scope, direct, *xs):
-        lib = _lib.load()
-        require_device(h, wz, wq, *xs, what="sepconvgru")
-        h = h.contiguous()
-        B, hd, H, W = h.shape
-        KH, KW = wz.shape[2:]
-        cin = wz.shape[1]
-        key = ("zr", wz.data_ptr(), wr.data_ptr())
-        wzr, bzr = scope.cats.get(key, (None, None)) if scope is not None else (None, None)
-        if direct is not None:
-            wzr, bzr = direct[0][0], direct[0][1]
-        if wzr is None:
-            wzr = torch.cat([wz, wr], 0).contiguous()
-            bzr = torch.cat([bz, br], 0).contiguous()
-            if scope is not None:
-                scope.cats[key] = (wzr, bzr)
-        st = stream_of(h)
-        zr = torch.empty(B, 2 * hd, H, W, device=h.device)
-        rh = torch.empty_like(h)
-        ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-        wq = wq.contiguous()
-        zf, zb = _wsplit(wzr)
-        qf, qb = _wsplit(wq)
-        check(lib.dro_convgru_gates_forward(_slices([h, *xs]), 1 + len(xs), ptr(wzr), ptr(bzr), B, H, W, hd,
-                                            KH, KW, ptr(zr), ptr(rh), ptr(zf), ptr(ws), nws, st),
-              "dro_convgru_gates_forward")
-        q = torch.empty_like(h)
-        hn = torch.empty_like(h)
-        z_sl = DroSlice(zr.data_ptr(), hd, 2 * hd, 0, 0)
-        h_sl = DroSlice(h.data_ptr(), hd, hd, 0, 0)
-        wsq, nwsq = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-        check(lib.dro_convgru_blend_forward(_slices([rh, *xs]), 1 + len(xs), ptr(wq), ptr(bq),
-                                            B, H, W, hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl),
-                                            ptr(q), ptr(hn), hd, 0, ptr(qf), ptr(wsq), nwsq, st),
-              "dro_convgru_blend_forward")
-        ctx.wsplit = (zb, qb)
-        ctx.save_for_backward(h, rh, wzr, wq, zr, q, *xs)
-        ctx.sinks = [_sink_of(x) for x in xs]
-        ctx.scope = scope
-        ctx.direct = direct
-        ctx.keys = (key, ("q", wq.data_ptr()))
-        return hn
 
-    @staticmethod
-    def backward(ctx, dhn):
-        lib = _lib.load()
-        h, rh, wzr, wq, zr, q, *xs = ctx.saved_tensors
-        B, hd, H, W = h.shape
-        KH, KW = wq.shape[2:]
-        cin = wq.shape[1]
-        st = stream_of(h)
-        dhn = dhn.contiguous()
-        need = ctx.needs_input_grad
-        n = 1 + len(xs)
-        # stage 1: pre-activation grads of q and z, dh = dh' (1-z)
-        dq, dh = torch.empty_like(h), torch.empty_like(h)
-        dzr = torch.empty_like(zr)
-        check(lib.dro_gru_backward_elem(1, B, hd, H, W, ptr(dhn), ptr(zr), ptr(q), ptr(h), None, ptr(dq),
-                                        ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(1)")
-        # candidate conv over [r*h, x]: d(r*h), dx (overwrite), dWq, dbq
-        drh = torch.empty_like(h)
-        # sources with a gradient sink (hip.grad_sink) are accumulated in place and
-        # get None from autograd; the others get fresh buffers
-        sinks = [s if need[9 + i] else None for i, s in enumerate(ctx.sinks)]
-        dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need[9 + i] and sinks[i] is None
-               else None for i, x in enumerate(xs)]
-        sk = [s.target() if s is not None else (None, 0) for s in sinks]
-        tg = [t if s is not None else d for (t, _), s, d in zip(sk, sinks, dxs)]
-        qacc0 = [0] + [a for _, a in sk]
-        if ctx.direct is not None:
-            return _SepGRUHalf._backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs,
-                                                tg, qacc0)
-        gwq, gbq, qacc, qfirst = _grad_buffers(ctx.scope, ctx.keys[1], wq, hd, h.device)
-        ptrs, ctot, coff = _grad_targets([drh, *tg])
-        acc = (ctypes.c_int * n)(*qacc0)
-        ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq.contiguous()), B, H, W, hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
-                                      ptr(gwq), ptr(gbq), qacc, ptr(ctx.wsplit[1]), ptr(ws), nws, st),
-              "dro_conv2d_backward(q)")
-        # stage 2: pre-activation grad of r, dh += d(r*h) r
-        check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
-                                        ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
-        # gate conv over [h, x]: dh, dx accumulate; dWz|dWr, dbz|dbr
-        gwzr, gbzr, zacc, zfirst = _grad_buffers(ctx.scope, ctx.keys[0], wzr, 2 * hd, h.device)
-        ptrs, ctot, coff = _grad_targets([dh, *tg])
-        acc = (ctypes.c_int * n)(*([1] * n))
-        ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
-                                      ptr(gwzr), ptr(gbzr), zacc, ptr(ctx.wsplit[0]), ptr(ws), nws, st),
-              "dro_conv2d_backward(zr)")
-        gz = (gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:]) if zfirst else (None,) * 4
-        gq = (gwq, gbq) if qfirst else (None, None)
-        return (dh if need[0] else None, *gz, *gq, None, None, *dxs)
+@_sepgru_op.register_fake
+def _(h, wz, bz, wr, br, wq, bq, xs, wzr, bzr):
+    B, hd, H, W = h.shape
+    return h.new_empty(h.shape), h.new_empty((B, 2 * hd, H, W)), h.new_empty(h.shape), h.new_empty(h.shape)
 
-    @staticmethod
-    def _backward_direct(ctx, lib, h, rh, wzr, wq, zr, q, xs, dhn, dq, dh, dzr, dxs, tg, qacc0):
-        """Data-gradient chain and, when not batched, dWq/dbq and dWz|r/dbz|r
-        (accumulated into the flat .grad views) on the current stream."""
-        B, hd, H, W = h.shape
-        KH, KW = wq.shape[2:]
-        cin = wq.shape[1]
-        st = stream_of(h)
-        n = 1 + len(xs)
+
+def _sepgru_setup(ctx, inputs, output):
+    h, wz, bz, wr, br, wq, bq, xs, wzr_in, bzr_in = inputs
+    hn, zr, rh, q = output
+    zb, qb, wzr = _LAST_WSPLIT.pop()
+    ctx.wsplit = (zb, qb)
+    ctx.save_for_backward(h.contiguous(), rh, wzr, wq.contiguous(), zr, q, *xs)
+    ctx.mark_non_differentiable(zr, rh, q)
+    ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in xs]
+    ctx.need = (h.requires_grad, [x.requires_grad for x in xs],
+                any(t.requires_grad for t in (wz, bz, wr, br)), any(t.requires_grad for t in (wq, bq)))
+    ctx.scope = current_scope()
+    ctx.keys = (("zr", wz.data_ptr(), wr.data_ptr()), ("q", wq.data_ptr()))
+    ctx.direct = _SEPGRU_DIRECT.pop() if _SEPGRU_DIRECT else None
+
+
+_SEPGRU_DIRECT = []   # the in-place weight-gradient targets of the call being set up (sepconvgru_half)
+
+
+def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
+    h, rh, wzr, wq, zr, q, *xs = ctx.saved_tensors
+    B, hd, H, W = h.shape
+    need_h, need_x, need_zr_w, need_q_w = ctx.need
+    dhn = dhn.contiguous()
+    # stage 1: pre-activation grads of q and z, dh = dh' (1-z)
+    dq, dh = torch.empty_like(h), torch.empty_like(h)
+    dzr = torch.empty_like(zr)
+    torch.ops.dro.gru_backward_elem(1, dhn, zr, q, h, None, dq, dzr, dh)
+    # candidate conv over [r*h, x]: d(r*h), dx (overwrite); sources with a
+    # gradient sink are accumulated in place and get None from autograd
+    drh = torch.empty_like(h)
+    sinks = ctx.sinks
+    dxs = [torch.empty(B, x.shape[1], H, W, device=h.device) if need_x[i] and sinks[i] is None
+           else None for i, x in enumerate(xs)]
+    sk = [sn.target() if sn is not None else (None, 0) for sn in sinks]
+    tg = [t if sn is not None else d for (t, _), sn, d in zip(sk, sinks, dxs)]
+    qacc0 = [0] + [a for _, a in sk]
+    zb, qb = ctx.wsplit
+    nones = (None,) * 6
+    if ctx.direct is not None:
         (_, _), (gwzr, gbzr), (gwq, gbq) = ctx.direct
-        drh = torch.empty_like(h)
-        ptrs, ctot, coff = _grad_targets([drh, *tg])
-        acc = (ctypes.c_int * n)(*qacc0)
-        ws, nws = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dq), ptrs, ctot, coff, acc,
-                                      None, None, 0, ptr(ctx.wsplit[1]), ptr(ws), nws, st),
-              "dro_conv2d_backward(q data)")
+        _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [drh, *tg], qacc0, wsplit=qb)
         if not _queue_weight_grad([rh, *xs], wq.shape, 0, 1.0, dq, None, gwq, gbq):
-            wsw, nwsw = _workspace(B, H, W, cin, hd, KH, KW, h.device)
-            check(lib.dro_conv2d_backward(_slices([rh, *xs]), n, ptr(wq), B, H, W, hd, KH, KW,
-                                          0, ctypes.c_float(1.0), None, ptr(dq), None, None, None,
-                                          None, ptr(gwq), ptr(gbq), 1, None, ptr(wsw), nwsw, st),
-                  "dro_conv2d_backward(q weight)")
-        check(lib.dro_gru_backward_elem(2, B, hd, H, W, None, ptr(zr), None, ptr(h), ptr(drh), None,
-                                        ptr(dzr), ptr(dh), st), "dro_gru_backward_elem(2)")
-        ptrs, ctot, coff = _grad_targets([dh, *tg])
-        acc = (ctypes.c_int * n)(*([1] * n))
-        ws, nws = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dzr), ptrs, ctot, coff, acc,
-                                      None, None, 0, ptr(ctx.wsplit[0]), ptr(ws), nws, st),
-              "dro_conv2d_backward(zr data)")
-        if _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
-            need = ctx.needs_input_grad
-            return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
-        wsw, nwsw = _workspace(B, H, W, cin, 2 * hd, KH, KW, h.device)
-        check(lib.dro_conv2d_backward(_slices([h, *xs]), n, ptr(wzr), B, H, W, 2 * hd, KH, KW,
-                                      0, ctypes.c_float(1.0), None, ptr(dzr), None, None, None, None,
-                                      ptr(gwzr), ptr(gbzr), 1, None, ptr(wsw), nwsw, st),
-              "dro_conv2d_backward(zr weight)")
-        need = ctx.needs_input_grad
-        return (dh if need[0] else None, None, None, None, None, None, None, None, None, *dxs)
+            _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwq, gbq, 1)
+        torch.ops.dro.gru_backward_elem(2, None, zr, None, h, drh, None, dzr, dh)
+        _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), wsplit=zb)
+        if not _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
+            _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwzr, gbzr, 1)
+        return (dh if need_h else None, *nones, dxs, None, None)
+    gwq, gbq, qacc, qfirst = _grad_buffers(ctx.scope, ctx.keys[1], wq, hd, h.device)
+    _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [drh, *tg], qacc0, gwq, gbq, qacc, qb)
+    # stage 2: pre-activation grad of r, dh += d(r*h) r
+    torch.ops.dro.gru_backward_elem(2, None, zr, None, h, drh, None, dzr, dh)
+    # gate conv over [h, x]: dh, dx accumulate; dWz|dWr, dbz|dbr
+    gwzr, gbzr, zacc, zfirst = _grad_buffers(ctx.scope, ctx.keys[0], wzr, 2 * hd, h.device)
+    _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), gwzr, gbzr, zacc, zb)
+    gz = (gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:]) if (zfirst and need_zr_w) else (None,) * 4
+    gq = (gwq, gbq) if (qfirst and need_q_w) else (None, None)
+    return (dh if need_h else None, *gz, *gq, dxs, None, None)
+
+
+torch.library.register_autograd("dro::sepconvgru_half", _sepgru_backward, setup_context=_sepgru_setup)
 
 
 def sepconvgru_half(h, convz, convr, convq, xs):
-    """h' for one SepConvGRU direction; xs: the input sources (virtual concat)."""
+    """h' for one SepConvGRU direction; xs: the input sources (virtual concat).
+    torch.ops.dro.sepconvgru_half."""
     direct = None
     zr = _direct_targets((convz.weight, convr.weight), (convz.bias, convr.bias), mark=False)
     if zr is not None:
@@ -678,5 +741,20 @@ def sepconvgru_half(h, convz, convr, convq, xs):
         if qd is not None:
             direct = ((zr[0], zr[1]), (zr[2], zr[3]), (qd[2], qd[3]))
             _mark_direct([convz.weight, convz.bias, convr.weight, convr.bias, convq.weight, convq.bias])
-    return _SepGRUHalf.apply(h, convz.weight, convz.bias, convr.weight, convr.bias, convq.weight,
-                             convq.bias, current_scope(), direct, *xs)
+    scope = current_scope()
+    wzr = bzr = None
+    if direct is not None:
+        wzr, bzr = direct[0]
+    elif scope is not None:
+        key = ("zr", convz.weight.data_ptr(), convr.weight.data_ptr())
+        ent = scope.cats.get(key)
+        if ent is None:
+            ent = scope.cats[key] = (torch.cat([convz.weight, convr.weight], 0).detach().contiguous(),
+                                     torch.cat([convz.bias, convr.bias], 0).detach().contiguous())
+        wzr, bzr = ent
+    _SEPGRU_DIRECT[:] = [direct] if direct is not None else []
+    try:
+        return torch.ops.dro.sepconvgru_half(h, convz.weight, convz.bias, convr.weight, convr.bias, convq.weight,
+                                             convq.bias, list(xs), wzr, bzr)[0]
+    finally:
+        _SEPGRU_DIRECT.clear()

@@ -1,11 +1,15 @@
-"""torch.autograd.Function wrappers over the C ABI of libdro_amd.so.
+"""torch.library custom ops (namespace `dro`, torch.ops.dro.*) over the C ABI
+of libdro_amd.so, and the Python entry points the drop-in modules call.
 
-Each Function checks dtype/device/shape up front (RuntimeError, as the
-reference's ATen ops would raise), allocates outputs through the caching
-allocator, and launches on the current stream.
+Each op checks dtype/device/shape up front (RuntimeError, as the reference's
+ATen ops would raise), allocates outputs through the caching allocator, and
+launches on the current stream.  Differentiable ops register their backward
+(itself a registered op) with torch.library.register_autograd and a fake
+kernel with the output shapes; tests/test_library.py checks the schemas.
 """
 import contextlib
 import ctypes
+from typing import Optional
 
 import torch
 
@@ -17,19 +21,13 @@ DEPTH_METRIC, DEPTH_INV, DEPTH_DISP = 0, 1, 2
 
 
 def _pose_layout(pose, lead):
-    """Return (flat pose [*lead, 6|12] contiguous, mode, restore-fn for its grad)."""
+    """Return (flat pose [*lead, 6|12] contiguous, mode).  The flattening is
+    differentiable torch indexing, so a matrix pose's gradient reaches it
+    through autograd."""
     if pose.shape[-1] == 6 and pose.dim() == len(lead) + 1:
-        return pose.contiguous(), POSE_EULER, lambda g: g
+        return pose.contiguous(), POSE_EULER
     if pose.shape[-2:] in ((3, 4), (4, 4)) and pose.dim() == len(lead) + 2:
-        rows = pose.shape[-2]
-        flat = pose[..., :3, :].contiguous().view(*lead, 12)
-
-        def restore(g):
-            g = g.view(*lead, 3, 4)
-            if rows == 4:
-                g = torch.cat([g, g.new_zeros(*lead, 1, 4)], dim=-2)
-            return g
-        return flat, POSE_MATRIX, restore
+        return pose[..., :3, :].contiguous().view(*lead, 12), POSE_MATRIX
     raise RuntimeError(f"pose must be [...,6] (euler) or [...,3|4,4] matrices, got {tuple(pose.shape)}")
 
 
@@ -150,83 +148,133 @@ def record_bilinear_cells():
         _CELLS[0] = prev
 
 
-def _cell_map(tag, shape, device):
+def _new_cells(tag, shape, device, *inputs):
+    """A cell map (-1 filled) when recording and a backward will run."""
     rec = _CELLS[0]
-    return rec.new(tag, shape, device) if rec is not None and torch.is_grad_enabled() else None
+    if rec is None or not torch.is_grad_enabled() or not any(t is not None and t.requires_grad for t in inputs):
+        return None
+    return rec.new(tag, shape, device)
 
 
-class _WarpCost(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale,
-                reduce_mean, tag):
-        lib = _lib.load()
-        require_device(fmap, fmap_ref, depth, K, ref_K, what="warp_cost")
-        B, C, h, w = fmap.shape
-        N = fmap_ref.shape[0]
-        if fmap_ref.shape != (N, B, C, h, w) or depth.shape != (B, 1, h, w) or K.shape != (B, 3, 3):
-            raise RuntimeError("warp_cost: shape mismatch (fmap [B,C,h,w], fmap_ref [N,B,C,h,w], "
-                               "depth [B,1,h,w], K [B,3,3])")
-        pose_flat, pose_mode, restore = _pose_layout(pose, (N, B))
-        require_device(pose_flat, what="warp_cost")
-        sinks = (_sink_of(fmap), _sink_of(fmap_ref))
-        fmap, fmap_ref, depth = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous()
-        K, ref_K = K.contiguous(), ref_K.contiguous()
-        out_shape = (B, C, h, w) if reduce_mean else (N, B, C, h, w)
-        cost = torch.empty(out_shape, device=fmap.device, dtype=torch.float32)
-        check(lib.dro_warp_cost_forward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode,
-                                        min_disp, max_disp, ptr(K), ptr(ref_K), scale,
-                                        ptr(pose_flat), pose_mode, B, N, C, h, w, int(reduce_mean),
-                                        ptr(cost), stream_of(fmap)), "dro_warp_cost_forward")
-        ctx.save_for_backward(fmap, fmap_ref, depth, pose_flat, K, ref_K)
-        ctx.sinks = sinks
-        ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode, int(reduce_mean))
-        ctx.restore = restore
-        ctx.cells = _cell_map(tag, (N, B, h, w), fmap.device)
-        return cost
+def _opt(t):
+    """Empty-tensor placeholder -> None (custom ops return tensors only)."""
+    return None if t is None or t.numel() == 0 and t.dim() == 1 and t.shape[0] == 0 else t
 
-    @staticmethod
-    def backward(ctx, gcost):
-        lib = _lib.load()
-        fmap, fmap_ref, depth, pose_flat, K, ref_K = ctx.saved_tensors
-        depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean = ctx.cfg
-        B, C, h, w = fmap.shape
-        N = fmap_ref.shape[0]
-        need = ctx.needs_input_grad
-        gcost = gcost.contiguous()
-        # feature maps shared by all cost calls of a step: summed in their sinks
-        sf, sr = ctx.sinks
-        sf = sf if need[0] else None
-        sr = sr if need[1] else None
-        accumulate = 0
-        if sf is not None:
-            g_f, af = sf.target()
-            accumulate |= af
-        else:
-            g_f = torch.empty_like(fmap) if need[0] else None
-        if sr is not None:
-            g_r, ar = sr.target()
-            accumulate |= 2 * ar
-        else:
-            g_r = torch.empty_like(fmap_ref) if need[1] else None
-        g_d = torch.empty_like(depth) if need[2] else None
-        g_p = torch.empty_like(pose_flat) if need[3] else None
-        ws = None
-        if g_d is not None or g_p is not None or ctx.cells is not None:
-            nbytes = lib.dro_warp_cost_workspace_bytes(B, N, h, w)
-            ws = torch.empty(nbytes // 4 + 1, device=fmap.device, dtype=torch.float32)
-        check(lib.dro_warp_cost_backward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode,
-                                         min_disp, max_disp, ptr(K), ptr(ref_K), scale,
-                                         ptr(pose_flat), pose_mode, B, N, C, h, w, reduce_mean,
-                                         ptr(gcost), ptr(g_f), ptr(g_r), ptr(g_d), ptr(g_p),
-                                         accumulate, ptr(ws), ptr(ctx.cells), stream_of(fmap)),
-              "dro_warp_cost_backward")
-        if g_p is not None:
-            g_p = ctx.restore(g_p)
-        if sf is not None:
-            g_f = None
-        if sr is not None:
-            g_r = None
-        return g_f, g_r, g_d, g_p, None, None, None, None, None, None, None, None
+
+def _none_like(device):
+    return torch.empty(0, device=device)
+
+
+# =========================================================================== torch.library ops
+# Every kernel entry point of libdro_amd.so is a torch.library custom op in the
+# `dro` namespace (torch.ops.dro.*), with a fake (meta) kernel giving output
+# shapes and, for the differentiable ones, register_autograd over a
+# registered backward op.  The implementations launch through the C ABI on
+# the current stream; there is no CPU kernel (a CPU tensor raises).
+Tensor = torch.Tensor
+
+
+# ------------------------------------------------------------------------- warp + feature cost
+@torch.library.custom_op("dro::warp_cost", mutates_args=())
+def _warp_cost_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
+                  depth_mode: int, min_disp: float, max_disp: float, scale: float, pose_mode: int,
+                  reduce_mean: bool, cells: Optional[Tensor]) -> Tensor:
+    """get_cost_each / depth_cost_calc (DepthPoseNet.py:76-105): fmap [B,C,h,w],
+    fmap_ref [N,B,C,h,w], depth [B,1,h,w], pose [N,B,6|12] -> cost [B,C,h,w]
+    (reduce_mean) or [N,B,C,h,w].  `cells` (int32 [N,B,h,w] or None) is the
+    test hook the backward fills."""
+    lib = _lib.load()
+    require_device(fmap, fmap_ref, depth, pose, K, ref_K, what="warp_cost")
+    B, C, h, w = fmap.shape
+    N = fmap_ref.shape[0]
+    fmap, fmap_ref, depth = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous()
+    cost = torch.empty((B, C, h, w) if reduce_mean else (N, B, C, h, w), device=fmap.device)
+    check(lib.dro_warp_cost_forward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode, min_disp, max_disp,
+                                    ptr(K.contiguous()), ptr(ref_K.contiguous()), scale, ptr(pose.contiguous()),
+                                    pose_mode, B, N, C, h, w, int(reduce_mean), ptr(cost), stream_of(fmap)),
+          "dro_warp_cost_forward")
+    return cost
+
+
+@_warp_cost_op.register_fake
+def _(fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean,
+      cells):
+    B, C, h, w = fmap.shape
+    return fmap.new_empty((B, C, h, w) if reduce_mean else (fmap_ref.shape[0], B, C, h, w))
+
+
+@torch.library.custom_op("dro::warp_cost_backward",
+                         mutates_args=("grad_fmap_out", "grad_fmap_ref_out", "cells"))
+def _warp_cost_bwd_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
+                      grad_cost: Tensor, depth_mode: int, min_disp: float, max_disp: float, scale: float,
+                      pose_mode: int, reduce_mean: bool, need_fmap: bool, need_fmap_ref: bool, need_depth: bool,
+                      need_pose: bool, grad_fmap_out: Optional[Tensor], grad_fmap_ref_out: Optional[Tensor],
+                      accumulate: int, cells: Optional[Tensor]) -> list[Tensor]:
+    """Backward of dro::warp_cost.  grad_fmap_out / grad_fmap_ref_out: buffers
+    the feature gradients are written (accumulate bit 0 / 1: added) into in
+    place -- the gradient sinks of maps every cost call of a step shares; the
+    returned gradient of such an input is empty.  Returns [g_fmap, g_fmap_ref,
+    g_depth, g_pose] (empty where not needed)."""
+    lib = _lib.load()
+    B, C, h, w = fmap.shape
+    N = fmap_ref.shape[0]
+    dev = fmap.device
+    fmap, fmap_ref, depth, pose = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous(), pose.contiguous()
+    K, ref_K = K.contiguous(), ref_K.contiguous()
+    g_f = grad_fmap_out if grad_fmap_out is not None else (torch.empty_like(fmap) if need_fmap else None)
+    g_r = grad_fmap_ref_out if grad_fmap_ref_out is not None else (
+        torch.empty_like(fmap_ref) if need_fmap_ref else None)
+    g_d = torch.empty_like(depth) if need_depth else None
+    g_p = torch.empty_like(pose) if need_pose else None
+    ws = None
+    if g_d is not None or g_p is not None or cells is not None:
+        ws = torch.empty(lib.dro_warp_cost_workspace_bytes(B, N, h, w) // 4 + 1, device=dev)
+    check(lib.dro_warp_cost_backward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode, min_disp, max_disp,
+                                     ptr(K), ptr(ref_K), scale, ptr(pose), pose_mode, B, N, C, h, w,
+                                     int(reduce_mean), ptr(grad_cost.contiguous()), ptr(g_f), ptr(g_r), ptr(g_d),
+                                     ptr(g_p), accumulate, ptr(ws), ptr(cells), stream_of(fmap)),
+          "dro_warp_cost_backward")
+    out = lambda g, own: g if (g is not None and not own) else _none_like(dev)
+    return [out(g_f, grad_fmap_out is not None), out(g_r, grad_fmap_ref_out is not None), out(g_d, False),
+            out(g_p, False)]
+
+
+@_warp_cost_bwd_op.register_fake
+def _(fmap, fmap_ref, depth, pose, K, ref_K, grad_cost, depth_mode, min_disp, max_disp, scale, pose_mode,
+      reduce_mean, need_fmap, need_fmap_ref, need_depth, need_pose, grad_fmap_out, grad_fmap_ref_out, accumulate,
+      cells):
+    e = fmap.new_empty(0)
+    return [fmap.new_empty(fmap.shape) if need_fmap and grad_fmap_out is None else e,
+            fmap_ref.new_empty(fmap_ref.shape) if need_fmap_ref and grad_fmap_ref_out is None else e,
+            depth.new_empty(depth.shape) if need_depth else e, pose.new_empty(pose.shape) if need_pose else e]
+
+
+def _warp_cost_setup(ctx, inputs, output):
+    fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean, cells = inputs
+    ctx.save_for_backward(fmap, fmap_ref, depth, pose, K, ref_K, cells)
+    ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean)
+    ctx.need = (fmap.requires_grad, fmap_ref.requires_grad, depth.requires_grad, pose.requires_grad)
+    # maps shared by every cost call of a step: gradients summed in their sinks
+    ctx.sinks = (_sink_of(fmap) if ctx.need[0] else None, _sink_of(fmap_ref) if ctx.need[1] else None)
+
+
+def _warp_cost_backward(ctx, gcost):
+    fmap, fmap_ref, depth, pose, K, ref_K, cells = ctx.saved_tensors
+    depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean = ctx.cfg
+    sf, sr = ctx.sinks
+    acc, bf, br = 0, None, None
+    if sf is not None:
+        bf, a = sf.target()
+        acc |= a
+    if sr is not None:
+        br, a = sr.target()
+        acc |= 2 * a
+    g = torch.ops.dro.warp_cost_backward(fmap, fmap_ref, depth, pose, K, ref_K, gcost, depth_mode, min_disp,
+                                         max_disp, scale, pose_mode, reduce_mean, *ctx.need, bf, br, acc, cells)
+    return (*[_opt(t) for t in g], None, None, None, None, None, None, None, None, None)
+
+
+torch.library.register_autograd("dro::warp_cost", _warp_cost_backward, setup_context=_warp_cost_setup)
 
 
 def warp_cost(fmap, fmap_ref, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_METRIC,
@@ -238,54 +286,97 @@ def warp_cost(fmap, fmap_ref, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_ME
     pose [N,B,6] euler vectors or [N,B,3|4,4] matrices; K/ref_K full-res [B,3,3].
     Returns the mean cost over refs [B,C,h,w] (reduce_mean) or [N,B,C,h,w].
     `tag` names the call in a record_bilinear_cells() record (tests).
+    torch.ops.dro.warp_cost underneath.
     """
     if fmap_ref.dim() == 4:
         fmap_ref = fmap_ref.unsqueeze(0)
         pose = pose.unsqueeze(0)
-    min_disp, max_disp = _disp_range(min_depth, max_depth)
+    require_device(fmap, fmap_ref, depth, K, what="warp_cost")
+    B, C, h, w = fmap.shape
+    N = fmap_ref.shape[0]
+    if fmap_ref.shape != (N, B, C, h, w) or depth.shape != (B, 1, h, w) or K.shape != (B, 3, 3):
+        raise RuntimeError("warp_cost: shape mismatch (fmap [B,C,h,w], fmap_ref [N,B,C,h,w], "
+                           "depth [B,1,h,w], K [B,3,3])")
     if depth_mode == DEPTH_DISP and (min_depth is None or max_depth is None):
         raise RuntimeError("warp_cost: DEPTH_DISP needs min_depth and max_depth")
-    return _WarpCost.apply(fmap, fmap_ref, depth, pose, K, K if ref_K is None else ref_K,
-                           depth_mode, float(min_disp), float(max_disp), float(scale), reduce_mean, tag)
+    pose_flat, pose_mode = _pose_layout(pose, (N, B))
+    require_device(pose_flat, what="warp_cost")
+    min_disp, max_disp = _disp_range(min_depth, max_depth)
+    ref_K = K if ref_K is None else ref_K
+    cells = _new_cells(tag, (N, B, h, w), fmap.device, fmap, fmap_ref, depth, pose_flat)
+    return torch.ops.dro.warp_cost(fmap, fmap_ref, depth, pose_flat, K, ref_K, depth_mode, float(min_disp),
+                                   float(max_disp), float(scale), pose_mode, bool(reduce_mean), cells)
 
 
-class _ViewSynthesis(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, ref_image, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale):
-        lib = _lib.load()
-        require_device(ref_image, depth, K, ref_K, what="view_synthesis")
-        N, B, C, H, W = ref_image.shape
-        if depth.shape != (B, 1, H, W) or K.shape != (B, 3, 3) or ref_K.shape != (B, 3, 3):
-            raise RuntimeError("view_synthesis: ref_image [N,B,C,H,W], depth [B,1,H,W], K/ref_K [B,3,3]")
-        pose_flat, pose_mode, restore = _pose_layout(pose, (N, B))
-        require_device(pose_flat, what="view_synthesis")
-        ref_image, depth, K, ref_K = ref_image.contiguous(), depth.contiguous(), K.contiguous(), ref_K.contiguous()
-        warped = torch.empty_like(ref_image)
-        check(lib.dro_view_synthesis_forward(ptr(ref_image), ptr(depth), depth_mode, min_disp, max_disp, ptr(K),
-                                             ptr(ref_K), scale, ptr(pose_flat), pose_mode, B, N, C, H, W,
-                                             ptr(warped), stream_of(ref_image)), "dro_view_synthesis_forward")
-        ctx.save_for_backward(ref_image, depth, pose_flat, K, ref_K)
-        ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode)
-        ctx.restore = restore
-        ctx.cells = _cell_map("view_synthesis", (N, B, H, W), ref_image.device)
-        return warped
+# ------------------------------------------------------------------------- view synthesis
+@torch.library.custom_op("dro::view_synthesis", mutates_args=())
+def _view_synthesis_op(ref_image: Tensor, depth: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor, depth_mode: int,
+                       min_disp: float, max_disp: float, scale: float, pose_mode: int,
+                       cells: Optional[Tensor]) -> Tensor:
+    """view_synthesis (camera_utils.py:23-56) of N views: ref_image [N,B,C,H,W],
+    depth [B,1,H,W], pose [N,B,6|12] -> warped [N,B,C,H,W]."""
+    lib = _lib.load()
+    require_device(ref_image, depth, pose, K, ref_K, what="view_synthesis")
+    N, B, C, H, W = ref_image.shape
+    ref_image = ref_image.contiguous()
+    warped = torch.empty_like(ref_image)
+    check(lib.dro_view_synthesis_forward(ptr(ref_image), ptr(depth.contiguous()), depth_mode, min_disp, max_disp,
+                                         ptr(K.contiguous()), ptr(ref_K.contiguous()), scale, ptr(pose.contiguous()),
+                                         pose_mode, B, N, C, H, W, ptr(warped), stream_of(ref_image)),
+          "dro_view_synthesis_forward")
+    return warped
 
-    @staticmethod
-    def backward(ctx, gw):
-        lib = _lib.load()
-        ref_image, depth, pose_flat, K, ref_K = ctx.saved_tensors
-        depth_mode, min_disp, max_disp, scale, pose_mode = ctx.cfg
-        N, B, C, H, W = ref_image.shape
-        need = ctx.needs_input_grad
-        g_r = torch.empty_like(ref_image) if need[0] else None
-        g_d = torch.empty_like(depth) if need[1] else None
-        g_p = torch.empty_like(pose_flat) if need[2] else None
-        ws = torch.empty(lib.dro_warp_cost_workspace_bytes(B, N, H, W) // 4 + 1, device=depth.device)
-        check(lib.dro_view_synthesis_backward(ptr(ref_image), ptr(depth), depth_mode, min_disp, max_disp, ptr(K),
-                                              ptr(ref_K), scale, ptr(pose_flat), pose_mode, B, N, C, H, W,
-                                              ptr(gw.contiguous()), ptr(g_r), ptr(g_d), ptr(g_p), ptr(ws),
-                                              ptr(ctx.cells), stream_of(depth)), "dro_view_synthesis_backward")
-        return g_r, g_d, (ctx.restore(g_p) if g_p is not None else None), None, None, None, None, None, None
+
+@_view_synthesis_op.register_fake
+def _(ref_image, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale, pose_mode, cells):
+    return ref_image.new_empty(ref_image.shape)
+
+
+@torch.library.custom_op("dro::view_synthesis_backward", mutates_args=("cells",))
+def _view_synthesis_bwd_op(ref_image: Tensor, depth: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
+                           grad_warped: Tensor, depth_mode: int, min_disp: float, max_disp: float, scale: float,
+                           pose_mode: int, need_ref: bool, need_depth: bool, need_pose: bool,
+                           cells: Optional[Tensor]) -> list[Tensor]:
+    """Backward of dro::view_synthesis: [g_ref_image, g_depth (summed over the
+    views), g_pose] (empty where not needed)."""
+    lib = _lib.load()
+    N, B, C, H, W = ref_image.shape
+    dev = depth.device
+    ref_image, depth, pose = ref_image.contiguous(), depth.contiguous(), pose.contiguous()
+    K, ref_K = K.contiguous(), ref_K.contiguous()
+    g_r = torch.empty_like(ref_image) if need_ref else None
+    g_d = torch.empty_like(depth) if need_depth else None
+    g_p = torch.empty_like(pose) if need_pose else None
+    ws = torch.empty(lib.dro_warp_cost_workspace_bytes(B, N, H, W) // 4 + 1, device=dev)
+    check(lib.dro_view_synthesis_backward(ptr(ref_image), ptr(depth), depth_mode, min_disp, max_disp, ptr(K),
+                                          ptr(ref_K), scale, ptr(pose), pose_mode, B, N, C, H, W,
+                                          ptr(grad_warped.contiguous()), ptr(g_r), ptr(g_d), ptr(g_p), ptr(ws),
+                                          ptr(cells), stream_of(depth)), "dro_view_synthesis_backward")
+    return [t if t is not None else _none_like(dev) for t in (g_r, g_d, g_p)]
+
+
+@_view_synthesis_bwd_op.register_fake
+def _(ref_image, depth, pose, K, ref_K, grad_warped, depth_mode, min_disp, max_disp, scale, pose_mode, need_ref,
+      need_depth, need_pose, cells):
+    e = depth.new_empty(0)
+    return [ref_image.new_empty(ref_image.shape) if need_ref else e, depth.new_empty(depth.shape) if need_depth else e,
+            pose.new_empty(pose.shape) if need_pose else e]
+
+
+def _view_synthesis_setup(ctx, inputs, output):
+    ref_image, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, scale, pose_mode, cells = inputs
+    ctx.save_for_backward(ref_image, depth, pose, K, ref_K, cells)
+    ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode)
+    ctx.need = (ref_image.requires_grad, depth.requires_grad, pose.requires_grad)
+
+
+def _view_synthesis_backward(ctx, gw):
+    ref_image, depth, pose, K, ref_K, cells = ctx.saved_tensors
+    g = torch.ops.dro.view_synthesis_backward(ref_image, depth, pose, K, ref_K, gw, *ctx.cfg, *ctx.need, cells)
+    return (*[_opt(t) for t in g], None, None, None, None, None, None, None, None)
+
+
+torch.library.register_autograd("dro::view_synthesis", _view_synthesis_backward, setup_context=_view_synthesis_setup)
 
 
 def view_synthesis(ref_image, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_METRIC, min_depth=None,
@@ -295,90 +386,135 @@ def view_synthesis(ref_image, depth, pose, K, ref_K=None, *, depth_mode=DEPTH_ME
     in `depth_mode`, pose [N,B,6] euler vectors or [N,B,3|4,4] matrices (target
     -> reference, Camera(ref_K, Tcw=pose)), K/ref_K [B,3,3] scaled by `scale`
     (scale_intrinsics).  Returns the warped references, same shape as ref_image.
-    The kernels are the cost's (warp_cost_fwd/bwd_feat/bwd_geo in SAMPLE mode)."""
+    The kernels are the cost's (warp_cost_fwd/bwd_feat/bwd_geo in SAMPLE mode);
+    torch.ops.dro.view_synthesis underneath."""
     single = ref_image.dim() == 4
     if single:
         ref_image, pose = ref_image.unsqueeze(0), pose.unsqueeze(0)
     if depth_mode == DEPTH_DISP and (min_depth is None or max_depth is None):
         raise RuntimeError("view_synthesis: DEPTH_DISP needs min_depth and max_depth")
+    require_device(ref_image, depth, K, what="view_synthesis")
+    N, B, C, H, W = ref_image.shape
+    if depth.shape != (B, 1, H, W) or K.shape != (B, 3, 3):
+        raise RuntimeError("view_synthesis: ref_image [N,B,C,H,W], depth [B,1,H,W], K/ref_K [B,3,3]")
+    pose_flat, pose_mode = _pose_layout(pose, (N, B))
     min_disp, max_disp = _disp_range(min_depth, max_depth)
-    out = _ViewSynthesis.apply(ref_image, depth, pose, K, K if ref_K is None else ref_K, depth_mode,
-                               float(min_disp), float(max_disp), float(scale))
+    cells = _new_cells("view_synthesis", (N, B, H, W), depth.device, ref_image, depth, pose_flat)
+    out = torch.ops.dro.view_synthesis(ref_image, depth, pose_flat, K, K if ref_K is None else ref_K, depth_mode,
+                                       float(min_disp), float(max_disp), float(scale), pose_mode, cells)
     return out[0] if single else out
+
+
+# ------------------------------------------------------------------------- plane sweep (forward only)
+@torch.library.custom_op("dro::plane_sweep", mutates_args=())
+def _plane_sweep_op(fmap: Tensor, fmap_ref: Tensor, disp: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
+                    min_disp: float, max_disp: float, scale: float, pose_mode: int) -> Tensor:
+    """D fronto-parallel planes: fmap/fmap_ref [B,C,h,w], disp [D] (sigmoid
+    space), pose [B,6|12] -> cost volume [B,D,C,h,w]."""
+    lib = _lib.load()
+    require_device(fmap, fmap_ref, disp, pose, K, ref_K, what="plane_sweep_cost")
+    B, C, h, w = fmap.shape
+    D = disp.numel()
+    cost = torch.empty(B, D, C, h, w, device=fmap.device)
+    check(lib.dro_plane_sweep_forward(ptr(fmap.contiguous()), ptr(fmap_ref.contiguous()), ptr(disp.contiguous()), D,
+                                      min_disp, max_disp, ptr(K.contiguous()), ptr(ref_K.contiguous()), scale,
+                                      ptr(pose.contiguous()), pose_mode, B, C, h, w, ptr(cost), stream_of(fmap)),
+          "dro_plane_sweep_forward")
+    return cost
+
+
+@_plane_sweep_op.register_fake
+def _(fmap, fmap_ref, disp, pose, K, ref_K, min_disp, max_disp, scale, pose_mode):
+    B, C, h, w = fmap.shape
+    return fmap.new_empty((B, disp.numel(), C, h, w))
 
 
 def plane_sweep_cost(fmap, fmap_ref, disp, pose, K, ref_K=None, *, min_depth, max_depth,
                      scale=1.0 / 8):
     """Cost of D fronto-parallel planes (disp [D] in sigmoid space): [B,D,C,h,w]."""
-    lib = _lib.load()
     require_device(fmap, fmap_ref, disp, K, what="plane_sweep_cost")
-    B, C, h, w = fmap.shape
-    D = disp.numel()
-    pose_flat, pose_mode, _ = _pose_layout(pose, (B,))
-    ref_K = K if ref_K is None else ref_K
+    B = fmap.shape[0]
+    pose_flat, pose_mode = _pose_layout(pose, (B,))
     min_disp, max_disp = _disp_range(min_depth, max_depth)
-    fmap, fmap_ref, disp = fmap.contiguous(), fmap_ref.contiguous(), disp.contiguous()
-    K, ref_K = K.contiguous(), ref_K.contiguous()
-    cost = torch.empty(B, D, C, h, w, device=fmap.device, dtype=torch.float32)
-    check(lib.dro_plane_sweep_forward(ptr(fmap), ptr(fmap_ref), ptr(disp), D, float(min_disp),
-                                      float(max_disp), ptr(K), ptr(ref_K), float(scale),
-                                      ptr(pose_flat), pose_mode, B, C, h, w, ptr(cost),
-                                      stream_of(fmap)), "dro_plane_sweep_forward")
-    return cost
+    return torch.ops.dro.plane_sweep(fmap, fmap_ref, disp, pose_flat, K, K if ref_K is None else ref_K,
+                                     float(min_disp), float(max_disp), float(scale), pose_mode)
 
 
 # ------------------------------------------------------------------------- photometric loss
-class _Photometric(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, image, context, inv_depths, pose, K, ref_K, opts):
-        lib = _lib.load()
-        require_device(image, context, inv_depths, K, ref_K, what="photometric_loss")
-        n, B, _, H, W = inv_depths.shape
-        N = context.shape[0]
-        if image.shape != (B, 3, H, W) or context.shape != (N, B, 3, H, W):
-            raise RuntimeError("photometric_loss: image [B,3,H,W], context [N,B,3,H,W] and "
-                               "inv_depths [n,B,1,H,W] must share B,H,W (full-res predictions)")
-        pose_flat, pose_mode, restore = _pose_layout(pose, (N, n, B))
-        ssim_w, C1, C2, smooth_w, automask, reduce_min = opts
-        image, context, inv_depths = image.contiguous(), context.contiguous(), inv_depths.contiguous()
-        K, ref_K = K.contiguous(), ref_K.contiguous()
-        nbytes = lib.dro_photometric_workspace_bytes(B, N, n, H, W)
-        ws = torch.empty(nbytes, device=image.device, dtype=torch.uint8)
-        out = torch.empty(3, device=image.device, dtype=torch.float32)
-        check(lib.dro_photometric_forward(ptr(image), ptr(context), ptr(inv_depths), ptr(K),
-                                          ptr(ref_K), ptr(pose_flat), pose_mode, B, N, n, H, W,
-                                          ssim_w, C1, C2, smooth_w, automask, reduce_min,
-                                          ptr(out), ptr(ws), stream_of(image)),
-              "dro_photometric_forward")
-        ctx.save_for_backward(image, context, inv_depths, pose_flat, K, ref_K, ws)
-        ctx.cfg = (pose_mode, opts)
-        ctx.restore = restore
-        ctx.cells = _cell_map("photo", (N, n, B, H, W), image.device)
-        metrics = out[1:].detach()
-        # per-pixel argmin over the candidate maps (uint8 [n,B,H,W], the first
-        # region of the workspace); exposed for parity tests
-        sel = ws[:n * B * H * W].view(n, B, H, W)
-        ctx.mark_non_differentiable(metrics, sel)
-        return out[0:1], metrics, sel
+@torch.library.custom_op("dro::photometric_loss", mutates_args=())
+def _photometric_op(image: Tensor, context: Tensor, inv_depths: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
+                    pose_mode: int, ssim_w: float, C1: float, C2: float, smooth_w: float, automask: bool,
+                    reduce_min: bool, cells: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor]:
+    """MultiViewPhotometricDecayLoss (multiview_photometric_loss_mf.py:303-361):
+    image [B,3,H,W], context [N,B,3,H,W], inv_depths [n,B,1,H,W], pose
+    [N,n,B,6|12] -> (loss [1], metrics [2] (photometric, smoothness), the
+    forward state [bytes] the backward reads; its first n*B*H*W bytes are the
+    per-pixel min selection).  `cells` (int32 [N,n,B,H,W] or None): the
+    backward's test hook."""
+    lib = _lib.load()
+    require_device(image, context, inv_depths, pose, K, ref_K, what="photometric_loss")
+    n, B, _, H, W = inv_depths.shape
+    N = context.shape[0]
+    ws = torch.empty(lib.dro_photometric_workspace_bytes(B, N, n, H, W), device=image.device, dtype=torch.uint8)
+    out = torch.empty(3, device=image.device)
+    check(lib.dro_photometric_forward(ptr(image.contiguous()), ptr(context.contiguous()), ptr(inv_depths.contiguous()),
+                                      ptr(K.contiguous()), ptr(ref_K.contiguous()), ptr(pose.contiguous()), pose_mode,
+                                      B, N, n, H, W, ssim_w, C1, C2, smooth_w, int(automask), int(reduce_min),
+                                      ptr(out), ptr(ws), stream_of(image)), "dro_photometric_forward")
+    return out[0:1].clone(), out[1:].clone(), ws
 
-    @staticmethod
-    def backward(ctx, gloss, _gmetrics, _gsel):
-        lib = _lib.load()
-        image, context, inv_depths, pose_flat, K, ref_K, ws = ctx.saved_tensors
-        pose_mode, (ssim_w, C1, C2, smooth_w, automask, reduce_min) = ctx.cfg
-        n, B, _, H, W = inv_depths.shape
-        N = context.shape[0]
-        gloss = gloss.contiguous()
-        g_inv = torch.empty_like(inv_depths)
-        g_pose = torch.empty_like(pose_flat) if ctx.needs_input_grad[3] else None
-        check(lib.dro_photometric_backward(ptr(image), ptr(context), ptr(inv_depths), ptr(K),
-                                           ptr(ref_K), ptr(pose_flat), pose_mode, B, N, n, H, W,
-                                           ssim_w, C1, C2, smooth_w, automask, reduce_min,
-                                           ptr(gloss), ptr(g_inv), ptr(g_pose), ptr(ws), ptr(ctx.cells),
-                                           stream_of(image)), "dro_photometric_backward")
-        if g_pose is not None:
-            g_pose = ctx.restore(g_pose)
-        return None, None, g_inv if ctx.needs_input_grad[2] else None, g_pose, None, None, None
+
+@_photometric_op.register_fake
+def _(image, context, inv_depths, pose, K, ref_K, pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min, cells):
+    n, B, _, H, W = inv_depths.shape
+    nb = _lib.load().dro_photometric_workspace_bytes(B, context.shape[0], n, H, W)
+    return image.new_empty(1), image.new_empty(2), image.new_empty(nb, dtype=torch.uint8)
+
+
+@torch.library.custom_op("dro::photometric_loss_backward", mutates_args=("cells",))
+def _photometric_bwd_op(image: Tensor, context: Tensor, inv_depths: Tensor, pose: Tensor, K: Tensor,
+                        ref_K: Tensor, state: Tensor, grad_loss: Tensor, pose_mode: int, ssim_w: float, C1: float,
+                        C2: float, smooth_w: float, automask: bool, reduce_min: bool, need_pose: bool,
+                        cells: Optional[Tensor]) -> list[Tensor]:
+    """Backward of dro::photometric_loss: [g_inv_depths, g_pose (empty unless need_pose)]."""
+    lib = _lib.load()
+    n, B, _, H, W = inv_depths.shape
+    N = context.shape[0]
+    image, context, inv_depths, pose = image.contiguous(), context.contiguous(), inv_depths.contiguous(), pose.contiguous()
+    K, ref_K = K.contiguous(), ref_K.contiguous()
+    g_inv = torch.empty_like(inv_depths)
+    g_pose = torch.empty_like(pose) if need_pose else None
+    check(lib.dro_photometric_backward(ptr(image), ptr(context), ptr(inv_depths), ptr(K), ptr(ref_K), ptr(pose),
+                                       pose_mode, B, N, n, H, W, ssim_w, C1, C2, smooth_w, int(automask),
+                                       int(reduce_min), ptr(grad_loss.contiguous()), ptr(g_inv), ptr(g_pose),
+                                       ptr(state), ptr(cells), stream_of(image)), "dro_photometric_backward")
+    return [g_inv, g_pose if g_pose is not None else _none_like(image.device)]
+
+
+@_photometric_bwd_op.register_fake
+def _(image, context, inv_depths, pose, K, ref_K, state, grad_loss, pose_mode, ssim_w, C1, C2, smooth_w, automask,
+      reduce_min, need_pose, cells):
+    return [inv_depths.new_empty(inv_depths.shape), pose.new_empty(pose.shape) if need_pose else pose.new_empty(0)]
+
+
+def _photometric_setup(ctx, inputs, output):
+    image, context, inv_depths, pose, K, ref_K, pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min, cells = inputs
+    _, metrics, state = output
+    ctx.save_for_backward(image, context, inv_depths, pose, K, ref_K, state, cells)
+    ctx.cfg = (pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min)
+    ctx.need = (inv_depths.requires_grad, pose.requires_grad)
+    ctx.mark_non_differentiable(metrics, state)
+
+
+def _photometric_backward(ctx, gloss, _gmetrics, _gstate):
+    image, context, inv_depths, pose, K, ref_K, state, cells = ctx.saved_tensors
+    g_inv, g_pose = torch.ops.dro.photometric_loss_backward(image, context, inv_depths, pose, K, ref_K, state, gloss,
+                                                            *ctx.cfg, ctx.need[1], cells)
+    return (g_inv if ctx.need[0] else None, _opt(g_pose), None, None, None, None, None, None, None, None, None,
+            None, None, None)
+
+
+torch.library.register_autograd("dro::photometric_loss", _photometric_backward, setup_context=_photometric_setup)
 
 
 def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=0.85, C1=1e-4,
@@ -391,66 +527,89 @@ def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=
     Returns (loss [1], detached metrics [2] = (photometric_loss, smoothness_loss))
     and, with return_selection, the per-pixel min-candidate index uint8 [n,B,H,W]
     (candidate order of the reference's torch.cat: warped_0, unwarped_0, ...).
+    torch.ops.dro.photometric_loss underneath.
     """
-    opts = (float(ssim_w), float(C1), float(C2), float(smooth_w), int(bool(automask)),
-            int(bool(reduce_min)))
-    loss, metrics, sel = _Photometric.apply(image, context, inv_depths, pose, K,
-                                            K if ref_K is None else ref_K, opts)
-    return (loss, metrics, sel) if return_selection else (loss, metrics)
+    require_device(image, context, inv_depths, K, what="photometric_loss")
+    n, B, _, H, W = inv_depths.shape
+    N = context.shape[0]
+    if image.shape != (B, 3, H, W) or context.shape != (N, B, 3, H, W):
+        raise RuntimeError("photometric_loss: image [B,3,H,W], context [N,B,3,H,W] and "
+                           "inv_depths [n,B,1,H,W] must share B,H,W (full-res predictions)")
+    pose_flat, pose_mode = _pose_layout(pose, (N, n, B))
+    require_device(pose_flat, what="photometric_loss")
+    cells = _new_cells("photo", (N, n, B, H, W), image.device, inv_depths, pose_flat)
+    loss, metrics, state = torch.ops.dro.photometric_loss(
+        image, context, inv_depths, pose_flat, K, K if ref_K is None else ref_K, pose_mode, float(ssim_w),
+        float(C1), float(C2), float(smooth_w), bool(automask), bool(reduce_min), cells)
+    if return_selection:
+        return loss, metrics, state[:n * B * H * W].view(n, B, H, W)
+    return loss, metrics
 
 
 # ------------------------------------------------------------------------- supervised loss
-class _Supervised(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, gt_inv, inv_depths, pose, gt_pose, K, ref_K, min_depth, max_depth):
-        lib = _lib.load()
-        require_device(gt_inv, inv_depths, gt_pose, K, ref_K, what="supervised_loss")
-        n, B, _, H, W = inv_depths.shape
-        N = gt_pose.shape[0]
-        if gt_inv.shape != (B, 1, H, W) or K.shape != (B, 3, 3) or ref_K.shape != (B, 3, 3):
-            raise RuntimeError("supervised_loss: gt_inv [B,1,H,W] and inv_depths [n,B,1,H,W] must "
-                               "share B,H,W; K/ref_K [B,3,3]")
-        pose_flat, pose_mode, restore = _pose_layout(pose, (N, n, B))
-        gt_flat, gt_mode, _ = _pose_layout(gt_pose, (N, B))
-        if gt_mode != POSE_MATRIX:
-            raise RuntimeError("supervised_loss: gt_pose must be [N,B,3|4,4] matrices")
-        require_device(pose_flat, what="supervised_loss")
-        gt_inv, inv_depths = gt_inv.contiguous(), inv_depths.contiguous()
-        K, ref_K = K.contiguous(), ref_K.contiguous()
-        ws = torch.empty(lib.dro_supervised_workspace_bytes(B, N, n, H, W) // 4 + 1,
-                         device=gt_inv.device, dtype=torch.float32)
-        out = torch.empty(3, device=gt_inv.device, dtype=torch.float32)
-        check(lib.dro_supervised_forward(ptr(gt_inv), ptr(inv_depths), ptr(K), ptr(ref_K),
-                                         ptr(gt_flat), ptr(pose_flat), pose_mode, B, N, n, H, W,
-                                         min_depth, max_depth, ptr(out), ptr(ws),
-                                         stream_of(gt_inv)), "dro_supervised_forward")
-        ctx.save_for_backward(gt_inv, inv_depths, pose_flat, gt_flat, K, ref_K)
-        ctx.cfg = (pose_mode, min_depth, max_depth)
-        ctx.restore = restore
-        metrics = out[1:].detach()
-        ctx.mark_non_differentiable(metrics)
-        return out[0:1], metrics
+@torch.library.custom_op("dro::supervised_loss", mutates_args=())
+def _supervised_op(gt_inv: Tensor, inv_depths: Tensor, pose: Tensor, gt_pose: Tensor, K: Tensor, ref_K: Tensor,
+                   pose_mode: int, min_depth: float, max_depth: float) -> tuple[Tensor, Tensor]:
+    """SupervisedDepthPoseLoss (supervised_loss.py:343-371, 'sparse-l1'):
+    gt_inv [B,1,H,W], inv_depths [n,B,1,H,W], pose [N,n,B,6|12], gt_pose
+    [N,B,12] -> (loss [1], metrics [2] (depth_loss, pose_loss))."""
+    lib = _lib.load()
+    require_device(gt_inv, inv_depths, pose, gt_pose, K, ref_K, what="supervised_loss")
+    n, B, _, H, W = inv_depths.shape
+    N = gt_pose.shape[0]
+    ws = torch.empty(lib.dro_supervised_workspace_bytes(B, N, n, H, W) // 4 + 1, device=gt_inv.device)
+    out = torch.empty(3, device=gt_inv.device)
+    check(lib.dro_supervised_forward(ptr(gt_inv.contiguous()), ptr(inv_depths.contiguous()), ptr(K.contiguous()),
+                                     ptr(ref_K.contiguous()), ptr(gt_pose.contiguous()), ptr(pose.contiguous()),
+                                     pose_mode, B, N, n, H, W, min_depth, max_depth, ptr(out), ptr(ws),
+                                     stream_of(gt_inv)), "dro_supervised_forward")
+    return out[0:1].clone(), out[1:].clone()
 
-    @staticmethod
-    def backward(ctx, gloss, _gmetrics):
-        lib = _lib.load()
-        gt_inv, inv_depths, pose_flat, gt_flat, K, ref_K = ctx.saved_tensors
-        pose_mode, min_depth, max_depth = ctx.cfg
-        n, B, _, H, W = inv_depths.shape
-        N = gt_flat.shape[0]
-        gloss = gloss.contiguous()
-        g_inv = torch.empty_like(inv_depths)
-        g_pose = torch.empty_like(pose_flat)
-        ws = torch.empty(lib.dro_supervised_workspace_bytes(B, N, n, H, W) // 4 + 1,
-                         device=gt_inv.device, dtype=torch.float32)
-        check(lib.dro_supervised_backward(ptr(gt_inv), ptr(inv_depths), ptr(K), ptr(ref_K),
-                                          ptr(gt_flat), ptr(pose_flat), pose_mode, B, N, n, H, W,
-                                          min_depth, max_depth, ptr(gloss), ptr(g_inv),
-                                          ptr(g_pose), ptr(ws), stream_of(gt_inv)),
-              "dro_supervised_backward")
-        need = ctx.needs_input_grad
-        return (None, g_inv if need[1] else None, ctx.restore(g_pose) if need[2] else None,
-                None, None, None, None, None)
+
+@_supervised_op.register_fake
+def _(gt_inv, inv_depths, pose, gt_pose, K, ref_K, pose_mode, min_depth, max_depth):
+    return gt_inv.new_empty(1), gt_inv.new_empty(2)
+
+
+@torch.library.custom_op("dro::supervised_loss_backward", mutates_args=())
+def _supervised_bwd_op(gt_inv: Tensor, inv_depths: Tensor, pose: Tensor, gt_pose: Tensor, K: Tensor, ref_K: Tensor,
+                       grad_loss: Tensor, pose_mode: int, min_depth: float, max_depth: float) -> list[Tensor]:
+    """Backward of dro::supervised_loss: [g_inv_depths, g_pose]."""
+    lib = _lib.load()
+    n, B, _, H, W = inv_depths.shape
+    N = gt_pose.shape[0]
+    gt_inv, inv_depths, pose, gt_pose = gt_inv.contiguous(), inv_depths.contiguous(), pose.contiguous(), gt_pose.contiguous()
+    K, ref_K = K.contiguous(), ref_K.contiguous()
+    g_inv, g_pose = torch.empty_like(inv_depths), torch.empty_like(pose)
+    ws = torch.empty(lib.dro_supervised_workspace_bytes(B, N, n, H, W) // 4 + 1, device=gt_inv.device)
+    check(lib.dro_supervised_backward(ptr(gt_inv), ptr(inv_depths), ptr(K), ptr(ref_K), ptr(gt_pose), ptr(pose),
+                                      pose_mode, B, N, n, H, W, min_depth, max_depth, ptr(grad_loss.contiguous()),
+                                      ptr(g_inv), ptr(g_pose), ptr(ws), stream_of(gt_inv)), "dro_supervised_backward")
+    return [g_inv, g_pose]
+
+
+@_supervised_bwd_op.register_fake
+def _(gt_inv, inv_depths, pose, gt_pose, K, ref_K, grad_loss, pose_mode, min_depth, max_depth):
+    return [inv_depths.new_empty(inv_depths.shape), pose.new_empty(pose.shape)]
+
+
+def _supervised_setup(ctx, inputs, output):
+    gt_inv, inv_depths, pose, gt_pose, K, ref_K, pose_mode, min_depth, max_depth = inputs
+    ctx.save_for_backward(gt_inv, inv_depths, pose, gt_pose, K, ref_K)
+    ctx.cfg = (pose_mode, min_depth, max_depth)
+    ctx.need = (inv_depths.requires_grad, pose.requires_grad)
+    ctx.mark_non_differentiable(output[1])
+
+
+def _supervised_backward(ctx, gloss, _gmetrics):
+    gt_inv, inv_depths, pose, gt_pose, K, ref_K = ctx.saved_tensors
+    g_inv, g_pose = torch.ops.dro.supervised_loss_backward(gt_inv, inv_depths, pose, gt_pose, K, ref_K, gloss,
+                                                           *ctx.cfg)
+    return (None, g_inv if ctx.need[0] else None, g_pose if ctx.need[1] else None, None, None, None, None, None,
+            None)
+
+
+torch.library.register_autograd("dro::supervised_loss", _supervised_backward, setup_context=_supervised_setup)
 
 
 def supervised_loss(gt_inv, inv_depths, pose, gt_pose, K, ref_K=None, *, min_depth, max_depth):
@@ -458,48 +617,90 @@ def supervised_loss(gt_inv, inv_depths, pose, gt_pose, K, ref_K=None, *, min_dep
 
     gt_inv [B,1,H,W]; inv_depths [n,B,1,H,W]; pose [N,n,B,6] euler vectors or
     [N,n,B,3|4,4] matrices; gt_pose [N,B,3|4,4].  Returns (loss [1], detached
-    metrics [2] = (depth_loss, pose_loss)).
+    metrics [2] = (depth_loss, pose_loss)).  torch.ops.dro.supervised_loss.
     """
-    return _Supervised.apply(gt_inv, inv_depths, pose, gt_pose, K, K if ref_K is None else ref_K,
-                             float(min_depth), float(max_depth))
+    require_device(gt_inv, inv_depths, gt_pose, K, what="supervised_loss")
+    n, B, _, H, W = inv_depths.shape
+    N = gt_pose.shape[0]
+    ref_K = K if ref_K is None else ref_K
+    if gt_inv.shape != (B, 1, H, W) or K.shape != (B, 3, 3) or ref_K.shape != (B, 3, 3):
+        raise RuntimeError("supervised_loss: gt_inv [B,1,H,W] and inv_depths [n,B,1,H,W] must "
+                           "share B,H,W; K/ref_K [B,3,3]")
+    pose_flat, pose_mode = _pose_layout(pose, (N, n, B))
+    gt_flat, gt_mode = _pose_layout(gt_pose, (N, B))
+    if gt_mode != POSE_MATRIX:
+        raise RuntimeError("supervised_loss: gt_pose must be [N,B,3|4,4] matrices")
+    require_device(pose_flat, what="supervised_loss")
+    return torch.ops.dro.supervised_loss(gt_inv, inv_depths, pose_flat, gt_flat.detach(), K, ref_K, pose_mode,
+                                         float(min_depth), float(max_depth))
 
 
 # ------------------------------------------------------------------------- convex upsample
-class _ConvexUpsample(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, inv, mask, ratio, add, mul):
-        lib = _lib.load()
-        require_device(inv, mask, what="convex_upsample")
-        B, _, h, w = inv.shape
-        if mask.shape != (B, 9 * ratio * ratio, h, w):
-            raise RuntimeError("convex_upsample: mask must be [B, 9*r*r, h, w]")
-        inv, mask = inv.contiguous(), mask.contiguous()
-        out = torch.empty(B, 1, h * ratio, w * ratio, device=inv.device, dtype=torch.float32)
-        check(lib.dro_convex_upsample_forward(ptr(inv), ptr(mask), B, h, w, ratio, ctypes.c_float(add),
-                                              ctypes.c_float(mul), ptr(out), stream_of(inv)),
-              "dro_convex_upsample_forward")
-        ctx.save_for_backward(inv, mask)
-        ctx.ratio, ctx.mul = ratio, mul
-        return out
+@torch.library.custom_op("dro::convex_upsample", mutates_args=())
+def _convex_upsample_op(inv: Tensor, mask: Tensor, ratio: int, add: float, mul: float) -> Tensor:
+    """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74): inv [B,1,h,w], mask
+    [B,9*r*r,h,w] -> add + mul * up [B,1,r*h,r*w]."""
+    lib = _lib.load()
+    require_device(inv, mask, what="convex_upsample")
+    B, _, h, w = inv.shape
+    out = torch.empty(B, 1, h * ratio, w * ratio, device=inv.device)
+    check(lib.dro_convex_upsample_forward(ptr(inv.contiguous()), ptr(mask.contiguous()), B, h, w, ratio,
+                                          ctypes.c_float(add), ctypes.c_float(mul), ptr(out), stream_of(inv)),
+          "dro_convex_upsample_forward")
+    return out
 
-    @staticmethod
-    def backward(ctx, gout):
-        lib = _lib.load()
-        inv, mask = ctx.saved_tensors
-        B, _, h, w = inv.shape
-        g_inv = torch.empty_like(inv) if ctx.needs_input_grad[0] else None
-        g_mask = torch.empty_like(mask)
-        check(lib.dro_convex_upsample_backward(ptr(inv), ptr(mask), ptr(gout.contiguous()), B, h, w,
-                                               ctx.ratio, ctypes.c_float(ctx.mul), ptr(g_inv), ptr(g_mask),
-                                               stream_of(inv)), "dro_convex_upsample_backward")
-        return g_inv, g_mask if ctx.needs_input_grad[1] else None, None, None, None
+
+@_convex_upsample_op.register_fake
+def _(inv, mask, ratio, add, mul):
+    B, _, h, w = inv.shape
+    return inv.new_empty((B, 1, h * ratio, w * ratio))
+
+
+@torch.library.custom_op("dro::convex_upsample_backward", mutates_args=())
+def _convex_upsample_bwd_op(inv: Tensor, mask: Tensor, grad_out: Tensor, ratio: int, mul: float,
+                            need_inv: bool) -> list[Tensor]:
+    """Backward of dro::convex_upsample: [g_inv (empty unless need_inv), g_mask]."""
+    lib = _lib.load()
+    B, _, h, w = inv.shape
+    g_inv = torch.empty_like(inv) if need_inv else None
+    g_mask = torch.empty_like(mask)
+    check(lib.dro_convex_upsample_backward(ptr(inv), ptr(mask), ptr(grad_out.contiguous()), B, h, w, ratio,
+                                           ctypes.c_float(mul), ptr(g_inv), ptr(g_mask), stream_of(inv)),
+          "dro_convex_upsample_backward")
+    return [g_inv if g_inv is not None else _none_like(inv.device), g_mask]
+
+
+@_convex_upsample_bwd_op.register_fake
+def _(inv, mask, grad_out, ratio, mul, need_inv):
+    return [inv.new_empty(inv.shape) if need_inv else inv.new_empty(0), mask.new_empty(mask.shape)]
+
+
+def _convex_upsample_setup(ctx, inputs, output):
+    inv, mask, ratio, add, mul = inputs
+    ctx.save_for_backward(inv.contiguous(), mask.contiguous())
+    ctx.cfg = (ratio, mul, inv.requires_grad, mask.requires_grad)
+
+
+def _convex_upsample_backward(ctx, gout):
+    inv, mask = ctx.saved_tensors
+    ratio, mul, need_inv, need_mask = ctx.cfg
+    g_inv, g_mask = torch.ops.dro.convex_upsample_backward(inv, mask, gout, ratio, mul, need_inv)
+    return _opt(g_inv), g_mask if need_mask else None, None, None, None
+
+
+torch.library.register_autograd("dro::convex_upsample", _convex_upsample_backward,
+                                setup_context=_convex_upsample_setup)
 
 
 def convex_upsample(inv, mask, ratio=8, affine=None):
     """DepthPoseNet.upsample_depth (DepthPoseNet.py:63-74): [B,1,h,w] -> [B,1,rh,rw];
     affine=(add, mul) folds `add + mul * out` (scale_inv_depth) into the kernel."""
+    require_device(inv, mask, what="convex_upsample")
+    B, _, h, w = inv.shape
+    if mask.shape != (B, 9 * ratio * ratio, h, w):
+        raise RuntimeError("convex_upsample: mask must be [B, 9*r*r, h, w]")
     add, mul = affine if affine is not None else (0.0, 1.0)
-    return _ConvexUpsample.apply(inv, mask, int(ratio), float(add), float(mul))
+    return torch.ops.dro.convex_upsample(inv, mask, int(ratio), float(add), float(mul))
 
 
 def _ptr_table(ts):
@@ -509,55 +710,91 @@ def _ptr_table(ts):
     return arr
 
 
-class _ConvexUpsampleMany(torch.autograd.Function):
-    """n convex upsamples in one launch each way -> [n, B, 1, rh, rw]."""
+@torch.library.custom_op("dro::convex_upsample_many", mutates_args=())
+def _convex_upsample_many_op(invs: list[Tensor], masks: list[Tensor], ratio: int, add: float,
+                             mul: float) -> Tensor:
+    """n convex upsamples in one launch: invs n x [B,1,h,w], masks n x
+    [B,9*r*r,h,w] -> [n,B,1,r*h,r*w]."""
+    lib = _lib.load()
+    invs = [t.contiguous() for t in invs]
+    masks = [t.contiguous() for t in masks]
+    require_device(*invs, *masks, what="convex_upsample_many")
+    n = len(invs)
+    B, _, h, w = invs[0].shape
+    out = torch.empty(n, B, 1, h * ratio, w * ratio, device=invs[0].device)
+    check(lib.dro_convex_upsample_many_forward(_ptr_table(invs), _ptr_table(masks), n, B, h, w, ratio,
+                                               ctypes.c_float(add), ctypes.c_float(mul), ptr(out), stream_of(out)),
+          "dro_convex_upsample_many_forward")
+    return out
 
-    @staticmethod
-    def forward(ctx, ratio, add, mul, n, *tensors):
-        lib = _lib.load()
-        invs = [t.contiguous() for t in tensors[:n]]
-        masks = [t.contiguous() for t in tensors[n:]]
-        require_device(*invs, *masks, what="convex_upsample_many")
-        B, _, h, w = invs[0].shape
-        for i, m in zip(invs, masks):
-            if i.shape != (B, 1, h, w) or m.shape != (B, 9 * ratio * ratio, h, w):
-                raise RuntimeError("convex_upsample_many: every inv must be [B,1,h,w] and mask [B,9*r*r,h,w]")
-        out = torch.empty(n, B, 1, h * ratio, w * ratio, device=invs[0].device, dtype=torch.float32)
-        check(lib.dro_convex_upsample_many_forward(_ptr_table(invs), _ptr_table(masks), n, B, h, w, ratio,
-                                                   ctypes.c_float(add), ctypes.c_float(mul), ptr(out),
-                                                   stream_of(out)), "dro_convex_upsample_many_forward")
-        ctx.save_for_backward(*invs, *masks)
-        ctx.n, ctx.ratio, ctx.mul = n, ratio, mul
-        return out
 
-    @staticmethod
-    def backward(ctx, gout):
-        lib = _lib.load()
-        n = ctx.n
-        saved = ctx.saved_tensors
-        invs, masks = saved[:n], saved[n:]
-        B, _, h, w = invs[0].shape
-        g_inv = [torch.empty_like(t) if ctx.needs_input_grad[4 + i] else None for i, t in enumerate(invs)]
-        g_mask = [torch.empty_like(m) for m in masks]
-        nb = int(lib.dro_convex_upsample_many_workspace_bytes(n, B, h, w))
-        ws = torch.empty(nb, dtype=torch.uint8, device=gout.device)
-        check(lib.dro_convex_upsample_many_backward(_ptr_table(invs), _ptr_table(masks), ptr(gout.contiguous()),
-                                                    n, B, h, w, ctx.ratio, ctypes.c_float(ctx.mul),
-                                                    _ptr_table(g_inv), _ptr_table(g_mask), ptr(ws), nb,
-                                                    stream_of(gout)), "dro_convex_upsample_many_backward")
-        g_mask = [g if ctx.needs_input_grad[4 + n + i] else None for i, g in enumerate(g_mask)]
-        return (None, None, None, None, *g_inv, *g_mask)
+@_convex_upsample_many_op.register_fake
+def _(invs, masks, ratio, add, mul):
+    B, _, h, w = invs[0].shape
+    return invs[0].new_empty((len(invs), B, 1, h * ratio, w * ratio))
+
+
+@torch.library.custom_op("dro::convex_upsample_many_backward", mutates_args=())
+def _convex_upsample_many_bwd_op(invs: list[Tensor], masks: list[Tensor], grad_out: Tensor, ratio: int, mul: float,
+                                 need_inv: list[bool]) -> list[Tensor]:
+    """Backward of dro::convex_upsample_many: the n inverse-depth gradients
+    (empty where not needed) followed by the n mask gradients; deterministic
+    (two passes, no atomics)."""
+    lib = _lib.load()
+    n = len(invs)
+    B, _, h, w = invs[0].shape
+    g_inv = [torch.empty_like(t) if need_inv[i] else None for i, t in enumerate(invs)]
+    g_mask = [torch.empty_like(m) for m in masks]
+    nb = int(lib.dro_convex_upsample_many_workspace_bytes(n, B, h, w))
+    ws = torch.empty(nb, dtype=torch.uint8, device=grad_out.device)
+    check(lib.dro_convex_upsample_many_backward(_ptr_table(invs), _ptr_table(masks), ptr(grad_out.contiguous()),
+                                                n, B, h, w, ratio, ctypes.c_float(mul), _ptr_table(g_inv),
+                                                _ptr_table(g_mask), ptr(ws), nb, stream_of(grad_out)),
+          "dro_convex_upsample_many_backward")
+    return [g if g is not None else _none_like(grad_out.device) for g in g_inv] + g_mask
+
+
+@_convex_upsample_many_bwd_op.register_fake
+def _(invs, masks, grad_out, ratio, mul, need_inv):
+    return ([t.new_empty(t.shape) if need_inv[i] else t.new_empty(0) for i, t in enumerate(invs)] +
+            [m.new_empty(m.shape) for m in masks])
+
+
+def _convex_upsample_many_setup(ctx, inputs, output):
+    invs, masks, ratio, add, mul = inputs
+    invs = [t.contiguous() for t in invs]
+    masks = [t.contiguous() for t in masks]
+    ctx.save_for_backward(*invs, *masks)
+    ctx.cfg = (len(invs), ratio, mul, [t.requires_grad for t in invs], [m.requires_grad for m in masks])
+
+
+def _convex_upsample_many_backward(ctx, gout):
+    n, ratio, mul, need_inv, need_mask = ctx.cfg
+    saved = ctx.saved_tensors
+    g = torch.ops.dro.convex_upsample_many_backward(list(saved[:n]), list(saved[n:]), gout, ratio, mul, need_inv)
+    g_inv = [_opt(t) for t in g[:n]]
+    g_mask = [t if need_mask[i] else None for i, t in enumerate(g[n:])]
+    return g_inv, g_mask, None, None, None
+
+
+torch.library.register_autograd("dro::convex_upsample_many", _convex_upsample_many_backward,
+                                setup_context=_convex_upsample_many_setup)
 
 
 def convex_upsample_many(invs, masks, ratio=8, affine=None):
     """convex_upsample of n (inv, mask) pairs in one launch each way: returns the
     stacked [n, B, 1, rh, rw] (the losses read the predictions stacked;
     stacked_view() recovers it from its unbind() views).  Deterministic
-    backward (no atomics)."""
+    backward (no atomics).  torch.ops.dro.convex_upsample_many underneath."""
     if not 1 <= len(invs) == len(masks) <= 32:
         raise RuntimeError("convex_upsample_many: 1..32 (inv, mask) pairs")
+    require_device(*invs, *masks, what="convex_upsample_many")
+    B, _, h, w = invs[0].shape
+    for i, m in zip(invs, masks):
+        if i.shape != (B, 1, h, w) or m.shape != (B, 9 * ratio * ratio, h, w):
+            raise RuntimeError("convex_upsample_many: every inv must be [B,1,h,w] and mask [B,9*r*r,h,w]")
     add, mul = affine if affine is not None else (0.0, 1.0)
-    return _ConvexUpsampleMany.apply(int(ratio), float(add), float(mul), len(invs), *invs, *masks)
+    return torch.ops.dro.convex_upsample_many(list(invs), list(masks), int(ratio), float(add), float(mul))
 
 
 def stacked_view(ts):
@@ -574,28 +811,44 @@ def stacked_view(ts):
 
 
 # ------------------------------------------------------------------ bilinear 2x upsample
-class _Bilinear2x(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x):
-        lib = _lib.load()
-        require_device(x, what="bilinear_upsample2x")
-        N, C, h, w = x.shape
-        x = x.contiguous()
-        out = torch.empty(N, C, 2 * h, 2 * w, device=x.device, dtype=torch.float32)
-        check(lib.dro_bilinear_upsample2x_forward(ptr(x), N * C, h, w, ptr(out), stream_of(x)),
-              "dro_bilinear_upsample2x_forward")
-        ctx.shape = (N, C, h, w)
-        return out
+@torch.library.custom_op("dro::bilinear_upsample2x", mutates_args=())
+def _bilinear2x_op(x: Tensor) -> Tensor:
+    """F.interpolate(x, scale_factor=2, bilinear, align_corners=False), float32 NCHW."""
+    lib = _lib.load()
+    require_device(x, what="bilinear_upsample2x")
+    N, C, h, w = x.shape
+    out = torch.empty(N, C, 2 * h, 2 * w, device=x.device)
+    check(lib.dro_bilinear_upsample2x_forward(ptr(x.contiguous()), N * C, h, w, ptr(out), stream_of(x)),
+          "dro_bilinear_upsample2x_forward")
+    return out
 
-    @staticmethod
-    def backward(ctx, gout):
-        lib = _lib.load()
-        N, C, h, w = ctx.shape
-        gout = gout.contiguous()
-        gx = torch.empty(N, C, h, w, device=gout.device, dtype=torch.float32)
-        check(lib.dro_bilinear_upsample2x_backward(ptr(gout), N * C, h, w, ptr(gx), stream_of(gout)),
-              "dro_bilinear_upsample2x_backward")
-        return gx
+
+@_bilinear2x_op.register_fake
+def _(x):
+    N, C, h, w = x.shape
+    return x.new_empty((N, C, 2 * h, 2 * w))
+
+
+@torch.library.custom_op("dro::bilinear_upsample2x_backward", mutates_args=())
+def _bilinear2x_bwd_op(grad_out: Tensor) -> Tensor:
+    lib = _lib.load()
+    N, C, H2, W2 = grad_out.shape
+    h, w = H2 // 2, W2 // 2
+    gx = torch.empty(N, C, h, w, device=grad_out.device)
+    check(lib.dro_bilinear_upsample2x_backward(ptr(grad_out.contiguous()), N * C, h, w, ptr(gx), stream_of(grad_out)),
+          "dro_bilinear_upsample2x_backward")
+    return gx
+
+
+@_bilinear2x_bwd_op.register_fake
+def _(grad_out):
+    N, C, H2, W2 = grad_out.shape
+    return grad_out.new_empty((N, C, H2 // 2, W2 // 2))
+
+
+torch.library.register_autograd("dro::bilinear_upsample2x",
+                                lambda ctx, g: torch.ops.dro.bilinear_upsample2x_backward(g),
+                                setup_context=lambda ctx, inputs, output: None)
 
 
 def bilinear_upsample2x(x):
@@ -603,37 +856,55 @@ def bilinear_upsample2x(x):
     NCHW (reference networks/optim/extractor.py:91-97); deterministic backward."""
     if x.dtype != torch.float32 or x.dim() != 4:
         raise RuntimeError("bilinear_upsample2x: expects a float32 NCHW tensor")
-    return _Bilinear2x.apply(x)
+    return torch.ops.dro.bilinear_upsample2x(x)
 
 
 # ------------------------------------------------------------------ ResNet stem max pooling
-class _MaxPool3s2(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x):
-        lib = _lib.load()
-        require_device(x, what="maxpool3x3s2")
-        N, C, H, W = x.shape
-        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-        x = x.contiguous()
-        y = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.float32)
-        arg = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.uint8)
-        check(lib.dro_maxpool3x3s2_forward(ptr(x), N * C, H, W, ptr(y), ptr(arg), stream_of(x)),
-              "dro_maxpool3x3s2_forward")
-        ctx.save_for_backward(arg)
-        ctx.shape = (N, C, H, W)
-        ctx.mark_non_differentiable(arg)
-        return y
+@torch.library.custom_op("dro::maxpool3x3s2", mutates_args=())
+def _maxpool_op(x: Tensor) -> tuple[Tensor, Tensor]:
+    """F.max_pool2d(x, 3, 2, 1): (y, argmax uint8 in the 3x3 window)."""
+    lib = _lib.load()
+    require_device(x, what="maxpool3x3s2")
+    N, C, H, W = x.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty(N, C, Ho, Wo, device=x.device)
+    arg = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.uint8)
+    check(lib.dro_maxpool3x3s2_forward(ptr(x.contiguous()), N * C, H, W, ptr(y), ptr(arg), stream_of(x)),
+          "dro_maxpool3x3s2_forward")
+    return y, arg
 
-    @staticmethod
-    def backward(ctx, gy):
-        lib = _lib.load()
-        (arg,) = ctx.saved_tensors
-        N, C, H, W = ctx.shape
-        gy = gy.contiguous()
-        gx = torch.empty(N, C, H, W, device=gy.device, dtype=torch.float32)
-        check(lib.dro_maxpool3x3s2_backward(ptr(gy), ptr(arg), N * C, H, W, ptr(gx), stream_of(gy)),
-              "dro_maxpool3x3s2_backward")
-        return gx
+
+@_maxpool_op.register_fake
+def _(x):
+    N, C, H, W = x.shape
+    sh = (N, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1)
+    return x.new_empty(sh), x.new_empty(sh, dtype=torch.uint8)
+
+
+@torch.library.custom_op("dro::maxpool3x3s2_backward", mutates_args=())
+def _maxpool_bwd_op(grad_out: Tensor, argmax: Tensor, H: int, W: int) -> Tensor:
+    lib = _lib.load()
+    N, C = grad_out.shape[:2]
+    gx = torch.empty(N, C, H, W, device=grad_out.device)
+    check(lib.dro_maxpool3x3s2_backward(ptr(grad_out.contiguous()), ptr(argmax), N * C, H, W, ptr(gx),
+                                        stream_of(grad_out)), "dro_maxpool3x3s2_backward")
+    return gx
+
+
+@_maxpool_bwd_op.register_fake
+def _(grad_out, argmax, H, W):
+    return grad_out.new_empty((grad_out.shape[0], grad_out.shape[1], H, W))
+
+
+def _maxpool_setup(ctx, inputs, output):
+    ctx.save_for_backward(output[1])
+    ctx.hw = inputs[0].shape[2:]
+    ctx.mark_non_differentiable(output[1])
+
+
+torch.library.register_autograd(
+    "dro::maxpool3x3s2", lambda ctx, gy, _garg: torch.ops.dro.maxpool3x3s2_backward(gy, ctx.saved_tensors[0], *ctx.hw),
+    setup_context=_maxpool_setup)
 
 
 def maxpool3x3s2(x):
@@ -642,7 +913,128 @@ def maxpool3x3s2(x):
     backward, one argmax byte per output instead of int64 indices."""
     if x.dtype != torch.float32 or x.dim() != 4:
         raise RuntimeError("maxpool3x3s2: expects a float32 NCHW tensor")
-    return _MaxPool3s2.apply(x)
+    return torch.ops.dro.maxpool3x3s2(x)[0]
+
+
+# ------------------------------------------------------------------ PoseHead mean
+@torch.library.custom_op("dro::pose_mean", mutates_args=())
+def _pose_mean_op(y: Tensor, pose: Optional[Tensor], rot_scale: float) -> Tensor:
+    """PoseHead's output (update.py:16-28): y.mean((2, 3)) [B,C] with channels
+    3..5 scaled by rot_scale, plus `pose` [B,C] when given."""
+    lib = _lib.load()
+    require_device(y, pose, what="pose_mean")
+    B, C, H, W = y.shape
+    out = torch.empty(B, C, device=y.device)
+    check(lib.dro_pose_mean_forward(ptr(y.contiguous()), ptr(pose.contiguous() if pose is not None else None),
+                                    ptr(out), B, C, H * W, float(rot_scale), stream_of(y)), "dro_pose_mean_forward")
+    return out
+
+
+@_pose_mean_op.register_fake
+def _(y, pose, rot_scale):
+    return y.new_empty(y.shape[:2])
+
+
+@torch.library.custom_op("dro::pose_mean_backward", mutates_args=())
+def _pose_mean_bwd_op(grad_out: Tensor, H: int, W: int, rot_scale: float) -> Tensor:
+    lib = _lib.load()
+    B, C = grad_out.shape
+    gy = torch.empty(B, C, H, W, device=grad_out.device)
+    check(lib.dro_pose_mean_backward(ptr(grad_out.contiguous()), ptr(gy), B, C, H * W, float(rot_scale),
+                                     stream_of(grad_out)), "dro_pose_mean_backward")
+    return gy
+
+
+@_pose_mean_bwd_op.register_fake
+def _(grad_out, H, W, rot_scale):
+    return grad_out.new_empty((*grad_out.shape, H, W))
+
+
+def _pose_mean_setup(ctx, inputs, output):
+    y, pose, rot_scale = inputs
+    ctx.cfg = (y.shape[2], y.shape[3], rot_scale, pose is not None and pose.requires_grad)
+
+
+def _pose_mean_backward(ctx, gout):
+    H, W, rs, pose_grad = ctx.cfg
+    return torch.ops.dro.pose_mean_backward(gout, H, W, rs), (gout if pose_grad else None), None
+
+
+torch.library.register_autograd("dro::pose_mean", _pose_mean_backward, setup_context=_pose_mean_setup)
+
+
+def pose_mean(y, rot_scale=0.01, pose=None):
+    """PoseHead's output (update.py:16-28) -- y.mean((2, 3)) with the rotation
+    channels (3..5) scaled by rot_scale -- plus `pose` when given (the update
+    `pose + pose_head(net)`, update.py:189-197): one launch forward, one
+    backward.  y [B, C, H, W], pose [B, C].  torch.ops.dro.pose_mean."""
+    require_device(y, pose, what="pose_mean")
+    return torch.ops.dro.pose_mean(y, pose, float(rot_scale))
+
+
+# ------------------------------------------------------------------ training-mode BatchNorm (+ skip) (+ ReLU)
+# Not a torch.library op: its launch updates the running statistics in place
+# (fused into the statistics pass), and torch.library refuses an autograd
+# formula for an op that mutates inputs; splitting the update out would add
+# two launches per BN site (~120 per step).
+class _BatchNormAct(torch.autograd.Function):
+    """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, skip, running_mean, running_var, num_batches, relu, eps,
+                momentum):
+        lib = _lib.load()
+        require_device(x, what="batchnorm_act")
+        N, C, H, W = x.shape
+        x = x.contiguous()
+        skip = skip.contiguous() if skip is not None else None
+        y = torch.empty_like(x)
+        smean = torch.empty(C, device=x.device, dtype=torch.float32)
+        sinv = torch.empty(C, device=x.device, dtype=torch.float32)
+        nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        check(lib.dro_batchnorm_relu_forward(
+            ptr(x), ptr(weight), ptr(bias), ptr(skip), int(relu), N, C, H * W, float(eps),
+            float(momentum), ptr(running_mean), ptr(running_var), ptr(num_batches), ptr(y),
+            ptr(smean), ptr(sinv), ptr(ws), nws, stream_of(x)), "dro_batchnorm_relu_forward")
+        ctx.save_for_backward(x, y, weight, smean, sinv)
+        ctx.relu, ctx.has_skip = int(relu), skip is not None
+        ctx.affine = (weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = _lib.load()
+        x, y, weight, smean, sinv = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gy = gy.contiguous()
+        gx = torch.empty_like(x)
+        gw = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[0] else None
+        gb = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[1] else None
+        gs = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
+        nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        check(lib.dro_batchnorm_relu_backward(
+            ptr(gy), ptr(x), ptr(y), ptr(weight), ptr(smean), ptr(sinv), ctx.relu, N, C, H * W,
+            ptr(gx), ptr(gw), ptr(gb), ptr(gs), ptr(ws), nws, stream_of(gy)),
+            "dro_batchnorm_relu_backward")
+        return gx, gw, gb, gs, None, None, None, None, None, None
+
+
+def batchnorm_act(x, bn, skip=None, relu=True):
+    """act(bn(x) + skip) for a training-mode nn.BatchNorm2d `bn` (float32 NCHW):
+    torch.nn.functional.batch_norm(training=True) semantics, including the
+    running-statistics update and num_batches_tracked (reference
+    networks/optim/extractor.py:7-107 via torchvision's BasicBlock)."""
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError("batchnorm_act: expects a float32 NCHW tensor")
+    if bn.momentum is None:
+        raise NotImplementedError("batchnorm_act: cumulative averaging (momentum=None)")
+    track = bn.track_running_stats and bn.running_mean is not None
+    return _BatchNormAct.apply(
+        x, bn.weight, bn.bias, skip, bn.running_mean if track else None,
+        bn.running_var if track else None, bn.num_batches_tracked if track else None,
+        1 if relu else 0, bn.eps, bn.momentum)
 
 
 # ------------------------------------------------------------------ depth evaluation metrics
@@ -740,94 +1132,3 @@ def depth_metrics_demon(gt, gt_pose, pred, min_depth, max_depth, use_gt_scale=Tr
     return out
 
 
-class _PoseMean(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, y, pose, rot_scale):
-        lib = _lib.load()
-        require_device(y, pose, what="pose_mean")
-        B, C, H, W = y.shape
-        y = y.contiguous()
-        p = pose.contiguous() if pose is not None else None
-        out = torch.empty(B, C, device=y.device, dtype=torch.float32)
-        check(lib.dro_pose_mean_forward(ptr(y), ptr(p), ptr(out), B, C, H * W, float(rot_scale), stream_of(y)),
-              "dro_pose_mean_forward")
-        ctx.meta = (B, C, H, W, float(rot_scale), pose is not None)
-        return out
-
-    @staticmethod
-    def backward(ctx, gout):
-        lib = _lib.load()
-        B, C, H, W, rs, has_pose = ctx.meta
-        gout = gout.contiguous()
-        gy = torch.empty(B, C, H, W, device=gout.device, dtype=torch.float32)
-        check(lib.dro_pose_mean_backward(ptr(gout), ptr(gy), B, C, H * W, rs, stream_of(gout)),
-              "dro_pose_mean_backward")
-        return gy, (gout if has_pose and ctx.needs_input_grad[1] else None), None
-
-
-def pose_mean(y, rot_scale=0.01, pose=None):
-    """PoseHead's output (update.py:16-28) -- y.mean((2, 3)) with the rotation
-    channels (3..5) scaled by rot_scale -- plus `pose` when given (the update
-    `pose + pose_head(net)`, update.py:189-197): one launch forward, one
-    backward.  y [B, C, H, W], pose [B, C]."""
-    return _PoseMean.apply(y, pose, rot_scale)
-
-
-class _BatchNormAct(torch.autograd.Function):
-    """Training-mode BN (+ skip) (+ ReLU) in two launches each way (csrc/batchnorm.hip)."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias, skip, running_mean, running_var, num_batches, relu, eps,
-                momentum):
-        lib = _lib.load()
-        require_device(x, what="batchnorm_act")
-        N, C, H, W = x.shape
-        x = x.contiguous()
-        skip = skip.contiguous() if skip is not None else None
-        y = torch.empty_like(x)
-        smean = torch.empty(C, device=x.device, dtype=torch.float32)
-        sinv = torch.empty(C, device=x.device, dtype=torch.float32)
-        nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
-        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
-        check(lib.dro_batchnorm_relu_forward(
-            ptr(x), ptr(weight), ptr(bias), ptr(skip), int(relu), N, C, H * W, float(eps),
-            float(momentum), ptr(running_mean), ptr(running_var), ptr(num_batches), ptr(y),
-            ptr(smean), ptr(sinv), ptr(ws), nws, stream_of(x)), "dro_batchnorm_relu_forward")
-        ctx.save_for_backward(x, y, weight, smean, sinv)
-        ctx.relu, ctx.has_skip = int(relu), skip is not None
-        ctx.affine = (weight is not None, bias is not None)
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        lib = _lib.load()
-        x, y, weight, smean, sinv = ctx.saved_tensors
-        N, C, H, W = x.shape
-        gy = gy.contiguous()
-        gx = torch.empty_like(x)
-        gw = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[0] else None
-        gb = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[1] else None
-        gs = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
-        nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
-        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
-        check(lib.dro_batchnorm_relu_backward(
-            ptr(gy), ptr(x), ptr(y), ptr(weight), ptr(smean), ptr(sinv), ctx.relu, N, C, H * W,
-            ptr(gx), ptr(gw), ptr(gb), ptr(gs), ptr(ws), nws, stream_of(gy)),
-            "dro_batchnorm_relu_backward")
-        return gx, gw, gb, gs, None, None, None, None, None, None
-
-
-def batchnorm_act(x, bn, skip=None, relu=True):
-    """act(bn(x) + skip) for a training-mode nn.BatchNorm2d `bn` (float32 NCHW):
-    torch.nn.functional.batch_norm(training=True) semantics, including the
-    running-statistics update and num_batches_tracked (reference
-    networks/optim/extractor.py:7-107 via torchvision's BasicBlock)."""
-    if x.dtype != torch.float32 or x.dim() != 4:
-        raise RuntimeError("batchnorm_act: expects a float32 NCHW tensor")
-    if bn.momentum is None:
-        raise NotImplementedError("batchnorm_act: cumulative averaging (momentum=None)")
-    track = bn.track_running_stats and bn.running_mean is not None
-    return _BatchNormAct.apply(
-        x, bn.weight, bn.bias, skip, bn.running_mean if track else None,
-        bn.running_var if track else None, bn.num_batches_tracked if track else None,
-        1 if relu else 0, bn.eps, bn.momentum)

@@ -106,6 +106,10 @@ class GradBuckets:
         self.issued = []              # bucket indices in issue order (last step; tests)
         self.issued_in_backward = 0   # of those, issued from backward hooks (tests)
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        # the stream every bucket's collective is issued from: created here, never
+        # during a graph capture (a stream first created inside a capture was
+        # the common factor of round 3's capture_end crashes)
+        self._comm = torch.cuda.Stream(device=self.flat.device) if self.flat.is_cuda else None
         for p in self.params:
             # hip convs may accumulate this gradient in place (hip/conv.py, direct path)
             p._dro_direct = True
@@ -202,28 +206,20 @@ class GradBuckets:
             self._next += 1
             self.issued.append(b)
             if self.reduce and not self.suspend:
-                side = self._bside[b] if self.flat.is_cuda else ()
-                if side:
-                    # in-place weight gradients from another stream: issue from a
-                    # comm stream that waits for them and for the gather
-                    comm = self._comm_stream()
-                    comm.wait_event(self._events[b])
-                    for st in side:
-                        comm.wait_stream(st)
-                    with torch.cuda.stream(comm):
-                        self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
-                                                             group=self.group, async_op=True))
+                if self._comm is None:                       # CPU (gloo tests)
+                    self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
+                                                         group=self.group, async_op=True))
                     continue
-                if self._events[b] is not None:
-                    torch.cuda.current_stream().wait_event(self._events[b])
-                self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
-                                                     group=self.group, async_op=True))
-
-    def _comm_stream(self):
-        st = getattr(self, "_comm", None)
-        if st is None:
-            st = self._comm = torch.cuda.Stream(device=self.flat.device)
-        return st
+                # from the comm stream, after the bucket's gather (its event) and
+                # any in-place weight gradients written on another stream: the
+                # backward's next kernels on the compute streams do not wait for it
+                comm = self._comm
+                comm.wait_event(self._events[b])
+                for st in self._bside[b]:
+                    comm.wait_stream(st)
+                with torch.cuda.stream(comm):
+                    self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
+                                                         group=self.group, async_op=True))
 
     def _gather(self, b):
         """Copy bucket b's adopted gradients into the flat buffer (one launch).
@@ -286,6 +282,8 @@ class GradBuckets:
             for work in self._pending:
                 work.wait()
             self._pending = []
+            if self._comm is not None and self.reduce and not self.suspend:
+                torch.cuda.current_stream().wait_stream(self._comm)
         if self.world > 1 and not self.suspend:
             self.flat.div_(self.world)
 
@@ -585,13 +583,15 @@ class GraphedTrainStep:
     The first eager steps (bucket discovery, MIOpen algorithm selection) run
     before capture on a side stream and are real training steps.
 
-    With a gradient exchange (world > 1), the graph holds zero -> forward ->
-    loss -> backward only; each step() replays it, then all-reduces the flat
-    gradient eagerly (ONE RCCL collective) and runs the fused Adam launch.
-    RCCL collectives captured inside the graph (`reduce_in_graph=True`, the
-    bucketed all-reduces overlapping backward) crash this image's RCCL
-    (2.26.6 / HIP 7.0) in hipStreamEndCapture (SIGSEGV at capture_end, seen at
-    world size 1 with the collectives forced on), so they stay opt-in.
+    With a gradient exchange over RCCL (world > 1, backend "nccl"), the
+    bucketed all-reduces are captured IN the graph (reduce_in_graph, the
+    default): each bucket's collective is issued from the backward hook that
+    completes it, on the comm stream, so the replayed graph runs it beside the
+    rest of the backward (horovod_trainer.py:66-69's DistributedOptimizer
+    hooks, done as graph branches).  With any other backend (gloo: the CPU
+    tests and the one-GPU rehearsal), or reduce_in_graph=False, the graph
+    holds zero -> forward -> loss -> backward and each step() all-reduces the
+    flat gradient after the replay, then runs Adam.
 
     The graphs hold the ADDRESSES of the parameters, gradients and Adam state:
     restore checkpoints in place (tensor.copy_), or build a new GraphedTrainStep
@@ -599,9 +599,13 @@ class GraphedTrainStep:
     """
 
     def __init__(self, trainer, example_batch, warmup=3, flips=(False, True), share_pool=True,
-                 reduce_in_graph=False):
+                 reduce_in_graph=None):
         self.tr = trainer
-        # collectives outside the graph when there is an exchange at all
+        if reduce_in_graph is None:
+            reduce_in_graph = (os.environ.get("DRO_REDUCE_IN_GRAPH", "1") != "0" and dist.is_initialized()
+                               and dist.get_backend(trainer.grads.group) == "nccl")
+        self.in_graph = trainer.grads.reduce and bool(reduce_in_graph)
+        # collectives outside the graph when there is an exchange that is not captured
         self.outside = trainer.grads.reduce and not reduce_in_graph
         self.model = trainer.model
         self.static = _clone_batch(example_batch)

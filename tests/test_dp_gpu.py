@@ -7,12 +7,11 @@
   the mean of the two per-rank losses -- the exact data-parallel semantics with
   per-replica BatchNorm statistics (no SyncBN, as the reference).
 * RCCL with the captured hipGraph step: a world-size-1 "nccl" (RCCL) group
-  with the exchange forced on (always_reduce); GraphedTrainStep (graph of
-  zero -> forward -> backward, then ONE eager RCCL all-reduce and Adam, its
-  world > 1 mode) replay vs the eager step (bucketed all-reduces issued from
-  the backward hooks) from the same state.  Collectives captured INSIDE the
-  graph crash this image's RCCL at capture_end (SIGSEGV): opt-in only
-  (GraphedTrainStep reduce_in_graph), not run here.
+  with the exchange forced on (always_reduce); GraphedTrainStep replay vs the
+  eager step (bucketed all-reduces issued from the backward hooks) from the
+  same state, in both of its modes: the bucketed all-reduces captured INSIDE
+  the graph from the backward hooks (the default at world > 1 over RCCL:
+  they overlap the rest of the backward), and the exchange after the replay.
 
 Reference: horovod_trainer.py:67-69 (dormant DistributedOptimizer),
 model_wrapper.py:818-822 (DistributedSampler).
@@ -136,7 +135,7 @@ def test_two_ranks_one_gpu_real_model_direct_weight_grads():
         assert l2 < 1e-5 and mx < 1e-4, (s, l2, mx)
 
 
-def _rccl_graph_worker(rank, port, out):
+def _rccl_graph_worker(rank, port, out, in_graph):
     """World-size-1 RCCL group; GraphedTrainStep with the exchange after the
     replayed graph; replay vs eager from the same state.  Runs in a child process so
     that RCCL's watchdog or teardown cannot take the test runner down."""
@@ -157,11 +156,12 @@ def _rccl_graph_worker(rank, port, out):
         K0 = batch["intrinsics"].clone()
         m = _model()
         tr = DataParallelTrainer(m, capturable=True, bucket_mb=4.0, always_reduce=True)
-        stage("trainer built; capturing")
-        gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False,))
+        stage(f"trainer built; capturing (in_graph={in_graph})")
+        gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False,), reduce_in_graph=in_graph)
         stage("captured")
-        assert gs.outside, "the exchange must run outside the captured graph"
+        assert gs.in_graph == in_graph and gs.outside == (not in_graph)
         nb, issued = len(tr.grads.buckets), list(tr.grads.issued)
+        in_bwd = tr.grads.issued_in_backward
         snap_m = {k: v.clone() for k, v in m.state_dict().items()}
         snap_s = [{k: v.clone() for k, v in st.items()} for st in tr.optimizer.state.values()]
 
@@ -183,7 +183,7 @@ def _rccl_graph_worker(rank, port, out):
         le = tr.step(batch, flip=False)[0].clone()
         ge = tr.grads.flat.clone()
         torch.cuda.synchronize()
-        out["res"] = (nb, issued, O.rel_err(lg.cpu(), le.cpu()), float((gg - ge).norm() / ge.norm()))
+        out["res"] = (nb, issued, in_bwd, O.rel_err(lg.cpu(), le.cpu()), float((gg - ge).norm() / ge.norm()))
     stage("results recorded; teardown")
     # the graphs hold RCCL kernels of this communicator: release them first
     del gs
@@ -194,13 +194,19 @@ def _rccl_graph_worker(rank, port, out):
 
 
 @pytest.mark.timeout(300)
-def test_rccl_exchange_with_captured_graph_step():
-    """RCCL (forced on at world size 1) around the step's hipGraph: replay +
-    all-reduce + Adam == the eager step with hook-issued bucket all-reduces."""
+@pytest.mark.parametrize("in_graph", [True, False])
+def test_rccl_exchange_with_captured_graph_step(in_graph):
+    """RCCL (forced on at world size 1) with the step's hipGraph -- the bucketed
+    all-reduces captured inside it from the backward hooks (in_graph), or one
+    all-reduce after the replay: replay == the eager step with hook-issued
+    bucket all-reduces, and in the captured step every bucket's collective was
+    issued from the backward hooks, in the common order."""
     with mp.Manager() as mgr:
         out = mgr.dict()
-        mp.spawn(_rccl_graph_worker, args=(_free_port(), out), nprocs=1, join=True)
-        nb, issued, loss_err, grad_err = out["res"]
+        mp.spawn(_rccl_graph_worker, args=(_free_port(), out, in_graph), nprocs=1, join=True)
+        nb, issued, in_bwd, loss_err, grad_err = out["res"]
     assert nb > 2 and issued == list(range(nb))
+    if in_graph:
+        assert in_bwd == nb, (in_bwd, nb)
     assert loss_err < 1e-5
     assert grad_err < 1e-4

@@ -512,10 +512,21 @@ def _grad_check(model, g64, tensor_tol=GRAD_TENSOR_TOL, l2_tol=GRAD_L2_TOL):
     den = sum(float(g64[k].double().pow(2).sum()) for k, _ in named)
     num = sum(float((g.double().cpu() - g64[k].double()).pow(2).sum()) for k, g in named)
     l2 = (num / den) ** 0.5
-    bad = [(k, e) for k, g in named for e in [rel(g, g64[k])] if e > tensor_tol]
+    errs = {k: rel(g, g64[k]) for k, g in named}
+    bad = [(k, e) for k, e in errs.items() if e > tensor_tol]
     if l2 > l2_tol:
         bad.append(("<global L2>", l2))
+    _log_margins("grad_check", l2=l2, worst=sorted(errs.items(), key=lambda t: -t[1])[:5])
     return sorted(bad, key=lambda t: -t[1]), l2
+
+
+def _log_margins(kind, **info):
+    """DRO_PARITY_LOG=<file>: append the measured errors (for DESIGN.md)."""
+    path = os.environ.get("DRO_PARITY_LOG")
+    if path:
+        import json
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", ""), "kind": kind, **info}) + "\n")
 
 
 def _fixture_check(model, fixture, g64, tensor_tol=GRAD_TENSOR_TOL):
@@ -529,6 +540,8 @@ def _fixture_check(model, fixture, g64, tensor_tol=GRAD_TENSOR_TOL):
     e_hip = grad_errors(named, fixture)
     e_ref = grad_errors(list(g64.items()), fixture)        # reference vs exact
     bad = [(k, e, e_ref[k] + tensor_tol) for k, e in e_hip.items() if e > e_ref[k] + tensor_tol]
+    _log_margins("fixture_check", worst=sorted(((k, e, e_ref[k]) for k, e in e_hip.items()),
+                                               key=lambda t: -(t[1] - t[2]))[:5])
     return bad, e_hip, e_ref
 
 
