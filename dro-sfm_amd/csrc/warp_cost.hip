@@ -369,6 +369,86 @@ __global__ __launch_bounds__(256) void plane_sweep_wide_kernel(WarpArgs a, const
   }
 }
 
+// LDS variant (round 4): a block owns CG channels of one batch image and DG
+// planes.  The CG reference channel planes (CG * h * w floats, <= 64 KB) are
+// staged into LDS once with 16-B loads and serve every plane and pixel of the
+// block, so the tap gathers are ds_read_b32 instead of global gathers; each
+// thread takes 4 consecutive pixels (one projection each per plane), reads the
+// target features as one 16-B load per channel and writes the 4 costs as one
+// 16-B non-temporal store.  Same arithmetic as plane_sweep_wide_kernel (taps
+// in nw, ne, sw, se order; zero weights for out-of-image taps), so the volume
+// is bit-identical to one warp_cost call per plane.
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+template <int CG>
+__global__ __launch_bounds__(256) void plane_sweep_lds_kernel(WarpArgs a, const float* __restrict__ disp, int D,
+                                                              int DG, float* __restrict__ cost) {
+  extern __shared__ float4 lds4[];
+  float* fr_l = reinterpret_cast<float*>(lds4);
+  const int P = a.h * a.w, P4 = P >> 2;
+  const int ncg = a.C / CG, ndg = (D + DG - 1) / DG;
+  // block -> (b, plane group, channel group); channel groups of one plane
+  // group are adjacent (they share the projections' inputs in L2)
+  int blk = blockIdx.x;
+  const int cg = blk % ncg;
+  blk /= ncg;
+  const int dg = blk % ndg;
+  const int b = blk / ndg;
+  const int c0 = cg * CG;
+  {   // stage fref[b, c0 .. c0+CG) (contiguous) into LDS
+    const float4* src = reinterpret_cast<const float4*>(a.fmap_ref + ((size_t)b * a.C + c0) * P);
+    for (int i = threadIdx.x; i < CG * P4; i += 256) lds4[i] = src[i];
+  }
+  __syncthreads();
+  float ki[9], kr[9];
+  cams(a, b, ki, kr);
+  float R[9], t[3];
+  load_pose(a.pose + (size_t)b * pose_stride(a.pose_mode), a.pose_mode, R, t);
+  const float4* fm4 = reinterpret_cast<const float4*>(a.fmap + ((size_t)b * a.C + c0) * P);
+  const int d_end = min(D, (dg + 1) * DG);
+  for (int d = dg * DG; d < d_end; ++d) {
+    float dd;
+    const float depth = decode_depth(disp[d], DRO_DEPTH_DISP, a.min_disp, a.span, &dd);
+    v4f* out4 = reinterpret_cast<v4f*>(cost + (((size_t)b * D + d) * a.C + c0) * P);
+    for (int q = threadIdx.x; q < P4; q += 256) {
+      int idx[4][4];
+      float wgt[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = 4 * q + k;
+        Proj pr;
+        project(ki, kr, R, t, (float)(p % a.w), (float)(p / a.w), depth, a.h, a.w, pr);
+        Taps T;
+        bilinear_taps(pr.ix, pr.iy, a.h, a.w, T);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          idx[k][e] = T.ok[e] ? T.idx[e] : 0;
+          wgt[k][e] = T.ok[e] ? T.wgt[e] : 0.f;
+        }
+      }
+#pragma unroll 2
+      for (int c = 0; c < CG; ++c) {
+        const float* pl = fr_l + c * P;
+        const float4 f = fm4[(size_t)c * P4 + q];
+        const float fv[4] = {f.x, f.y, f.z, f.w};
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float val = 0.f;
+          val += pl[idx[k][0]] * wgt[k][0];
+          val += pl[idx[k][1]] * wgt[k][1];
+          val += pl[idx[k][2]] * wgt[k][2];
+          val += pl[idx[k][3]] * wgt[k][3];
+          const float df = fv[k] - val;
+          o[k] = df * df;
+        }
+        const v4f ov = {o[0], o[1], o[2], o[3]};
+        __builtin_nontemporal_store(ov, out4 + (size_t)c * P4 + q);
+      }
+    }
+  }
+}
+
 int launch_pose_finalize(const double* partial, int nblk, int npose, const float* pose,
                          int pose_mode, float* gpose, hipStream_t s) {
   if (npose <= 0) return 0;
@@ -579,6 +659,28 @@ extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref,
   WarpArgs a = make_args(fmap, fmap_ref, nullptr, DRO_DEPTH_DISP, min_disp, max_disp, K, ref_K,
                          scale, pose, pose_mode, B, 1, C, h, w, 0);
   const int P = h * w;
+  // LDS path: 4-pixel vectors need P % 4 == 0 (and 16-B aligned maps); the
+  // channel group's reference planes must fit 64 KB of LDS
+  const bool aligned = ((reinterpret_cast<uintptr_t>(fmap) | reinterpret_cast<uintptr_t>(fmap_ref) |
+                         reinterpret_cast<uintptr_t>(cost)) & 15) == 0;
+  int CG = 8;
+  while (CG > 1 && (C % CG != 0 || (size_t)CG * P * sizeof(float) > 65536)) CG >>= 1;
+  if (aligned && P % 4 == 0 && C % CG == 0 && (size_t)CG * P * sizeof(float) <= 65536) {
+    // planes per block: enough blocks to fill the chip at least twice
+    const int per_dg = B * (C / CG);
+    int DG = 1;
+    while (DG < D && per_dg * ((D + 2 * DG - 1) / (2 * DG)) >= 512) DG *= 2;
+    const int nblk = per_dg * ((D + DG - 1) / DG);
+    const size_t lds = (size_t)CG * P * sizeof(float);
+    hipStream_t s = (hipStream_t)stream;
+    switch (CG) {
+      case 8: hipLaunchKernelGGL(plane_sweep_lds_kernel<8>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); break;
+      case 4: hipLaunchKernelGGL(plane_sweep_lds_kernel<4>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); break;
+      case 2: hipLaunchKernelGGL(plane_sweep_lds_kernel<2>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); break;
+      default: hipLaunchKernelGGL(plane_sweep_lds_kernel<1>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost);
+    }
+    return launch_status("plane_sweep_lds_kernel launch failed");
+  }
   dim3 grid((P + kWave - 1) / kWave, (C + 4 * kSweepCPT - 1) / (4 * kSweepCPT), B * D);
   hipLaunchKernelGGL(plane_sweep_wide_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, disp, D,
                      cost);
