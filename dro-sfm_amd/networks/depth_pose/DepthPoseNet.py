@@ -27,7 +27,6 @@ Execution plan (what changes versus the reference, never the math):
 """
 import contextlib
 import logging
-import os
 
 import torch
 import torch.nn as nn
@@ -56,27 +55,6 @@ def parse_version(version):
 _SIDE_STREAMS = {}
 
 
-_UPSAMPLE_MANY = [os.environ.get("DRO_UPSAMPLE_MANY", "1") != "0"]
-_DEPTH_ENCODER_POSE_STREAM = [os.environ.get("DRO_CNET_DEPTH_POSE_STREAM", "1") != "0"]
-
-
-def set_depth_encoder_pose_stream(enabled):
-    """cnet_depth on the pose block's stream, ahead of cnet_pose (default), or
-    on the main stream.  On the pose stream its forward runs beside fnet (the
-    depth block waits for it through an event) and its backward beside fnet's
-    backward: the in-graph timeline put it after fnet's backward on the main
-    stream (1.3 ms on the critical path, profiles/r3_step_timeline.txt).
-    Measured A/B on one box: 14.92-15.15 vs 16.38-17.16 ms/step
-    (profiles/r3_step_timeline_cnet_depth_pose_stream.txt)."""
-    _DEPTH_ENCODER_POSE_STREAM[0] = bool(enabled)
-
-
-def set_upsample_many(enabled):
-    """All kept predictions upsampled in one launch each way after the
-    recurrence (default), or one upsample launch per prediction (A/B)."""
-    _UPSAMPLE_MANY[0] = bool(enabled)
-
-
 _CONCURRENT_BLOCKS = [True]
 
 
@@ -88,16 +66,6 @@ def set_concurrent_blocks(enabled):
     of small launches overlap: 16.9 vs 19.0 ms/step (round 3, one box, two
     interleaved runs each); eager, 32.7 vs 32.0."""
     _CONCURRENT_BLOCKS[0] = bool(enabled)
-
-
-_POSE_ENCODER_SIDE = [True]
-
-
-def set_pose_encoder_stream(enabled):
-    """With the concurrent update blocks: run the pose context encoder
-    (cnet_pose, read only by the pose block) on the pose block's stream too
-    (default True), beside fnet and cnet_depth; its backward follows."""
-    _POSE_ENCODER_SIDE[0] = bool(enabled)
 
 
 def _pose_stream(device):
@@ -198,10 +166,8 @@ class DepthPoseNet(nn.Module):
         d_stream = p_stream = None
         d_event = None
         if self.iters > 0 and cuda:
-            if pside is not None and _POSE_ENCODER_SIDE[0]:
-                p_stream = pside
-                if _DEPTH_ENCODER_POSE_STREAM[0]:
-                    d_stream = pside
+            if pside is not None:
+                p_stream = d_stream = pside
             main = torch.cuda.current_stream(target_image.device)
             for st in {d_stream, p_stream} - {None}:
                 st.wait_stream(main)
@@ -322,7 +288,7 @@ class DepthPoseNet(nn.Module):
 
         if not self.training:
             return self.upsample_scaled(*up_pairs[-1], self.feat_ratio), pose_preds[-1].permute(1, 0, 2)  # [B,N,6]
-        if cuda and _UPSAMPLE_MANY[0]:
+        if cuda:
             inv_preds = self.upsample_many(up_pairs, self.feat_ratio)
             stamp("fwd:upsample")
         else:

@@ -504,17 +504,25 @@ GRAD_TENSOR_TOL = 1e-3     # per tensor: max|hip - fp64| / max|fp64|
 GRAD_L2_TOL = 1e-4         # the whole gradient: relative L2
 
 
-def _grad_check(model, g64, tensor_tol=GRAD_TENSOR_TOL, l2_tol=GRAD_L2_TOL):
-    """Every parameter gradient within tensor_tol (max-rel over its elements) of
-    the fp64 oracle on the kernels' branch, and the whole gradient within
-    l2_tol in relative L2.  Returns (offenders, l2)."""
-    named = [(k, v.grad) for k, v in model.depth_net.named_parameters() if k in g64 and v.grad is not None]
+def _grad_check_vs(grads, g64):
+    """(per-tensor max-rel errors, global relative L2) of a {name: grad} dict."""
+    named = [(k, g) for k, g in grads.items() if k in g64 and g is not None]
     den = sum(float(g64[k].double().pow(2).sum()) for k, _ in named)
     num = sum(float((g.double().cpu() - g64[k].double()).pow(2).sum()) for k, g in named)
-    l2 = (num / den) ** 0.5
-    errs = {k: rel(g, g64[k]) for k, g in named}
-    bad = [(k, e) for k, e in errs.items() if e > tensor_tol]
-    if l2 > l2_tol:
+    return {k: rel(g, g64[k]) for k, g in named}, (num / den) ** 0.5
+
+
+def _grad_check(model, g64, tensor_tol=GRAD_TENSOR_TOL, l2_tol=GRAD_L2_TOL, ref32=None):
+    """Every parameter gradient within tensor_tol (max-rel over its elements) of
+    the fp64 oracle on the kernels' branch, and the whole gradient within
+    l2_tol in relative L2.  ref32 (the fp32 oracle on the same branch, only
+    for inputs where the reference algorithm itself is ill-conditioned in
+    fp32): the bounds become max(bound, 4x the fp32 oracle's own distance).
+    Returns (offenders, l2)."""
+    errs, l2 = _grad_check_vs({k: v.grad for k, v in model.depth_net.named_parameters()}, g64)
+    e32, l2_32 = _grad_check_vs(ref32, g64) if ref32 is not None else ({}, 0.0)
+    bad = [(k, e) for k, e in errs.items() if e > max(tensor_tol, 4 * e32.get(k, 0.0))]
+    if l2 > max(l2_tol, 4 * l2_32):
         bad.append(("<global L2>", l2))
     _log_margins("grad_check", l2=l2, worst=sorted(errs.items(), key=lambda t: -t[1])[:5])
     return sorted(bad, key=lambda t: -t[1]), l2
@@ -675,8 +683,15 @@ def test_train_step_scannet_size_vs_oracle(hip, kind):
     forced = model._photometric_loss.last_selection.cpu().unsqueeze(2) if kind == "selfsup_view5" else None
     okind = "selfsup" if kind == "selfsup_view5" else "sup"
     loss64, g64 = _oracle_grads(spec, "it12-h-out", mind, maxd, batch, okind, torch.float64, forced, False, cells)
-    assert rel(out["loss"], loss64) < TOL
-    bad, l2 = _grad_check(model, g64)
+    # the untrained it12-h recurrence at 240x320 amplifies fp32 rounding itself:
+    # the reference algorithm evaluated in fp32 on the same branch (cells and
+    # selection) is the measure of what any fp32 evaluation can reach; the
+    # bounds are the fixed ones or 4x that distance, whichever is larger
+    loss32, g32 = _oracle_grads(spec, "it12-h-out", mind, maxd, batch, okind, torch.float32, forced, False, cells)
+    c_loss = rel(loss32, loss64)
+    _log_margins("fp32_oracle_conditioning", loss=c_loss, l2=_grad_check_vs(g32, g64)[1])
+    assert rel(out["loss"], loss64) < max(TOL, 4 * c_loss), (rel(out["loss"], loss64), c_loss)
+    bad, l2 = _grad_check(model, g64, tensor_tol=GRAD_TENSOR_TOL, l2_tol=GRAD_L2_TOL, ref32=g32)
     assert not bad, (bad[:5], l2)
 
 
