@@ -989,15 +989,21 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // 0..7
   const int noc = a.otiles * ((Cin + BC - 1) / BC);
-  const int tg = TG == 1 ? 0 : (int)blockIdx.x / noc;    // kernel row of this block (TG == 3)
-  const int t = (int)blockIdx.x - tg * noc;
+  // XCD-aware block order: the blocks of consecutive splits (adjacent pixel
+  // runs: their halo rows share cache lines) and the channel tiles of one split
+  // (they stage the same G / X tiles) land on the same XCD, i.e. the same L2
+  const int nbx = (int)gridDim.x;
+  const int lin = xcd_remap((int)(blockIdx.x + blockIdx.y * gridDim.x), (int)(gridDim.x * gridDim.y));
+  const int bx = lin % nbx, by = lin / nbx;
+  const int tg = TG == 1 ? 0 : bx / noc;    // kernel row of this block (TG == 3)
+  const int t = bx - tg * noc;
   const int ot = t % a.otiles, ct = t / a.otiles;
   const int o0 = ot * 64, c0 = ct * BC;
   const size_t HW = (size_t)H * W;
   const unsigned HWu = (unsigned)HW;
   int ntiles = a.g.B * a.tiles_img;
   if constexpr (MULTI) ntiles = P.use_tiles * P.nuse;
-  const int tbeg = blockIdx.y * a.chunks_per_split;
+  const int tbeg = by * a.chunks_per_split;
   const int tend = min(ntiles, tbeg + a.chunks_per_split);
   const bool do_bias = a.gbias && ct == 0 && tg == 0;
   const float galpha = a.galpha;
@@ -1102,19 +1108,33 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
     const float* xb = Xs + (wc * 32 + (lane & 31)) * HPAD + hi + (TG == 3 ? tg * HWd : 0);
     constexpr int KS = TAPSPLIT ? 32 : 16;        // k-steps (pixel pairs) per wave
     const int pbase = TAPSPLIT ? 0 : wg * 16;
+    // The tap count of a wave is a compile-time constant in each copy of the
+    // loop (3x3: wave group 0 takes taps 0-4, group 1 taps 5-8): a runtime
+    // `k < ntap` test put a branch into every k-step, and the compiler then
+    // waited for each LDS operand right before its MFMA (round 3 ISA:
+    // ds_read / s_waitcnt / v_mfma, serialised).  Without the branches the
+    // scheduler batches the reads (ds_read2 pairs of adjacent taps) ahead.
+    auto kloop = [&](auto nt_c, int tbase) __attribute__((always_inline)) {
+      constexpr int NT = decltype(nt_c)::value;
+      int toff[NT];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int pp = 2 * (pbase + s);              // even pixel of this k-step
-      const float av = ga[pp * GPAD];
-      const int poff = (pp / TW) * HWd + (pp % TW);
-#pragma unroll
-      for (int k = 0; k < TPW; ++k) {
-        if (TAPSPLIT ? k < ntap : true) {
-          const int tap = (TAPSPLIT ? tap0 : 0) + k;
-          const int ty = tap / KW, tx = tap - ty * KW;
-          acc[k] = mfma32(av, xb[poff + ty * HWd + tx], acc[k]);
-        }
+      for (int k = 0; k < NT; ++k) {
+        const int tap = tbase + k;
+        toff[k] = (tap / KW) * HWd + (tap % KW);
       }
+#pragma unroll 8
+      for (int s = 0; s < KS; ++s) {
+        const int pp = 2 * (pbase + s), poff = (pp / TW) * HWd + (pp % TW);
+        const float av = ga[pp * GPAD];
+#pragma unroll
+        for (int k = 0; k < NT; ++k) acc[k] = mfma32(av, xb[poff + toff[k]], acc[k]);
+      }
+    };
+    if constexpr (TAPSPLIT) {
+      if (wg == 0) kloop(std::integral_constant<int, 5>{}, 0);
+      else kloop(std::integral_constant<int, 4>{}, 5);
+    } else {
+      kloop(std::integral_constant<int, TPW>{}, 0);
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -1122,7 +1142,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
   // partials [split][tap][o][c]: lanes run along c, so each store is a
   // 128-B row segment (the [o][c][tap] order of wgrad_halo_kernel scattered
   // them 36 B apart -- 7x write amplification measured at this split count)
-  float* wpart = a.part + (size_t)blockIdx.y * Cout * Cin * T;
+  float* wpart = a.part + (size_t)by * Cout * Cin * T;
   const int c = c0 + wc * 32 + (lane & 31);
   const size_t tstride = (size_t)Cout * Cin;
   if (TAPSPLIT) {
@@ -1162,7 +1182,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(typename WgParam<MULTI>::T 
     for (int j = 0; j < 8; ++j) {
       const float v = wave_sum(bsum[j]);
       const int o = o0 + wave * 8 + j;
-      if (lane == 0 && o < Cout) a.bpart[(size_t)blockIdx.y * Cout + o] = v;
+      if (lane == 0 && o < Cout) a.bpart[(size_t)by * Cout + o] = v;
     }
   }
 }
