@@ -510,7 +510,8 @@ def _photometric_backward(ctx, gloss, _gmetrics, _gstate):
     image, context, inv_depths, pose, K, ref_K, state, cells = ctx.saved_tensors
     g_inv, g_pose = torch.ops.dro.photometric_loss_backward(image, context, inv_depths, pose, K, ref_K, state, gloss,
                                                             *ctx.cfg, ctx.need[1], cells)
-    return (g_inv if ctx.need[0] else None, _opt(g_pose), None, None, None, None, None, None, None, None, None,
+    # one entry per forward input: image, context, inv_depths, pose, then ten non-differentiable ones
+    return (None, None, g_inv if ctx.need[0] else None, _opt(g_pose), None, None, None, None, None, None, None,
             None, None, None)
 
 

@@ -114,7 +114,8 @@ class Cells:
     puts a coordinate on either side of a cell edge take different branches of
     the (exact) piecewise-linear function.  `forced` maps a call key to an
     int64 [B,h,w] tensor of packed cells ((y0 + 32768) << 16 | (x0 + 32768);
-    -1 = take the natural cell) that the sampler then uses, so the oracle is
+    -1 = take the natural cell) that the sampler then uses wherever the
+    given cell is the coordinate's own or a neighbouring one, so the oracle is
     evaluated on the branch another implementation took (the HIP kernels
     record theirs: hip.record_bilinear_cells); with record=True the natural
     cells of every call are kept in `recorded`.  Keys: ("depth", it, s, j),
@@ -150,9 +151,16 @@ def grid_sample_cells(img, grid, cells=None, book=None, key=None):
         book.recorded[key] = pack_cells(x0, y0)
     if cells is not None:
         c = cells.to(torch.int64).reshape(x0.shape)
-        forced = c != -1
-        x0 = torch.where(forced, ((c & 0xFFFF) - 32768).to(x0.dtype), x0)
-        y0 = torch.where(forced, (((c >> 16) & 0xFFFF) - 32768).to(y0.dtype), y0)
+        fx = ((c & 0xFFFF) - 32768).to(x0.dtype)
+        fy = (((c >> 16) & 0xFFFF) - 32768).to(y0.dtype)
+        # a cell is taken only where it is this coordinate's own cell or a
+        # neighbour (|t - 1/2| <= 1: the other side of a nearby grid line);
+        # where another evaluation's trajectory has diverged further (an
+        # ill-conditioned recurrence), the natural cell stays
+        near = ((ix.detach() - fx - 0.5).abs() <= 1.0) & ((iy.detach() - fy - 0.5).abs() <= 1.0)
+        forced = (c != -1) & near
+        x0 = torch.where(forced, fx, x0)
+        y0 = torch.where(forced, fy, y0)
     tx, ty = ix - x0, iy - y0
     flat = img.reshape(B, C, Hi * Wi)
     out = 0.0

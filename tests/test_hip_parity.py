@@ -191,7 +191,8 @@ def test_view_synthesis_golden(hip):
 def test_view_synthesis_kitti_size_vs_oracle(hip):
     """Metric-config warp: B=2, 192x640, N=2 reference images in one launch,
     inverse-depth input (the photometric loss's encoding, inv2depth in-kernel),
-    euler poses.  Warped images 1e-4 against the fp64 oracle; gradients of
+    euler poses.  Warped images 1e-4 against the fp64 oracle (or twice the fp32
+    oracle's own distance, the coordinates' rounding); gradients of
     sum(warped * G) w.r.t. the inverse depth (summed over both views), the
     poses and the reference images 1e-4 against the fp64 oracle on the
     kernel's bilinear cells."""
@@ -212,7 +213,14 @@ def test_view_synthesis_kitti_size_vs_oracle(hip):
     outs = [O.view_synthesis(r64[j], O.inv2depth(i64), v64[j], K.double(), K.double(),
                              O.Cells(forced={j: cells[j]}), j) for j in range(N)]
     out64 = torch.stack(outs)
-    assert rel(warped.double(), out64) < TOL
+    # the warped values carry the fp32 rounding of the sampling coordinates
+    # (|x| up to 640 px) times the image slope: the bound is the larger of TOL
+    # and twice what the fp32 oracle on the same cells shows against fp64
+    with torch.no_grad():
+        out32 = torch.stack([O.view_synthesis(refs[j], O.inv2depth(inv), vec[j], K, K,
+                                              O.Cells(forced={j: cells[j]}), j) for j in range(N)])
+    bound = max(TOL, 2 * rel(out32.double(), out64.detach()))
+    assert rel(warped.double(), out64) < bound
     (out64 * G.double()).sum().backward()
     assert rel(ig.grad.double(), i64.grad) < TOL
     assert rel(vg.grad.double(), v64.grad) < TOL
