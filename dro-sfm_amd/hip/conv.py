@@ -192,10 +192,12 @@ def _flat_view(tensors):
     return t0.detach().as_strided(shape, torch.empty(shape, device="meta").stride(), off)
 
 
-def _direct_targets(wparts, bparts, mark=True):
+def _direct_targets(wparts, bparts, mark=True, in_setup=False):
     """(fused weight, fused bias, grad-weight view, grad-bias view) when the
-    direct path applies to these parameters, else None."""
-    if not _DIRECT[0] or not torch.is_grad_enabled():
+    direct path applies to these parameters, else None.  in_setup: called from
+    an op's setup_context, which runs with grad mode off (inside the op's
+    autograd.Function forward): the grad-mode test was the caller's."""
+    if not _DIRECT[0] or not (in_setup or torch.is_grad_enabled()):
         return None
     ps = list(wparts) + list(bparts or ())
     for p in ps:
@@ -441,7 +443,7 @@ def _conv2d_setup(ctx, inputs, output):
     ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in srcs]
     ctx.need_src = [x.requires_grad for x in srcs]
     ctx.meta = (act, alpha, bias is not None, weight.requires_grad, bias is not None and bias.requires_grad)
-    ctx.direct = _direct_targets(params[:nweight], params[nweight:], mark=False) if params else None
+    ctx.direct = _direct_targets(params[:nweight], params[nweight:], mark=False, in_setup=True) if params else None
     ctx.scope = None if params else current_scope()
     ctx.nparams = len(params)
 
@@ -565,7 +567,7 @@ def _conv2d_strided_setup(ctx, inputs, output):
     has_bias = bias is not None
     ctx.meta = (stride, pad, act, has_bias, x.requires_grad, weight.requires_grad,
                 has_bias and bias.requires_grad)
-    ctx.direct = _direct_targets((weight,), (bias,) if has_bias else (), mark=False)
+    ctx.direct = _direct_targets((weight,), (bias,) if has_bias else (), mark=False, in_setup=True)
 
 
 def _conv2d_strided_backward(ctx, gout):
