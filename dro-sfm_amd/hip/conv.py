@@ -677,6 +677,7 @@ def _sepgru_setup(ctx, inputs, output):
     ctx.wsplit = (zb, qb)
     ctx.save_for_backward(h.contiguous(), rh, wzr, wq.contiguous(), zr, q, *xs)
     ctx.mark_non_differentiable(zr, rh, q)
+    ctx.set_materialize_grads(False)     # no zero-filled gradients for the three saved outputs
     ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in xs]
     ctx.need = (h.requires_grad, [x.requires_grad for x in xs],
                 any(t.requires_grad for t in (wz, bz, wr, br)), any(t.requires_grad for t in (wq, bq)))
@@ -692,6 +693,8 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
     h, rh, wzr, wq, zr, q, *xs = ctx.saved_tensors
     B, hd, H, W = h.shape
     need_h, need_x, need_zr_w, need_q_w = ctx.need
+    if dhn is None:
+        return (None,) * 7 + ([None] * len(xs), None, None)
     dhn = dhn.contiguous()
     # stage 1: pre-activation grads of q and z, dh = dh' (1-z)
     dq, dh = torch.empty_like(h), torch.empty_like(h)

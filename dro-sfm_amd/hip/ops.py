@@ -504,9 +504,12 @@ def _photometric_setup(ctx, inputs, output):
     ctx.cfg = (pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min)
     ctx.need = (inv_depths.requires_grad, pose.requires_grad)
     ctx.mark_non_differentiable(metrics, state)
+    ctx.set_materialize_grads(False)     # no zero-filled gradients for the non-differentiable outputs
 
 
 def _photometric_backward(ctx, gloss, _gmetrics, _gstate):
+    if gloss is None:
+        return (None,) * 14
     image, context, inv_depths, pose, K, ref_K, state, cells = ctx.saved_tensors
     g_inv, g_pose = torch.ops.dro.photometric_loss_backward(image, context, inv_depths, pose, K, ref_K, state, gloss,
                                                             *ctx.cfg, ctx.need[1], cells)
@@ -600,9 +603,12 @@ def _supervised_setup(ctx, inputs, output):
     ctx.cfg = (pose_mode, min_depth, max_depth)
     ctx.need = (inv_depths.requires_grad, pose.requires_grad)
     ctx.mark_non_differentiable(output[1])
+    ctx.set_materialize_grads(False)     # no zero-filled gradients for the non-differentiable outputs
 
 
 def _supervised_backward(ctx, gloss, _gmetrics):
+    if gloss is None:
+        return (None,) * 9
     gt_inv, inv_depths, pose, gt_pose, K, ref_K = ctx.saved_tensors
     g_inv, g_pose = torch.ops.dro.supervised_loss_backward(gt_inv, inv_depths, pose, gt_pose, K, ref_K, gloss,
                                                            *ctx.cfg)
@@ -901,6 +907,7 @@ def _maxpool_setup(ctx, inputs, output):
     ctx.save_for_backward(output[1])
     ctx.hw = inputs[0].shape[2:]
     ctx.mark_non_differentiable(output[1])
+    ctx.set_materialize_grads(False)     # no zero-filled gradients for the non-differentiable outputs
 
 
 torch.library.register_autograd(
