@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dro_amd.h"
 
@@ -393,6 +394,12 @@ __device__ __forceinline__ void block_sum_d(const float (&v)[NV], double (&out)[
     }
   }
   __syncthreads();
+}
+
+// host: an integer tuning override from the environment (A/B runs), or dflt
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
 }
 
 }  // namespace dro

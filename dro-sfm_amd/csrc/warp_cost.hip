@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void plane_sweep_wide_kernel(WarpArgs a, const
 // is bit-identical to one warp_cost call per plane.
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-template <int CG>
+template <int CG, bool NT>
 __global__ __launch_bounds__(256) void plane_sweep_lds_kernel(WarpArgs a, const float* __restrict__ disp, int D,
                                                               int DG, float* __restrict__ cost) {
   extern __shared__ float4 lds4[];
@@ -443,7 +443,10 @@ __global__ __launch_bounds__(256) void plane_sweep_lds_kernel(WarpArgs a, const 
           o[k] = df * df;
         }
         const v4f ov = {o[0], o[1], o[2], o[3]};
-        __builtin_nontemporal_store(ov, out4 + (size_t)c * P4 + q);
+        if (NT)
+          __builtin_nontemporal_store(ov, out4 + (size_t)c * P4 + q);
+        else
+          out4[(size_t)c * P4 + q] = ov;
       }
     }
   }
@@ -663,22 +666,37 @@ extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref,
   // channel group's reference planes must fit 64 KB of LDS
   const bool aligned = ((reinterpret_cast<uintptr_t>(fmap) | reinterpret_cast<uintptr_t>(fmap_ref) |
                          reinterpret_cast<uintptr_t>(cost)) & 15) == 0;
-  int CG = 8;
+  // tuning overrides (A/B runs, tools/bench_sweep.py): DRO_SWEEP_CG = largest
+  // channel group (default 8), DRO_SWEEP_BLOCKS = minimum grid (default 512),
+  // DRO_SWEEP_WIDE = 1 forces plane_sweep_wide_kernel, DRO_SWEEP_NT = 0 plain stores
+  static const int cg_max = env_int("DRO_SWEEP_CG", 8);
+  static const int min_blocks = env_int("DRO_SWEEP_BLOCKS", 512);
+  static const bool wide = env_int("DRO_SWEEP_WIDE", 0) != 0;
+  static const bool nt = env_int("DRO_SWEEP_NT", 1) != 0;      // non-temporal volume stores
+  int CG = cg_max;
   while (CG > 1 && (C % CG != 0 || (size_t)CG * P * sizeof(float) > 65536)) CG >>= 1;
-  if (aligned && P % 4 == 0 && C % CG == 0 && (size_t)CG * P * sizeof(float) <= 65536) {
+  if (!wide && aligned && P % 4 == 0 && C % CG == 0 && (size_t)CG * P * sizeof(float) <= 65536) {
     // planes per block: enough blocks to fill the chip at least twice
     const int per_dg = B * (C / CG);
     int DG = 1;
-    while (DG < D && per_dg * ((D + 2 * DG - 1) / (2 * DG)) >= 512) DG *= 2;
+    while (DG < D && per_dg * ((D + 2 * DG - 1) / (2 * DG)) >= min_blocks) DG *= 2;
     const int nblk = per_dg * ((D + DG - 1) / DG);
     const size_t lds = (size_t)CG * P * sizeof(float);
     hipStream_t s = (hipStream_t)stream;
+#define DRO_SWEEP_LAUNCH(CG_)                                                                                  \
+  do {                                                                                                         \
+    if (nt)                                                                                                    \
+      hipLaunchKernelGGL((plane_sweep_lds_kernel<CG_, true>), dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((plane_sweep_lds_kernel<CG_, false>), dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); \
+  } while (0)
     switch (CG) {
-      case 8: hipLaunchKernelGGL(plane_sweep_lds_kernel<8>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); break;
-      case 4: hipLaunchKernelGGL(plane_sweep_lds_kernel<4>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); break;
-      case 2: hipLaunchKernelGGL(plane_sweep_lds_kernel<2>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost); break;
-      default: hipLaunchKernelGGL(plane_sweep_lds_kernel<1>, dim3(nblk), dim3(256), lds, s, a, disp, D, DG, cost);
+      case 8: DRO_SWEEP_LAUNCH(8); break;
+      case 4: DRO_SWEEP_LAUNCH(4); break;
+      case 2: DRO_SWEEP_LAUNCH(2); break;
+      default: DRO_SWEEP_LAUNCH(1);
     }
+#undef DRO_SWEEP_LAUNCH
     return launch_status("plane_sweep_lds_kernel launch failed");
   }
   dim3 grid((P + kWave - 1) / kWave, (C + 4 * kSweepCPT - 1) / (4 * kSweepCPT), B * D);
