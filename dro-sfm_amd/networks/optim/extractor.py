@@ -22,6 +22,8 @@ in place, out_conv) run on the HIP conv engine's halo-tiled kernels
 have a native path too (the flattened implicit GEMM with the stride,
 set_native_strided_convs) but stay on MIOpen by default: measured faster.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -32,7 +34,9 @@ from ... import hip
 _FUSED_BN = [True]
 _NATIVE_POOL = [True]
 _NATIVE_CONV = [True]
-_NATIVE_STRIDED = [False]
+# DRO_NATIVE_STRIDED=1: the stride-2 convolutions on the HIP engine from the
+# start (parity runs of the whole suite on that path)
+_NATIVE_STRIDED = [os.environ.get("DRO_NATIVE_STRIDED", "0") == "1"]
 
 
 def set_native_strided_convs(enabled):

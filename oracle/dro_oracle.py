@@ -136,6 +136,27 @@ def pack_cells(x0, y0):
     return ((y0 + 32768) << 16) | (x0 + 32768)
 
 
+def cells_from_calls(calls):
+    """The product's bilinear-cell record (hip.record_bilinear_cells().calls:
+    (tag, int32 map) per op call) -> Cells(forced=...) keys:
+    ("depth", it, s, j) / ("pose", it, s, j) -> [B,h,w] for inner step s and
+    reference view j, ("photo", j, i) -> [B,H,W] (int64, CPU).  Each cost tag
+    is called once per inner step, in order; one call covers every view."""
+    out, steps = {}, {}
+    for tag, cells in calls:
+        c = cells.cpu().to(torch.int64)
+        if tag == "photo":
+            for j in range(c.shape[0]):
+                for i in range(c.shape[1]):
+                    out[("photo", j, i)] = c[j, i]
+        elif isinstance(tag, tuple):
+            s_ = steps.get(tag, 0)
+            steps[tag] = s_ + 1
+            for j in range(c.shape[0]):
+                out[(tag[0], tag[1], s_, j)] = c[j]
+    return out
+
+
 def grid_sample_cells(img, grid, cells=None, book=None, key=None):
     """F.grid_sample(img, grid, 'bilinear', 'zeros', align_corners=True), with
     the bilinear cell of each output taken from `cells` where given (see

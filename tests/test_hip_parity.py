@@ -459,23 +459,9 @@ def test_depth_pose_net_golden(hip, tag, version):
 
 
 def cells_from_record(rec):
-    """hip.record_bilinear_cells() record -> the oracle's Cells keys:
-    ("depth", it, s, j) / ("pose", it, s, j) -> [B,h,w], ("photo", j, i) ->
-    [B,H,W] (int64 on the CPU).  The product calls each tag once per inner
-    step s, in order; one call covers every reference view j."""
-    out, steps = {}, {}
-    for tag, cells in rec.calls:
-        c = cells.cpu().to(torch.int64)
-        if tag == "photo":
-            for j in range(c.shape[0]):
-                for i in range(c.shape[1]):
-                    out[("photo", j, i)] = c[j, i]
-        elif isinstance(tag, tuple):
-            s_ = steps.get(tag, 0)
-            steps[tag] = s_ + 1
-            for j in range(c.shape[0]):
-                out[(tag[0], tag[1], s_, j)] = c[j]
-    return out
+    """hip.record_bilinear_cells() record -> the oracle's Cells keys
+    (oracle.cells_from_calls)."""
+    return O.cells_from_calls(rec.calls)
 
 
 def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=False, cells=None,

@@ -6,6 +6,7 @@ reads the golden fixtures and the oracle).
 
 usage: python tools/grad_floor.py it8 it8-seq4-inter-out selfsup [flip]
        python tools/grad_floor.py kitti          (metric config 192x640, B=2, N=2)
+       python tools/grad_floor.py view5          (ScanNet view5 fixture, it12-h, N=4)
 """
 import os
 import sys
@@ -27,6 +28,13 @@ def golden_case(tag, version, kind):
              "rgb_context_original": list(d["refs"]), "intrinsics": d["K"].clone(),
              "depth": d["gt_depth"], "pose_context": [d["gt_poses"][:, j] for j in range(N)]}
     return tag, version, kind, T.fval(dn["min_depth"]), T.fval(dn["max_depth"]), batch
+
+
+def view5_case():
+    d = T.fx("train_step_it12h_selfsup_n4")
+    batch = {"rgb": d["image"], "rgb_context": list(d["refs"]), "rgb_original": d["image"],
+             "rgb_context_original": list(d["refs"]), "intrinsics": d["K"].clone()}
+    return "it12h", "it12-h-out", "selfsup", T.fval(d["min_depth"]), T.fval(d["max_depth"]), batch
 
 
 def kitti_case():
@@ -52,7 +60,8 @@ def run(spec, version, kind, mind, maxd, batch, dt, book, flip):
 
 def main():
     a = sys.argv[1:]
-    tag, version, kind, mind, maxd, batch = kitti_case() if a[0] == "kitti" else golden_case(*a[:3])
+    tag, version, kind, mind, maxd, batch = (kitti_case() if a[0] == "kitti" else view5_case() if a[0] == "view5"
+                                             else golden_case(*a[:3]))
     flip = "flip" in a
     spec = T.load_spec(os.path.join(T.G, f"depthposenet_{tag}_keys.json"))
     batch = {k: (v.cpu().clone() if torch.is_tensor(v) else [t.cpu() for t in v]) for k, v in batch.items()}
