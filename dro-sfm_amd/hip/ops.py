@@ -915,13 +915,20 @@ torch.library.register_autograd(
     setup_context=_maxpool_setup)
 
 
-def maxpool3x3s2(x):
+def maxpool3x3s2(x, tag=None):
     """F.max_pool2d(x, 3, 2, 1) for float32 NCHW on the GPU (ResNet stem,
     reference networks/optim/extractor.py:60-66); bit-identical forward and
-    backward, one argmax byte per output instead of int64 indices."""
+    backward, one argmax byte per output instead of int64 indices.  Inside
+    record_bilinear_cells() the argmax map (dy * 3 + dx per output, the window
+    the backward routes to) is recorded as ("maxpool", tag): near-ties of a
+    window are a branch of the step like bilinear cells (tests only)."""
     if x.dtype != torch.float32 or x.dim() != 4:
         raise RuntimeError("maxpool3x3s2: expects a float32 NCHW tensor")
-    return torch.ops.dro.maxpool3x3s2(x)[0]
+    y, arg = torch.ops.dro.maxpool3x3s2(x)
+    rec = _CELLS[0]
+    if rec is not None and torch.is_grad_enabled() and x.requires_grad:
+        rec.calls.append((("maxpool", tag), arg))
+    return y
 
 
 # ------------------------------------------------------------------ PoseHead mean

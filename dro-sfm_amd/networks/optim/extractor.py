@@ -169,7 +169,8 @@ class ResNetEncoder(nn.Module):
             chunks = len(x)
             x = torch.cat(list(x), 0)
         x = self.bn1.act(conv3x3(self.conv1, x))
-        x = hip.maxpool3x3s2(x) if (x.is_cuda and _NATIVE_POOL[0]) else F.max_pool2d(x, 3, 2, 1)
+        x = (hip.maxpool3x3s2(x, getattr(self, "_dro_tag", None)) if (x.is_cuda and _NATIVE_POOL[0])
+             else F.max_pool2d(x, 3, 2, 1))
         s4 = self.layer1(x)
         s8 = self.layer2(s4)
         x = self.layer3(s8)

@@ -149,6 +149,8 @@ def cells_from_calls(calls):
             for j in range(c.shape[0]):
                 for i in range(c.shape[1]):
                     out[("photo", j, i)] = c[j, i]
+        elif isinstance(tag, tuple) and tag[0] == "maxpool":
+            out[tag] = c                                    # [B, C, Ho, Wo] window index dy * 3 + dx
         elif isinstance(tag, tuple):
             s_ = steps.get(tag, 0)
             steps[tag] = s_ + 1
@@ -357,11 +359,35 @@ def _bn(p, name, x, training):
                         p[name + ".bias"], training=training, momentum=0.1, eps=1e-5)
 
 
-def resnet_encoder(p, pre, x, training, stride=8):
+def max_pool_3x3s2(x, forced=None):
+    """F.max_pool2d(x, 3, 2, 1); with `forced` ([B,C,Ho,Wo] int window index
+    dy * 3 + dx, another evaluation's argmax) the window element taken is the
+    forced one wherever it ties the window's maximum within 1e-5 of its
+    magnitude (a near-tie that rounding decides), else the natural maximum --
+    the value is continuous either way, the gradient goes where the forced
+    evaluation sent it."""
+    y = F.max_pool2d(x, 3, 2, 1)
+    if forced is None:
+        return y
+    B, C, H, W = x.shape
+    Ho, Wo = y.shape[-2:]
+    xp = F.pad(x, (1, 1, 1, 1), value=float("-inf"))
+    win = F.unfold(xp.reshape(B * C, 1, H + 2, W + 2), 3, stride=2)           # [B*C, 9, Ho*Wo]
+    win = win.reshape(B, C, 9, Ho, Wo)
+    idx = forced.to(torch.int64).reshape(B, C, 1, Ho, Wo).clamp(0, 8)
+    picked = torch.gather(win, 2, idx).squeeze(2)
+    tie = (y.detach() - picked.detach()).abs() <= 1e-5 * y.detach().abs().clamp_min(1e-30)
+    return torch.where(tie, picked, y)
+
+
+def resnet_encoder(p, pre, x, training, stride=8, cells=None):
     """ResNetEncoder.forward (networks/optim/extractor.py:67-107) on torchvision's
-    ResNet-18 layout (layer1..layer3, BasicBlocks) with the stride-8 fusion head."""
+    ResNet-18 layout (layer1..layer3, BasicBlocks) with the stride-8 fusion head.
+    cells: a Cells book whose ("maxpool", <encoder>) entry pins the stem
+    pooling's argmax (test hook)."""
     x = F.relu(_bn(p, pre + "bn1", _conv(p, pre + "conv1", x, 2, 3), training))
-    x = F.max_pool2d(x, 3, 2, 1)
+    forced = cells.forced.get(("maxpool", pre.rstrip("."))) if cells is not None else None
+    x = max_pool_3x3s2(x, forced)
     feats = {}
     for li, s in ((1, 1), (2, 2), (3, 2)):
         for bi in range(2):
@@ -473,17 +499,17 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
     hd, cd, S = cfg["hdim"], 32, cfg["seq"]
     scale = (lambda x: disp_to_depth(x, min_depth, max_depth)) if cfg["out_norm"] else (lambda x: x)
     B, N = image.shape[0], len(refs)
-    fm = resnet_encoder(p, "fnet.", torch.cat([image] + refs, 0), training)
+    fm = resnet_encoder(p, "fnet.", torch.cat([image] + refs, 0), training, cells=cells)
     fmap1, frefs = fm[:B], [fm[B * (j + 1):B * (j + 2)] for j in range(N)]
     poses = [pose_head(p, "pose_head.", torch.cat([fmap1, f], 1)) for f in frefs]
     inv = depth_head(p, "depth_head.", fmap1, torch.sigmoid)
     up = convex_upsample(inv, 0.25 * _conv(p, "upmask_net.mask.2",
                                             F.relu(_conv(p, "upmask_net.mask.0", fmap1, 1, 1))), 8)
     inv_preds, pose_preds = [scale(up)], [[q.clone() for q in poses]]
-    ctx_d = resnet_encoder(p, "cnet_depth.", image, training)
+    ctx_d = resnet_encoder(p, "cnet_depth.", image, training, cells=cells)
     h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
     ctx_p = resnet_encoder(p, "cnet_pose.", torch.cat([torch.cat([image, r], 1) for r in refs], 0),
-                           training)
+                           training, cells=cells)
     h_p = [torch.tanh(ctx_p[B * j:B * (j + 1), :hd]) for j in range(N)]
     x_p = [torch.relu(ctx_p[B * j:B * (j + 1), hd:hd + cd]) for j in range(N)]
     for it in range(cfg["outer"]):

@@ -372,3 +372,41 @@ def test_grid_sample_cells_matches_aten():
     r = one[0, 0, 4] * 0.75 + one[0, 0, 5] * 0.25      # the row interpolated at y = 4.25
     assert torch.allclose(d_nat, (r[8] - r[7]) * 19 / 2, atol=1e-10)
     assert torch.allclose(d_left, (r[7] - r[6]) * 19 / 2, atol=1e-10)
+
+
+def test_max_pool_forced_argmax():
+    """oracle.max_pool_3x3s2: with the natural argmax forced it equals
+    F.max_pool2d (values and gradients); on an exact tie the gradient goes to
+    the forced window element; a forced index that is not a near-tie is
+    ignored."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 3, 9, 11, generator=g, dtype=torch.float64)
+    y, ind = F.max_pool2d(x, 3, 2, 1, return_indices=True)
+    Ho, Wo = y.shape[-2:]
+    oy = torch.arange(Ho).view(1, 1, Ho, 1)
+    ox = torch.arange(Wo).view(1, 1, 1, Wo)
+    iy, ix = ind // 11, ind % 11
+    nat = (iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1))
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    G = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (O.max_pool_3x3s2(xa, nat) * G).sum().backward()
+    (F.max_pool2d(xb, 3, 2, 1) * G).sum().backward()
+    assert torch.allclose(xa.grad, xb.grad, rtol=0, atol=1e-14)
+    # exact tie in window (0, 1): input (0, 1) and (0, 2); natural picks the first
+    t = torch.zeros(1, 1, 3, 5, dtype=torch.float64)
+    t[0, 0, 0, 1] = t[0, 0, 0, 2] = 1.0
+    forced = torch.full((1, 1, 2, 3), -1, dtype=torch.int64)
+    nat_t = F.max_pool2d(t, 3, 2, 1, return_indices=True)[1]
+    forced[0, 0, 0, 1] = 1 * 3 + 1            # window rows -1..1, cols 1..3: input (0, 2) is dy 1, dx 1
+    tt = t.clone().requires_grad_(True)
+    O.max_pool_3x3s2(tt, forced.clamp_min(0)).sum().backward()
+    assert nat_t[0, 0, 0, 1] == 1                      # natural: the first maximum, x = 1
+    assert tt.grad[0, 0, 0, 2] >= 1.0                  # forced: routed to x = 2 for that window
+    far = torch.zeros_like(forced)                     # index 0 = the (padded / smaller) corner: not a tie
+    tf = t.clone().requires_grad_(True)
+    O.max_pool_3x3s2(tf, far).sum().backward()
+    tn = t.clone().requires_grad_(True)
+    F.max_pool2d(tn, 3, 2, 1).sum().backward()
+    assert torch.equal(tf.grad, tn.grad)

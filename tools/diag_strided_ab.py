@@ -73,7 +73,55 @@ def diff(a, b):
     return (num / den) ** 0.5, sorted(e.items(), key=lambda kv: -kv[1])[:5]
 
 
+class _Mixed(torch.autograd.Function):
+    """Stride-2 conv with the forward / backward each either native (HIP) or
+    exact (fp64 torch, rounded to fp32): DIAG_FWD / DIAG_BWD = native|exact."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        import torch.nn.functional as F
+        ctx.save_for_backward(x, w)
+        ctx.sp = (stride, pad)
+        exact_k = os.environ.get("DIAG_FWD_EXACT_K")     # e.g. "7" or "1,3": exact forward for these kernels only
+        if os.environ.get("DIAG_FWD", "native") == "exact" and (
+                exact_k is None or str(w.shape[-1]) in exact_k.split(",")):
+            y = F.conv2d(x.double(), w.double(), stride=stride, padding=pad)
+            if os.environ.get("DIAG_NOISE"):      # relative noise of this size on the exact output
+                g = torch.Generator(device=y.device).manual_seed(int(os.environ.get("DIAG_SEED", "0")))
+                y = y * (1 + float(os.environ["DIAG_NOISE"]) * torch.randn(y.shape, generator=g, device=y.device,
+                                                                          dtype=y.dtype))
+            return y.float()
+        return torch.ops.dro.conv2d_strided(x, w, None, stride, pad, 0)
+
+    @staticmethod
+    def backward(ctx, gout):
+        import torch.nn.functional as F
+        x, w = ctx.saved_tensors
+        s, p = ctx.sp
+        if os.environ.get("DIAG_BWD", "native") == "exact":
+            xd, wd = x.double().requires_grad_(), w.double().requires_grad_()
+            with torch.enable_grad():
+                yd = F.conv2d(xd, wd, stride=s, padding=p)
+                gx, gw = torch.autograd.grad(yd, (xd, wd), gout.double())
+            return gx.float(), gw.float(), None, None
+        gx, gw = torch.empty_like(x), torch.empty_like(w)
+        torch.ops.dro.conv2d_strided_backward(x, w, gout.contiguous(), s, p, gx, gw, None, 0)
+        return gx, gw, None, None
+
+
+def _mixed(x, weight, bias=None, stride=2, padding=1, act=None):
+    assert bias is None and act is None
+    return _Mixed.apply(x, weight, int(stride), int(padding))
+
+
 def oracle_check():
+    if "DIAG_FWD" in os.environ or "DIAG_BWD" in os.environ:
+        import dro_sfm_amd.hip as hip_
+        import dro_sfm_amd.networks.optim.extractor as ex_
+        hip_.conv2d_strided = _mixed
+        ex_.hip.conv2d_strided = _mixed
+        print("mixed strided conv: fwd", os.environ.get("DIAG_FWD", "native"), "bwd",
+              os.environ.get("DIAG_BWD", "native"))
     """view5: HIP (native, then MIOpen) vs the fp64 oracle on that run's own
     cells and selection, on the other run's cells, and on natural cells."""
     from oracle import dro_oracle as O
@@ -85,6 +133,10 @@ def oracle_check():
     cpu_batch = {k: (v.cpu().clone() if torch.is_tensor(v) else [t.cpu() for t in v]) for k, v in batch.items()}
     runs = {}
     import dro_sfm_amd.networks.optim.extractor as ex
+    from dro_sfm_amd.networks.depth_pose import DepthPoseNet as dpn
+    serial = os.environ.get("DIAG_SERIAL") == "1"
+    dpn.set_concurrent_blocks(not serial)
+    print("concurrent blocks:", not serial)
     for native in (True, False):
         ex.set_native_strided_convs(native)
         model = T._selfsup_model(mind, maxd, "it12h", "it12-h-out")
