@@ -14,6 +14,8 @@
 //   bn_bwd_reduce_kernel  partial sums of g and g * xhat, g = dy * [y > 0]
 //   bn_bwd_apply_kernel   dx = gamma * invstd * (g - mean(g) - xhat * mean(g xhat)),
 //                       dskip = g; first block of a channel writes dgamma, dbeta
+// Sites whose channels hold <= 16 K elements take ONE launch each way
+// (bn_fused_fwd_kernel / bn_fused_bwd_kernel, a block per channel, below).
 // Statistics follow torch.nn.functional.batch_norm (biased variance for the
 // normalisation, unbiased for running_var, running = (1 - m) * running + m * batch).
 // Layout: NCHW fp32, planes of HW contiguous floats.
@@ -243,6 +245,128 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(BnBwdArgs a, B
   }
 }
 
+// ---------------------------------------------------------------- one launch per direction
+// Small sites (a channel's N * HW <= 16 K elements: the encoders' layer2 /
+// layer3 at KITTI size, 480-1920 pixels per plane): ONE block of 1024 threads
+// per channel keeps its elements in registers (thread t holds elements
+// t + 1024 k, k < EPT), reduces them in a fixed order (per thread in k order,
+// then the block tree), and applies the transform from the registers -- one
+// launch forward and one backward instead of two each, no partials.
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedMaxEPT = 16;
+
+__device__ __forceinline__ double block_sum_fused(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < kFusedThreads / 64; ++i) s += red[i];
+  return s;
+}
+
+// element e of channel c (e < N * HW) -> its offset in the NCHW tensor
+__device__ __forceinline__ long long chan_off(int e, int c, const BnGeom& g) {
+  const int n = e / g.HW, i = e - n * g.HW;
+  return ((long long)n * g.C + c) * g.HW + i;
+}
+
+template <int EPT>
+__global__ __launch_bounds__(kFusedThreads) void bn_fused_fwd_kernel(BnFwdArgs a, BnGeom g) {
+  __shared__ double red[kFusedThreads / 64];
+  const int c = blockIdx.x;
+  const int L = g.N * g.HW;
+  float xv[EPT];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + kFusedThreads * k;
+    xv[k] = e < L ? a.x[chan_off(e, c, g)] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const double v = xv[k];
+    s1 += v;
+    s2 += v * v;
+  }
+  s1 = block_sum_fused(s1, red);
+  s2 = block_sum_fused(s2, red);
+  const double mean = s1 / (double)L;
+  double var = s2 / (double)L - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  const float k0 = (a.gamma ? a.gamma[c] : 1.f) * invstd, o = a.beta ? a.beta[c] : 0.f, mu = (float)mean;
+  if (threadIdx.x == 0) {
+    a.save_mean[c] = mu;
+    a.save_invstd[c] = invstd;
+    if (a.running_mean) {
+      const double unb = L > 1 ? var * (double)L / (double)(L - 1) : var;
+      a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
+      a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * (float)unb;
+    }
+    if (c == 0 && a.num_batches) *a.num_batches += 1;
+  }
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + kFusedThreads * k;
+    if (e >= L) continue;
+    const long long q = chan_off(e, c, g);      // recomputed: keeping EPT 64-bit offsets costs registers
+    float r = fmaf(xv[k] - mu, k0, o) + (a.skip ? a.skip[q] : 0.f);
+    a.y[q] = a.relu ? fmaxf(r, 0.f) : r;
+  }
+}
+
+template <int EPT>
+__global__ __launch_bounds__(kFusedThreads) void bn_fused_bwd_kernel(BnBwdArgs a, BnGeom g) {
+  __shared__ double red[kFusedThreads / 64];
+  const int c = blockIdx.x;
+  const int L = g.N * g.HW;
+  const float mean = a.save_mean[c], invstd = a.save_invstd[c];
+  const float* ysrc = a.relu ? a.y : a.dy;
+  float gv[EPT], xh[EPT];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + kFusedThreads * k;
+    const long long q = e < L ? chan_off(e, c, g) : 0;
+    const float d = a.dy[q], v = a.x[q], yy = ysrc[q];
+    gv[k] = e < L ? grad_in(d, yy, a.relu) : 0.f;
+    xh[k] = (v - mean) * invstd;
+  }
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    s1 += gv[k];
+    s2 += (double)(gv[k] * xh[k]);
+  }
+  s1 = block_sum_fused(s1, red);
+  s2 = block_sum_fused(s2, red);
+  const float kk = (a.gamma ? a.gamma[c] : 1.f) * invstd;
+  const float mg = (float)(s1 / (double)L), mgx = (float)(s2 / (double)L);
+  if (threadIdx.x == 0) {
+    if (a.dgamma) a.dgamma[c] = (float)s2;
+    if (a.dbeta) a.dbeta[c] = (float)s1;
+  }
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + kFusedThreads * k;
+    if (e >= L) continue;
+    const long long q = chan_off(e, c, g);
+    a.dx[q] = kk * (gv[k] - mg - xh[k] * mgx);
+    if (a.dskip) a.dskip[q] = gv[k];
+  }
+}
+
+// EPT for the one-launch path, 0 = the two-launch path
+int fused_ept(int N, int HW) {
+  const long long L = (long long)N * HW;
+  for (int e = 1; e <= kFusedMaxEPT; e *= 2)
+    if (L <= (long long)kFusedThreads * e) return e;
+  return 0;
+}
+
 // reduction chunking: ~1-2 K blocks over the whole tensor, chunks of >= 1 K floats
 BnGeom bn_geom(int N, int C, int HW) {
   BnGeom g;
@@ -316,6 +440,18 @@ extern "C" int dro_batchnorm_relu_forward(const float* x, const float* gamma, co
   }
   hipStream_t s = (hipStream_t)stream;
   double2* part = static_cast<double2*>(workspace);
+  if (const int ept = fused_ept(N, HW)) {
+    BnFwdArgs a{x, gamma, beta, skip, relu, eps, momentum, running_mean, running_var,
+                num_batches_tracked, y, save_mean, save_invstd, nullptr};
+    switch (ept) {
+      case 1: hipLaunchKernelGGL(bn_fused_fwd_kernel<1>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      case 2: hipLaunchKernelGGL(bn_fused_fwd_kernel<2>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      case 4: hipLaunchKernelGGL(bn_fused_fwd_kernel<4>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      case 8: hipLaunchKernelGGL(bn_fused_fwd_kernel<8>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      default: hipLaunchKernelGGL(bn_fused_fwd_kernel<16>, dim3(C), dim3(kFusedThreads), 0, s, a, g);
+    }
+    return launch_status("bn_fused_fwd_kernel launch failed");
+  }
   const bool vec = (HW & 3) == 0 && aligned16(x) && aligned16(y) && aligned16(skip);
   const dim3 rg(g.Q, N, C);
   if (vec)
@@ -358,6 +494,16 @@ extern "C" int dro_batchnorm_relu_backward(const float* grad_out, const float* x
   hipStream_t s = (hipStream_t)stream;
   BnBwdArgs a{grad_out, x, y, gamma, save_mean, save_invstd, relu, grad_x, grad_gamma, grad_beta,
               grad_skip, static_cast<double2*>(workspace)};
+  if (const int ept = fused_ept(N, HW)) {
+    switch (ept) {
+      case 1: hipLaunchKernelGGL(bn_fused_bwd_kernel<1>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      case 2: hipLaunchKernelGGL(bn_fused_bwd_kernel<2>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      case 4: hipLaunchKernelGGL(bn_fused_bwd_kernel<4>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      case 8: hipLaunchKernelGGL(bn_fused_bwd_kernel<8>, dim3(C), dim3(kFusedThreads), 0, s, a, g); break;
+      default: hipLaunchKernelGGL(bn_fused_bwd_kernel<16>, dim3(C), dim3(kFusedThreads), 0, s, a, g);
+    }
+    return launch_status("bn_fused_bwd_kernel launch failed");
+  }
   const bool vec = (HW & 3) == 0 && aligned16(grad_out) && aligned16(x) && aligned16(y) &&
                    aligned16(grad_x) && aligned16(grad_skip);
   const dim3 rg(g.Q, N, C);

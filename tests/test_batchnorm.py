@@ -16,7 +16,10 @@ import dro_sfm_amd.hip as hip
 from dro_sfm_amd.hip import _lib
 from dro_sfm_amd.networks.optim import extractor
 
-SHAPES = [(6, 64, 24, 80), (2, 3, 5, 7), (1, 16, 12, 40), (4, 1, 3, 4)]
+# one-launch path (a channel's N*H*W <= 16 K: bn_fused_*_kernel, every EPT) and
+# the two-launch path (> 16 K: partial sums + apply)
+SHAPES = [(6, 64, 24, 80), (2, 3, 5, 7), (1, 16, 12, 40), (4, 1, 3, 4), (2, 32, 48, 160), (3, 8, 37, 29),
+          (2, 8, 96, 100), (5, 4, 61, 67)]
 
 
 def _reference(x, w, b, skip, rm, rv, relu, eps, momentum):
