@@ -148,6 +148,16 @@ def record_bilinear_cells():
         _CELLS[0] = prev
 
 
+def record_branch(tag, mask, *inputs):
+    """Inside record_bilinear_cells(): keep a branch map an op already has --
+    the ReLU mask y > 0 of a BatchNorm+ReLU site, the stem pooling's argmax --
+    under `tag` (tests pin the oracle to it; nothing is computed when not
+    recording)."""
+    rec = _CELLS[0]
+    if rec is not None and torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in inputs):
+        rec.calls.append((tag, mask() if callable(mask) else mask))
+
+
 def _new_cells(tag, shape, device, *inputs):
     """A cell map (-1 filled) when recording and a backward will run."""
     rec = _CELLS[0]
@@ -925,9 +935,7 @@ def maxpool3x3s2(x, tag=None):
     if x.dtype != torch.float32 or x.dim() != 4:
         raise RuntimeError("maxpool3x3s2: expects a float32 NCHW tensor")
     y, arg = torch.ops.dro.maxpool3x3s2(x)
-    rec = _CELLS[0]
-    if rec is not None and torch.is_grad_enabled() and x.requires_grad:
-        rec.calls.append((("maxpool", tag), arg))
+    record_branch(("maxpool", tag), arg, x)
     return y
 
 

@@ -102,9 +102,13 @@ class DepthPoseNet(nn.Module):
         self.cnet = ResNetEncoder(out_chs=C, stride=r)
         self.cnet_depth = ResNetEncoder(out_chs=hd + cd, stride=r, num_input_images=1)
         self.cnet_pose = ResNetEncoder(out_chs=hd + cd, stride=r, num_input_images=2)
-        for name in ("fnet", "cnet", "cnet_depth", "cnet_pose"):    # test-record tags (hip.maxpool3x3s2)
+        for name in ("fnet", "cnet", "cnet_depth", "cnet_pose"):    # test-record tags (branch pinning)
             if hasattr(self, name):
-                object.__setattr__(getattr(self, name), "_dro_tag", name)
+                enc = getattr(self, name)
+                object.__setattr__(enc, "_dro_tag", name)
+                for mname, m in enc.named_modules():
+                    if isinstance(m, nn.BatchNorm2d):
+                        object.__setattr__(m, "_dro_tag", f"{name}.{mname}")
 
     # ------------------------------------------------------------------ helpers
     @property

@@ -98,7 +98,10 @@ class BatchNorm2d(nn.BatchNorm2d):
     def act(self, x, skip=None, relu=True):
         """relu(bn(x) + skip): one fused op in training mode on the GPU."""
         if _FUSED_BN[0] and self.training and x.is_cuda and self.momentum is not None:
-            return hip.batchnorm_act(x, self, skip=skip, relu=relu)
+            y = hip.batchnorm_act(x, self, skip=skip, relu=relu)
+            if relu:   # parity tests: the ReLU branch this site took (hip.record_bilinear_cells)
+                hip.ops.record_branch(("relu", getattr(self, "_dro_tag", None)), lambda: (y > 0).to(torch.uint8), x)
+            return y
         y = self(x)
         if skip is not None:
             y = y + skip

@@ -149,8 +149,8 @@ def cells_from_calls(calls):
             for j in range(c.shape[0]):
                 for i in range(c.shape[1]):
                     out[("photo", j, i)] = c[j, i]
-        elif isinstance(tag, tuple) and tag[0] == "maxpool":
-            out[tag] = c                                    # [B, C, Ho, Wo] window index dy * 3 + dx
+        elif isinstance(tag, tuple) and tag[0] in ("maxpool", "relu"):
+            out[tag] = c         # maxpool: [B,C,Ho,Wo] window index dy * 3 + dx; relu: y > 0 of a BN site
         elif isinstance(tag, tuple):
             s_ = steps.get(tag, 0)
             steps[tag] = s_ + 1
@@ -380,12 +380,28 @@ def max_pool_3x3s2(x, forced=None):
     return torch.where(tie, picked, y)
 
 
+def relu_pinned(v, cells=None, key=None):
+    """F.relu(v); with a Cells book holding ("relu", key) -- another
+    evaluation's mask y > 0 at this site -- the forced mask is taken where it
+    differs from v > 0 AND v is within 1e-5 of its channel's largest
+    magnitude from zero (a kink that rounding decides): there the output is
+    v * mask (the value stays within that margin of relu(v), the derivative
+    is the forced one)."""
+    forced = cells.forced.get(("relu", key)) if cells is not None else None
+    if forced is None:
+        return F.relu(v)
+    m = forced.to(torch.bool).reshape(v.shape)
+    scale = v.detach().abs().amax(dim=(0, 2, 3), keepdim=True)
+    use = (m != (v.detach() > 0)) & (v.detach().abs() <= 1e-5 * scale)
+    return torch.where(use, v * m.to(v.dtype), F.relu(v))
+
+
 def resnet_encoder(p, pre, x, training, stride=8, cells=None):
     """ResNetEncoder.forward (networks/optim/extractor.py:67-107) on torchvision's
     ResNet-18 layout (layer1..layer3, BasicBlocks) with the stride-8 fusion head.
     cells: a Cells book whose ("maxpool", <encoder>) entry pins the stem
     pooling's argmax (test hook)."""
-    x = F.relu(_bn(p, pre + "bn1", _conv(p, pre + "conv1", x, 2, 3), training))
+    x = relu_pinned(_bn(p, pre + "bn1", _conv(p, pre + "conv1", x, 2, 3), training), cells, pre + "bn1")
     forced = cells.forced.get(("maxpool", pre.rstrip("."))) if cells is not None else None
     x = max_pool_3x3s2(x, forced)
     feats = {}
@@ -393,12 +409,12 @@ def resnet_encoder(p, pre, x, training, stride=8, cells=None):
         for bi in range(2):
             b = f"{pre}layer{li}.{bi}."
             st = s if bi == 0 else 1
-            out = F.relu(_bn(p, b + "bn1", _conv(p, b + "conv1", x, st, 1), training))
+            out = relu_pinned(_bn(p, b + "bn1", _conv(p, b + "conv1", x, st, 1), training), cells, b + "bn1")
             out = _bn(p, b + "bn2", _conv(p, b + "conv2", out, 1, 1), training)
             idt = x
             if b + "downsample.0.weight" in p:
                 idt = _bn(p, b + "downsample.1", _conv(p, b + "downsample.0", x, st, 0), training)
-            x = F.relu(out + idt)
+            x = relu_pinned(out + idt, cells, b + "bn2")
         feats[li] = x
     x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
     x = F.relu(_conv(p, pre + "upconv1.0", x, 1, 1))

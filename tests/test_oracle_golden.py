@@ -410,3 +410,24 @@ def test_max_pool_forced_argmax():
     tn = t.clone().requires_grad_(True)
     F.max_pool2d(tn, 3, 2, 1).sum().backward()
     assert torch.equal(tf.grad, tn.grad)
+
+
+def test_relu_pinned():
+    """oracle.relu_pinned: the natural mask forced == F.relu; a forced mask
+    flips the derivative only where |v| is within 1e-5 of the channel scale."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(5)
+    v = torch.randn(2, 3, 4, 5, generator=g, dtype=torch.float64)
+    v[0, 1, 2, 3] = 1e-9                      # at the kink
+    book = O.Cells(forced={("relu", "s"): (v > 0).to(torch.uint8)})
+    a = v.clone().requires_grad_(True)
+    O.relu_pinned(a, book, "s").sum().backward()
+    b = v.clone().requires_grad_(True)
+    F.relu(b).sum().backward()
+    assert torch.equal(a.grad, b.grad)
+    flipped = (v > 0).to(torch.uint8)
+    flipped[0, 1, 2, 3] = 0                   # near the kink: taken
+    flipped[1, 0, 0, 0] = 1 - flipped[1, 0, 0, 0]   # far from it: ignored
+    c = v.clone().requires_grad_(True)
+    O.relu_pinned(c, O.Cells(forced={("relu", "s"): flipped}), "s").sum().backward()
+    assert c.grad[0, 1, 2, 3] == 0 and c.grad[1, 0, 0, 0] == b.grad[1, 0, 0, 0]
