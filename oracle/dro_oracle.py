@@ -107,6 +107,11 @@ def sample_grid(depth, K, ref_K, pose, scale):
     return torch.stack([u, v], -1).reshape(B, h, w, 2)
 
 
+# diagnostics: how many positions each kind of pinning actually moved off the
+# natural branch in the evaluations since the last clear (tools/diag_*)
+PIN_STATS = {"cells": 0, "maxpool": 0, "relu": 0}
+
+
 class Cells:
     """Bilinear cells of a step's warps (test hook).  grid_sample's value is
     continuous in the sampling position but its derivative jumps where a
@@ -182,6 +187,7 @@ def grid_sample_cells(img, grid, cells=None, book=None, key=None):
         # ill-conditioned recurrence), the natural cell stays
         near = ((ix.detach() - fx - 0.5).abs() <= 1.0) & ((iy.detach() - fy - 0.5).abs() <= 1.0)
         forced = (c != -1) & near
+        PIN_STATS["cells"] += int((forced & ((fx != x0) | (fy != y0))).sum())
         x0 = torch.where(forced, fx, x0)
         y0 = torch.where(forced, fy, y0)
     tx, ty = ix - x0, iy - y0
@@ -270,6 +276,9 @@ def smoothness(inv_depths, image, smooth_w):
     return smooth_w * (total / n)
 
 
+LAST_SELECTION = []   # per prediction, the natural min-candidate map of the last call (diagnostics)
+
+
 def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_w=0.85, C1=1e-4,
                            C2=9e-4, smooth_w=0.001, automask=True, reduce="min",
                            forced_selection=None, cells=None):
@@ -299,7 +308,9 @@ def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_
             idx = idx.unsqueeze(1) if idx.dim() == 3 else idx           # [B,1,H,W]
             li = torch.gather(torch.cat(maps, 1), 1, idx).mean()
         elif reduce == "min":
-            li = torch.cat(maps, 1).min(1, True)[0].mean()
+            mv, mi = torch.cat(maps, 1).min(1, True)
+            LAST_SELECTION[i:] = [mi.squeeze(1).to(torch.uint8)]     # diagnostics: the natural selection
+            li = mv.mean()
         else:
             li = sum(m.mean() for m in maps) / len(maps)
         photo = photo + 0.85 ** (n - i - 1) * li
@@ -377,6 +388,7 @@ def max_pool_3x3s2(x, forced=None):
     idx = forced.to(torch.int64).reshape(B, C, 1, Ho, Wo).clamp(0, 8)
     picked = torch.gather(win, 2, idx).squeeze(2)
     tie = (y.detach() - picked.detach()).abs() <= 1e-5 * y.detach().abs().clamp_min(1e-30)
+    PIN_STATS["maxpool"] += int((tie & (idx.squeeze(2) != torch.argmax(win.detach(), 2))).sum())
     return torch.where(tie, picked, y)
 
 
@@ -393,6 +405,8 @@ def relu_pinned(v, cells=None, key=None):
     m = forced.to(torch.bool).reshape(v.shape)
     scale = v.detach().abs().amax(dim=(0, 2, 3), keepdim=True)
     use = (m != (v.detach() > 0)) & (v.detach().abs() <= 1e-5 * scale)
+    PIN_STATS["relu"] += int(use.sum())
+    PIN_STATS["relu_far"] = PIN_STATS.get("relu_far", 0) + int(((m != (v.detach() > 0)) & ~use).sum())
     return torch.where(use, v * m.to(v.dtype), F.relu(v))
 
 

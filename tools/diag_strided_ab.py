@@ -150,8 +150,14 @@ def oracle_check():
         for name, (cells, sel) in (("own cells+sel", runs[hip_native][:2]),
                                    ("other run's cells+sel", runs[not hip_native][:2]),
                                    ("natural cells, own sel", (None, runs[hip_native][1]))):
+            for k_ in list(O.PIN_STATS):
+                O.PIN_STATS[k_] = 0
             _, g64 = T._oracle_grads(spec, "it12-h-out", mind, maxd, cpu_batch, "selfsup", torch.float64, sel,
                                      False, cells)
+            kinds = {}
+            for key in (cells or {}):
+                kinds[key[0]] = kinds.get(key[0], 0) + 1
+            print(f"    recorded keys {kinds}; positions moved off the natural branch {dict(O.PIN_STATS)}")
             l2, worst = diff(grads, {k: v.double() for k, v in g64.items() if k in grads})
             print(f"  HIP {'native' if hip_native else 'miopen'} vs fp64 on {name}: L2 {l2:.3e}  "
                   + ", ".join(f"{k} {v:.2e}" for k, v in worst[:3]), flush=True)
