@@ -547,7 +547,12 @@ def main():
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_blocks": "depth block + pose block (side stream, with both context encoders)",
                    "encoder_3x3_s1": "miopen" if args.miopen_encoder_convs else "hip",
-                   "encoder_strided": "hip" if args.native_strided_convs else "miopen"},
+                   "encoder_strided": "hip" if args.native_strided_convs else "miopen",
+                   "exchange": ("none (world 1)" if world == 1 else
+                                "bucketed all-reduce in the step graph, overlapping backward"
+                                if getattr(stepper, "in_graph", False) else
+                                "all-reduce after each graph replay" if stepper is not None else
+                                "bucketed all-reduce from backward hooks (eager)")},
         "final_loss": round(float(loss), 6),
     }
     if rank == 0 and not args.no_roofline:

@@ -36,6 +36,7 @@ The step order matches HorovodTrainer.train: zero_grad -> forward -> loss ->
 backward -> (all-reduce) -> Adam step.
 """
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -620,6 +621,22 @@ class GraphedTrainStep:
         cur.wait_stream(side)
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle() if share_pool else None
+        try:
+            self._capture_all(flips)
+        except RuntimeError as e:
+            if not self.in_graph:
+                raise
+            # a capture that fails with the collectives inside fails the same way on
+            # every rank (same program, same point): all ranks fall back together to
+            # the exchange after each replay, and say so
+            print(f"[GraphedTrainStep] capture with in-graph all-reduces failed ({e}); "
+                  "falling back to the exchange after each replay", file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            self.in_graph, self.outside = False, True
+            self.pool = torch.cuda.graph_pool_handle() if share_pool else None
+            self._capture_all(flips)
+
+    def _capture_all(self, flips):
         self.graphs = {}
         for f in flips:
             g = torch.cuda.CUDAGraph()
