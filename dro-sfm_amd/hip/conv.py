@@ -679,6 +679,7 @@ def _sepgru_setup(ctx, inputs, output):
     ctx.mark_non_differentiable(zr, rh, q)
     ctx.set_materialize_grads(False)     # no zero-filled gradients for the three saved outputs
     ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in xs]
+    ctx.hsink = _sink_of(h) if h.requires_grad else None
     ctx.need = (h.requires_grad, [x.requires_grad for x in xs],
                 any(t.requires_grad for t in (wz, bz, wr, br)), any(t.requires_grad for t in (wq, bq)))
     ctx.scope = current_scope()
@@ -696,8 +697,13 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
     if dhn is None:
         return (None,) * 7 + ([None] * len(xs), None, None)
     dhn = dhn.contiguous()
-    # stage 1: pre-activation grads of q and z, dh = dh' (1-z)
-    dq, dh = torch.empty_like(h), torch.empty_like(h)
+    # stage 1: pre-activation grads of q and z, dh = dh' (1-z).  When h has a
+    # gradient sink that no consumer has written yet (the next GRU step runs its
+    # backward before the heads that also read this state), dh is built right in
+    # the sink and autograd gets None for h (no add launch)
+    dq = torch.empty_like(h)
+    h_in_sink = ctx.hsink is not None and not ctx.hsink.written
+    dh = ctx.hsink.target()[0] if h_in_sink else torch.empty_like(h)
     dzr = torch.empty_like(zr)
     torch.ops.dro.gru_backward_elem(1, dhn, zr, q, h, None, dq, dzr, dh)
     # candidate conv over [r*h, x]: d(r*h), dx (overwrite); sources with a
@@ -720,7 +726,7 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
         _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), wsplit=zb)
         if not _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
             _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwzr, gbzr, 1)
-        return (dh if need_h else None, *nones, dxs, None, None)
+        return (dh if need_h and not h_in_sink else None, *nones, dxs, None, None)
     gwq, gbq, qacc, qfirst = _grad_buffers(ctx.scope, ctx.keys[1], wq, hd, h.device)
     _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [drh, *tg], qacc0, gwq, gbq, qacc, qb)
     # stage 2: pre-activation grad of r, dh += d(r*h) r
@@ -730,7 +736,7 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
     _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), gwzr, gbzr, zacc, zb)
     gz = (gwzr[:hd], gbzr[:hd], gwzr[hd:], gbzr[hd:]) if (zfirst and need_zr_w) else (None,) * 4
     gq = (gwq, gbq) if (qfirst and need_q_w) else (None, None)
-    return (dh if need_h else None, *gz, *gq, dxs, None, None)
+    return (dh if need_h and not h_in_sink else None, *gz, *gq, dxs, None, None)
 
 
 torch.library.register_autograd("dro::sepconvgru_half", _sepgru_backward, setup_context=_sepgru_setup)

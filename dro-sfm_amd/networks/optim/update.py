@@ -237,7 +237,8 @@ class BasicUpdateBlockDepth(nn.Module):
             # the state feeds the cost, the 7x7 conv, both GRU halves and the update
             inv_depth = hip.grad_sink(inv_depth)
             feat = self.encoder.sources(inv_depth, cost_func(scale_func(inv_depth)[0]))
-            net = self.depth_gru(net, [context, *feat])
+            # the state feeds the heads and the next GRU step: one gradient buffer
+            net = hip.grad_sink(self.depth_gru(net, [context, *feat]))
             delta, mask = self.heads(net)
             inv_depth = inv_depth + delta
             invs.append(inv_depth)
@@ -257,7 +258,7 @@ class BasicUpdateBlockPose(nn.Module):
     def forward(self, net, cost_func, pose, inp, seq_len=4):
         seq = []
         for _ in range(seq_len):
-            net = self.pose_gru(net, [inp, *self.encoder.sources(pose, cost_func(pose))])
+            net = hip.grad_sink(self.pose_gru(net, [inp, *self.encoder.sources(pose, cost_func(pose))]))
             pose = self.pose_head(net, pose)               # pose + pose_head(net), one launch
             seq.append(pose)
         return net, seq
