@@ -431,3 +431,21 @@ def test_relu_pinned():
     c = v.clone().requires_grad_(True)
     O.relu_pinned(c, O.Cells(forced={("relu", "s"): flipped}), "s").sum().backward()
     assert c.grad[0, 1, 2, 3] == 0 and c.grad[1, 0, 0, 0] == b.grad[1, 0, 0, 0]
+
+
+def test_cells_from_calls_keys():
+    """oracle.cells_from_calls maps the product's record (tag, map) in call
+    order to the oracle's keys: cost calls per inner step and view, the
+    photometric calls per (view, prediction), pooling argmax and ReLU masks
+    by encoder / BatchNorm site."""
+    cost = torch.zeros(2, 1, 3, 4, dtype=torch.int32)                 # [N=2, B=1, h, w]
+    photo = torch.zeros(2, 3, 1, 6, 8, dtype=torch.int32)             # [N=2, n=3, B=1, H, W]
+    calls = [(("depth", 0), cost), (("depth", 0), cost + 1), (("pose", 0), cost + 2), ("photo", photo),
+             (("maxpool", "fnet"), torch.zeros(1, 2, 3, 4, dtype=torch.uint8)),
+             (("relu", "fnet.layer1.0.bn1"), torch.ones(1, 2, 3, 4, dtype=torch.uint8))]
+    out = O.cells_from_calls(calls)
+    assert int(out[("depth", 0, 1, 0)][0, 0, 0]) == 1 and ("depth", 0, 1, 1) in out
+    assert int(out[("pose", 0, 0, 1)][0, 0, 0]) == 2
+    assert out[("photo", 1, 2)].shape == (1, 6, 8)
+    assert out[("maxpool", "fnet")].dtype == torch.int64
+    assert int(out[("relu", "fnet.layer1.0.bn1")].sum()) == 24
