@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void plane_sweep_wide_kernel(WarpArgs a, const
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 template <int CG, bool NT>
-__global__ __launch_bounds__(512) void plane_sweep_lds_kernel(WarpArgs a, const float* __restrict__ disp, int D,
+__global__ __launch_bounds__(1024) void plane_sweep_lds_kernel(WarpArgs a, const float* __restrict__ disp, int D,
                                                               int DG, float* __restrict__ cost) {
   extern __shared__ float4 lds4[];
   float* fr_l = reinterpret_cast<float*>(lds4);
@@ -406,11 +406,14 @@ __global__ __launch_bounds__(512) void plane_sweep_lds_kernel(WarpArgs a, const 
   load_pose(a.pose + (size_t)b * pose_stride(a.pose_mode), a.pose_mode, R, t);
   const float4* fm4 = reinterpret_cast<const float4*>(a.fmap + ((size_t)b * a.C + c0) * P);
   const int d_end = min(D, (dg + 1) * DG);
-  for (int d = dg * DG; d < d_end; ++d) {
+  // 1024-thread blocks: two planes side by side, 512 threads each
+  const int lanes = blockDim.x > 512 ? 512 : blockDim.x, pp = threadIdx.x / lanes, tq = threadIdx.x - pp * lanes;
+  const int pstep = blockDim.x / lanes;
+  for (int d = dg * DG + pp; d < d_end; d += pstep) {
     float dd;
     const float depth = decode_depth(disp[d], DRO_DEPTH_DISP, a.min_disp, a.span, &dd);
     v4f* out4 = reinterpret_cast<v4f*>(cost + (((size_t)b * D + d) * a.C + c0) * P);
-    for (int q = threadIdx.x; q < P4; q += blockDim.x) {
+    for (int q = tq; q < P4; q += lanes) {
       int idx[4][4];
       float wgt[4][4];
 #pragma unroll
@@ -673,7 +676,10 @@ extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref,
   static const int min_blocks = env_int("DRO_SWEEP_BLOCKS", 512);
   static const bool wide = env_int("DRO_SWEEP_WIDE", 0) != 0;
   static const bool nt = env_int("DRO_SWEEP_NT", 1) != 0;      // non-temporal volume stores
-  static const int threads = env_int("DRO_SWEEP_THREADS", 512) == 256 ? 256 : 512;   // 512: 16 waves per CU (46.7 -> 43.5 us)
+  static const int threads = [] {   // 512: 16 waves per CU (46.7 -> 43.5 us); 1024: two planes at once
+    const int t = env_int("DRO_SWEEP_THREADS", 512);
+    return t == 256 || t == 1024 ? t : 512;
+  }();
   int CG = cg_max;
   while (CG > 1 && (C % CG != 0 || (size_t)CG * P * sizeof(float) > 65536)) CG >>= 1;
   if (!wide && aligned && P % 4 == 0 && C % CG == 0 && (size_t)CG * P * sizeof(float) <= 65536) {
