@@ -344,6 +344,75 @@ def test_photometric_loss_kitti_size_vs_oracle(hip):
     assert rel(vg.grad.double(), gv64) <= max(TOL, 4 * rel(gv32, gv64))
 
 
+@pytest.mark.parametrize("reduce_min", [True, False])
+def test_photometric_loss_ragged_vs_oracle(hip, reduce_min):
+    """Ragged shapes (37x53: no dimension a multiple of the kernels' tiles,
+    B=1, n=3 predictions, N=3 views), min and mean reductions, against the
+    fp64 oracle on the kernel's selection and cells: loss 1e-4, gradients
+    1e-4 relative L2 (or 4x the fp32 oracle's own distance)."""
+    g = torch.Generator().manual_seed(12)
+    B, H, W, n, N = 1, 37, 53, 3, 3
+    K = kitti_K(B, W=W, H=H)
+    image = smooth_images(B, H, W, 71, detail=0.3)
+    ctx = torch.stack([smooth_images(B, H, W, 72 + j, detail=0.3) for j in range(N)])
+    invs = 0.05 + 0.3 * torch.rand(n, B, 1, H, W, generator=g)
+    vec = torch.cat([0.05 * torch.randn(B, N, n, 3, generator=g), 0.01 * torch.randn(B, N, n, 3, generator=g)], 3)
+    ig, vg = invs.to(DEV).requires_grad_(True), vec.to(DEV).requires_grad_(True)
+    with hip.record_bilinear_cells() as rec:
+        loss, metrics, sel = hip.photometric_loss(image.to(DEV), ctx.to(DEV), ig, vg.permute(1, 2, 0, 3),
+                                                  K.to(DEV), reduce_min=reduce_min, automask=reduce_min,
+                                                  return_selection=True)
+        loss.sum().backward()
+    ref = {}
+    for dt in (torch.float32, torch.float64):
+        ic = invs.to(dt).detach().clone().requires_grad_(True)
+        vc = vec.to(dt).detach().clone().requires_grad_(True)
+        out = O.photometric_decay_loss(image.to(dt), list(ctx.to(dt)), list(ic), K.to(dt), K.to(dt),
+                                       [[vc[:, j, i] for i in range(n)] for j in range(N)],
+                                       automask=reduce_min, reduce="min" if reduce_min else "mean",
+                                       forced_selection=sel.cpu().unsqueeze(2) if reduce_min else None,
+                                       cells=O.Cells(forced=cells_from_record(rec)))
+        out["loss"].sum().backward()
+        ref[dt] = (out, ic.grad.double(), vc.grad.double())
+    out64, gi64, gv64 = ref[torch.float64]
+    _, gi32, gv32 = ref[torch.float32]
+    assert rel(loss, out64["loss"]) < TOL
+    l2 = lambda a, b: float((a.double().cpu() - b).norm() / b.norm())
+    assert l2(ig.grad, gi64) <= max(TOL, 4 * l2(gi32, gi64)), (l2(ig.grad, gi64), l2(gi32, gi64))
+    assert l2(vg.grad, gv64) <= max(TOL, 4 * l2(gv32, gv64)), (l2(vg.grad, gv64), l2(gv32, gv64))
+
+
+def test_warp_cost_ragged_vs_oracle(hip):
+    """Ragged warp-cost shapes: 7x13 maps, C=22 (not a multiple of the
+    per-thread channel count), N=3 views in one launch, per-view costs and
+    the depth-mean cost; forward and all gradients 1e-4 against the fp64
+    oracle on the kernel's cells."""
+    g = torch.Generator().manual_seed(13)
+    B, C, h, w, N = 2, 22, 7, 13, 3
+    K = kitti_K(B, W=8 * w, H=8 * h)
+    fmap, frefs = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    disp = torch.rand(B, 1, h, w, generator=g)
+    poses = torch.cat([0.2 * torch.randn(N, B, 3, generator=g), 0.03 * torch.randn(N, B, 3, generator=g)], 2)
+    for reduce_mean in (False, True):
+        Gc = torch.randn((B, C, h, w) if reduce_mean else (N, B, C, h, w), generator=g)
+        tens = [t.to(DEV).requires_grad_(True) for t in (fmap, frefs, disp, poses)]
+        with hip.record_bilinear_cells() as rec:
+            out = hip.warp_cost(tens[0], tens[1], tens[2], tens[3], K.to(DEV), depth_mode=hip.DEPTH_DISP,
+                                min_depth=0.5, max_depth=80.0, reduce_mean=reduce_mean, tag=("depth", 0))
+            (out * Gc.to(DEV)).sum().backward()
+        cells = cells_from_record(rec)
+        r = [t.double().requires_grad_(True) for t in (fmap, frefs, disp, poses)]
+        book = O.Cells(forced=cells)
+        depth = O.inv2depth(O.disp_to_depth(r[2], 0.5, 80.0))
+        costs = [O.get_cost_each(r[3][j], r[0], r[1][j], depth, K.double(), K.double(), 1 / 8, book,
+                                 ("depth", 0, 0, j)) for j in range(N)]
+        ref = torch.stack(costs).mean(0) if reduce_mean else torch.stack(costs)
+        (ref * Gc.double()).sum().backward()
+        assert rel(out, ref) < TOL, reduce_mean
+        for a, b in zip(tens, r):
+            assert rel(a.grad, b.grad) < TOL, reduce_mean
+
+
 # ------------------------------------------------------------------ convex upsample
 def test_convex_upsample(hip):
     d = fx("upsample")
