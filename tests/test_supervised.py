@@ -93,10 +93,13 @@ def _scene(B, N, n, H, W, K, mind, maxd, seed, valid_frac=1.0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["scannet_view3", "scannet_view5", "kitti_sparse"])
+@pytest.mark.parametrize("cfg", ["scannet_view3", "scannet_view5", "kitti_sparse", "ragged"])
 @pytest.mark.parametrize("as_matrix", [False, True])
 def test_supervised_vs_oracle(hip, cfg, as_matrix):
-    if cfg.startswith("scannet"):
+    if cfg == "ragged":     # no dimension a multiple of the kernels' tiles, 3 views, 3 predictions
+        B, N, n, H, W, mind, maxd, frac = 3, 3, 3, 37, 53, 0.2, 10.0, 0.5
+        K = torch.tensor(SCANNET_K_320).unsqueeze(0).repeat(B, 1, 1)
+    elif cfg.startswith("scannet"):
         B, N, n, H, W, mind, maxd, frac = 2, (2 if cfg == "scannet_view3" else 4), 4, 240, 320, 0.2, 10.0, 1.0
         K = torch.tensor(SCANNET_K_320).unsqueeze(0).repeat(B, 1, 1)
     else:  # KITTI 192x640, sparse LiDAR-like GT (5 % valid), it12-h: n = 4
