@@ -158,6 +158,14 @@ def record_branch(tag, mask, *inputs):
         rec.calls.append((tag, mask() if callable(mask) else mask))
 
 
+def record_relu(y, mod):
+    """y (the ReLU output of module `mod`'s convolution) unchanged; inside
+    record_bilinear_cells() its branch y > 0 is kept under ("relu_seq",
+    mod._dro_tag), one entry per call of the site."""
+    record_branch(("relu_seq", getattr(mod, "_dro_tag", None)), lambda: (y > 0).to(torch.uint8), y)
+    return y
+
+
 def _new_cells(tag, shape, device, *inputs):
     """A cell map (-1 filled) when recording and a backward will run."""
     rec = _CELLS[0]

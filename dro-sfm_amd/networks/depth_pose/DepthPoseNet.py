@@ -109,6 +109,9 @@ class DepthPoseNet(nn.Module):
                 for mname, m in enc.named_modules():
                     if isinstance(m, nn.BatchNorm2d):
                         object.__setattr__(m, "_dro_tag", f"{name}.{mname}")
+        for mname, m in self.named_modules():      # conv ReLU sites (update.relu_rec)
+            if isinstance(m, nn.Conv2d):
+                object.__setattr__(m, "_dro_tag", mname)
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -185,6 +188,7 @@ class DepthPoseNet(nn.Module):
                 ctx_d = stamp_grad(self.cnet_depth(target_image), "bwd:cnet_depth_begin")
                 h_d, x_d = torch.split(ctx_d, [hd, cd], 1)     # split: one cat backward
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
+                hip.ops.record_branch(("relu_seq", "ctx_d"), lambda: (x_d > 0).to(torch.uint8), x_d)
                 stamp("fwd:cnet_depth")
                 if d_stream is not None and d_stream is p_stream:
                     d_event = torch.cuda.Event()
@@ -195,6 +199,7 @@ class DepthPoseNet(nn.Module):
                 ctx_p = stamp_grad(self.cnet_pose(pairs), "bwd:cnet_pose_begin")   # [N*B, hd+cd, h, w]
                 h_p, x_p = torch.split(ctx_p, [hd, cd], 1)
                 h_p, x_p = torch.tanh(h_p), torch.relu(x_p)
+                hip.ops.record_branch(("relu_seq", "ctx_p"), lambda: (x_p > 0).to(torch.uint8), x_p)
                 stamp("fwd:cnet_pose")
 
         fmaps = stamp_grad(self.fnet(torch.cat([target_image] + list(ref_imgs), 0)), "bwd:fnet_begin")

@@ -177,11 +177,12 @@ class ResNetEncoder(nn.Module):
         s4 = self.layer1(x)
         s8 = self.layer2(s4)
         x = self.layer3(s8)
-        x = conv3x3(self.upconv1[0], hip.bilinear_upsample2x(x), "relu")
-        x = conv3x3(self.upconv1_fusion[0], [x, s8], "relu")      # concat read in place
+        rec = hip.ops.record_relu         # parity tests: the ReLU branch of each decoder conv
+        x = rec(conv3x3(self.upconv1[0], hip.bilinear_upsample2x(x), "relu"), self.upconv1[0])
+        x = rec(conv3x3(self.upconv1_fusion[0], [x, s8], "relu"), self.upconv1_fusion[0])   # concat read in place
         if self.stride == 4:
-            x = conv3x3(self.upconv2[0], hip.bilinear_upsample2x(x), "relu")
-            x = conv3x3(self.upconv2_fusion[0], [x, s4], "relu")
+            x = rec(conv3x3(self.upconv2[0], hip.bilinear_upsample2x(x), "relu"), self.upconv2[0])
+            x = rec(conv3x3(self.upconv2_fusion[0], [x, s4], "relu"), self.upconv2_fusion[0])
         x = conv3x3(self.out_conv, x)
         if chunks is not None:
             return torch.chunk(x, chunks, 0)

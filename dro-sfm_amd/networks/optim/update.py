@@ -73,6 +73,9 @@ def conv_cat(x, convs, act=None):
     return torch.split(y, [c.out_channels for c in convs], 1)
 
 
+relu_rec = hip.ops.record_relu     # parity tests: the ReLU branch of a conv site
+
+
 def fused_groups(*convs):
     """Parameter groups read as one fused tensor: [weights], [biases]."""
     return [[c.weight for c in convs], [c.bias for c in convs]]
@@ -94,7 +97,7 @@ class DepthHead(nn.Module):
 
     def forward(self, x_d, act_fn=torch.tanh):
         act = {torch.tanh: "tanh", torch.sigmoid: "sigmoid"}.get(act_fn)
-        y = conv(conv(x_d, self.conv1.weight, self.conv1.bias, "relu"),
+        y = conv(relu_rec(conv(x_d, self.conv1.weight, self.conv1.bias, "relu"), self.conv1),
                  self.conv2.weight, self.conv2.bias, act)
         return y if act is not None else act_fn(y)
 
@@ -116,7 +119,7 @@ class PoseHead(nn.Module):
 
     def forward(self, x_p, pose=None):
         """The pose delta, or pose + delta when `pose` [B, 6] is given."""
-        y = conv(conv(x_p, self.conv1_pose.weight, self.conv1_pose.bias, "relu"),
+        y = conv(relu_rec(conv(x_p, self.conv1_pose.weight, self.conv1_pose.bias, "relu"), self.conv1_pose),
                  self.conv2_pose.weight, self.conv2_pose.bias)
         return hip.pose_mean(y, 0.01, pose)
 
@@ -168,10 +171,11 @@ class _Projection(nn.Module):
         t = self._tag
         c1, c2 = self.convc1, self.convc2
         s1, s2, f = (getattr(self, f"conv{t}{i}") for i in ("1", "2", ""))
-        cor = conv(conv(cost, c1.weight, c1.bias, "relu"), c2.weight, c2.bias, "relu")
-        sfm = conv(conv(state_map, s1.weight, s1.bias, "relu"), s2.weight, s2.bias, "relu")
+        cor = relu_rec(conv(relu_rec(conv(cost, c1.weight, c1.bias, "relu"), c1), c2.weight, c2.bias, "relu"), c2)
+        sfm = relu_rec(conv(relu_rec(conv(state_map, s1.weight, s1.bias, "relu"), s1), s2.weight, s2.bias, "relu"),
+                       s2)
         # both GRU halves read the fused features: their gradients meet in a sink
-        return [hip.grad_sink(conv([cor, sfm], f.weight, f.bias, "relu")), state_map]
+        return [hip.grad_sink(relu_rec(conv([cor, sfm], f.weight, f.bias, "relu"), f)), state_map]
 
 
 class ProjectionInputDepth(_Projection):
@@ -208,7 +212,7 @@ class UpMaskNet(nn.Module):
 
     def forward(self, feat):
         m0, m2 = self.mask[0], self.mask[2]
-        return conv(conv(feat, m0.weight, m0.bias, "relu"), m2.weight, m2.bias, None, 0.25)
+        return conv(relu_rec(conv(feat, m0.weight, m0.bias, "relu"), m0), m2.weight, m2.bias, None, 0.25)
 
 
 class BasicUpdateBlockDepth(nn.Module):
@@ -227,6 +231,7 @@ class BasicUpdateBlockDepth(nn.Module):
     def heads(self, net):
         """DepthHead.conv1 and mask.0 read the same state: one launch."""
         a, b = conv_cat(net, (self.depth_head.conv1, self.mask[0]), "relu")
+        a, b = relu_rec(a, self.depth_head.conv1), relu_rec(b, self.mask[0])
         c2, m2 = self.depth_head.conv2, self.mask[2]
         return conv(a, c2.weight, c2.bias, "tanh"), conv(b, m2.weight, m2.bias, None, 0.25)
 

@@ -156,6 +156,10 @@ def cells_from_calls(calls):
                     out[("photo", j, i)] = c[j, i]
         elif isinstance(tag, tuple) and tag[0] in ("maxpool", "relu"):
             out[tag] = c         # maxpool: [B,C,Ho,Wo] window index dy * 3 + dx; relu: y > 0 of a BN site
+        elif isinstance(tag, tuple) and tag[0] == "relu_seq":     # y > 0 of the n-th call of a conv ReLU site
+            n = steps.get(tag, 0)
+            steps[tag] = n + 1
+            out[("relu", (tag[1], n))] = c
         elif isinstance(tag, tuple):
             s_ = steps.get(tag, 0)
             steps[tag] = s_ + 1
@@ -402,12 +406,42 @@ def relu_pinned(v, cells=None, key=None):
     forced = cells.forced.get(("relu", key)) if cells is not None else None
     if forced is None:
         return F.relu(v)
+    return _relu_forced(v, forced, 1e-5)
+
+
+# near-kink margin of the update-block / head / decoder ReLU sites, relative to
+# the channel's largest magnitude: they sit behind the recurrence, where two
+# fp32 realisations of the step differ by more than at the encoders' BN sites
+SEQ_RELU_TOL = 1e-4
+
+
+def _relu_forced(v, forced, tol):
     m = forced.to(torch.bool).reshape(v.shape)
     scale = v.detach().abs().amax(dim=(0, 2, 3), keepdim=True)
-    use = (m != (v.detach() > 0)) & (v.detach().abs() <= 1e-5 * scale)
+    use = (m != (v.detach() > 0)) & (v.detach().abs() <= tol * scale)
     PIN_STATS["relu"] += int(use.sum())
     PIN_STATS["relu_far"] = PIN_STATS.get("relu_far", 0) + int(((m != (v.detach() > 0)) & ~use).sum())
     return torch.where(use, v * m.to(v.dtype), F.relu(v))
+
+
+def relu_site(v, rk, name):
+    """F.relu(v) at a convolution (or context) ReLU that runs once per call of
+    its block; rk = (cells, n, part): with a Cells book holding
+    ("relu", (name, n)) -- the product's mask y > 0 for the n-th call of that
+    site (hip.record_bilinear_cells, tag ("relu_seq", name)) -- the forced
+    mask is taken at near-kinks as in relu_pinned.  part = (j, B): the
+    product ran the reference views stacked along the batch (update.py:14),
+    the oracle runs view j -- its rows j*B..(j+1)*B of the recorded mask."""
+    if rk is None or rk[0] is None:
+        return F.relu(v)
+    cells, n, part = rk
+    forced = cells.forced.get(("relu", (name, n)))
+    if forced is None:
+        return F.relu(v)
+    if part is not None:
+        j, B = part
+        forced = forced[j * B:(j + 1) * B]
+    return _relu_forced(v, forced, SEQ_RELU_TOL)
 
 
 def resnet_encoder(p, pre, x, training, stride=8, cells=None):
@@ -430,13 +464,16 @@ def resnet_encoder(p, pre, x, training, stride=8, cells=None):
                 idt = _bn(p, b + "downsample.1", _conv(p, b + "downsample.0", x, st, 0), training)
             x = relu_pinned(out + idt, cells, b + "bn2")
         feats[li] = x
+    rk = (cells, 0, None)
     x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
-    x = F.relu(_conv(p, pre + "upconv1.0", x, 1, 1))
-    x = F.relu(_conv(p, pre + "upconv1_fusion.0", torch.cat([x, feats[2]], 1), 1, 1))
+    x = relu_site(_conv(p, pre + "upconv1.0", x, 1, 1), rk, pre + "upconv1.0")
+    x = relu_site(_conv(p, pre + "upconv1_fusion.0", torch.cat([x, feats[2]], 1), 1, 1), rk,
+                  pre + "upconv1_fusion.0")
     if stride == 4:
         x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
-        x = F.relu(_conv(p, pre + "upconv2.0", x, 1, 1))
-        x = F.relu(_conv(p, pre + "upconv2_fusion.0", torch.cat([x, feats[1]], 1), 1, 1))
+        x = relu_site(_conv(p, pre + "upconv2.0", x, 1, 1), rk, pre + "upconv2.0")
+        x = relu_site(_conv(p, pre + "upconv2_fusion.0", torch.cat([x, feats[1]], 1), 1, 1), rk,
+                      pre + "upconv2_fusion.0")
     return _conv(p, pre + "out_conv", x, 1, 1)
 
 
@@ -451,60 +488,71 @@ def sep_conv_gru(p, pre, h, x):
     return h
 
 
-def depth_head(p, pre, x, act=torch.tanh):
-    """DepthHead (update.py:5-14)."""
-    return act(_conv(p, pre + "conv2", F.relu(_conv(p, pre + "conv1", x, 1, 1)), 1, 1))
+def depth_head(p, pre, x, act=torch.tanh, rk=None):
+    """DepthHead (update.py:5-14).  rk: relu_site's (cells, call, part)."""
+    return act(_conv(p, pre + "conv2", relu_site(_conv(p, pre + "conv1", x, 1, 1), rk, pre + "conv1"), 1, 1))
 
 
-def pose_head(p, pre, x):
+def pose_head(p, pre, x, rk=None):
     """PoseHead (update.py:16-28): spatial mean, rotation scaled by 0.01."""
-    o = _conv(p, pre + "conv2_pose", F.relu(_conv(p, pre + "conv1_pose", x, 1, 1)), 1, 1)
+    o = _conv(p, pre + "conv2_pose", relu_site(_conv(p, pre + "conv1_pose", x, 1, 1), rk, pre + "conv1_pose"),
+              1, 1)
     o = o.mean(3).mean(2)
     return torch.cat([o[:, :3], 0.01 * o[:, 3:]], 1)
 
 
-def mask_head(p, pre, x):
+def mask_head(p, pre, x, rk=None):
     """.25 * mask(x): 3x3 -> relu -> 1x1 to 9*r*r (update.py:150-153, :128-139)."""
-    return 0.25 * _conv(p, pre + "2", F.relu(_conv(p, pre + "0", x, 1, 1)), 1, 0)
+    return 0.25 * _conv(p, pre + "2", relu_site(_conv(p, pre + "0", x, 1, 1), rk, pre + "0"), 1, 0)
 
 
-def projection_depth(p, pre, inv, cost):
+def _branch(p, pre, x, names, pads, rk):
+    """relu(conv(relu(conv(x)))) of the two projection branches."""
+    (a, b), (pa, pb) = names, pads
+    return relu_site(_conv(p, pre + b, relu_site(_conv(p, pre + a, x, 1, pa), rk, pre + a), 1, pb), rk, pre + b)
+
+
+def projection_depth(p, pre, inv, cost, rk=None):
     """ProjectionInputDepth (update.py:77-99)."""
-    cor = F.relu(_conv(p, pre + "convc2", F.relu(_conv(p, pre + "convc1", cost)), 1, 1))
-    dfm = F.relu(_conv(p, pre + "convd2", F.relu(_conv(p, pre + "convd1", inv, 1, 3)), 1, 1))
-    out = F.relu(_conv(p, pre + "convd", torch.cat([cor, dfm], 1), 1, 1))
+    cor = _branch(p, pre, cost, ("convc1", "convc2"), (0, 1), rk)
+    dfm = _branch(p, pre, inv, ("convd1", "convd2"), (3, 1), rk)
+    out = relu_site(_conv(p, pre + "convd", torch.cat([cor, dfm], 1), 1, 1), rk, pre + "convd")
     return torch.cat([out, inv], 1)
 
 
-def projection_pose(p, pre, pose, cost):
+def projection_pose(p, pre, pose, cost, rk=None):
     """ProjectionInputPose (update.py:102-124): pose broadcast to a constant map."""
     B, _, h, w = cost.shape
     pm = pose.reshape(B, 6, 1, 1).expand(B, 6, h, w)
-    cor = F.relu(_conv(p, pre + "convc2", F.relu(_conv(p, pre + "convc1", cost)), 1, 1))
-    pfm = F.relu(_conv(p, pre + "convp2", F.relu(_conv(p, pre + "convp1", pm, 1, 3)), 1, 1))
-    out = F.relu(_conv(p, pre + "convp", torch.cat([cor, pfm], 1), 1, 1))
+    cor = _branch(p, pre, cost, ("convc1", "convc2"), (0, 1), rk)
+    pfm = _branch(p, pre, pm, ("convp1", "convp2"), (3, 1), rk)
+    out = relu_site(_conv(p, pre + "convp", torch.cat([cor, pfm], 1), 1, 1), rk, pre + "convp")
     return torch.cat([out, pm], 1)
 
 
-def update_block_depth(p, pre, net, cost_fn, inv, ctx, S, scale):
-    """BasicUpdateBlockDepth.forward (update.py:155-173)."""
+def update_block_depth(p, pre, net, cost_fn, inv, ctx, S, scale, cells=None, it=0):
+    """BasicUpdateBlockDepth.forward (update.py:155-173).  cells/it: the ReLU
+    sites' call index is it * S + step (relu_site)."""
     invs, masks = [], []
-    for _ in range(S):
-        feat = projection_depth(p, pre + "encoder.", inv, cost_fn(scale(inv)))
+    for s in range(S):
+        rk = (cells, it * S + s, None)
+        feat = projection_depth(p, pre + "encoder.", inv, cost_fn(scale(inv)), rk)
         net = sep_conv_gru(p, pre + "depth_gru.", net, torch.cat([ctx, feat], 1))
-        inv = inv + depth_head(p, pre + "depth_head.", net)
+        inv = inv + depth_head(p, pre + "depth_head.", net, rk=rk)
         invs.append(inv)
-        masks.append(mask_head(p, pre + "mask.", net))
+        masks.append(mask_head(p, pre + "mask.", net, rk))
     return net, masks, invs
 
 
-def update_block_pose(p, pre, net, cost_fn, pose, ctx, S):
-    """BasicUpdateBlockPose.forward (update.py:184-199)."""
+def update_block_pose(p, pre, net, cost_fn, pose, ctx, S, cells=None, it=0, part=None):
+    """BasicUpdateBlockPose.forward (update.py:184-199).  part = (j, B): this
+    is reference view j (relu_site)."""
     seqs = []
-    for _ in range(S):
-        feat = projection_pose(p, pre + "encoder.", pose, cost_fn(pose))
+    for s in range(S):
+        rk = (cells, it * S + s, part)
+        feat = projection_pose(p, pre + "encoder.", pose, cost_fn(pose), rk)
         net = sep_conv_gru(p, pre + "pose_gru.", net, torch.cat([ctx, feat], 1))
-        pose = pose + pose_head(p, pre + "pose_head.", net)
+        pose = pose + pose_head(p, pre + "pose_head.", net, rk)
         seqs.append(pose)
     return net, seqs
 
@@ -531,17 +579,16 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
     B, N = image.shape[0], len(refs)
     fm = resnet_encoder(p, "fnet.", torch.cat([image] + refs, 0), training, cells=cells)
     fmap1, frefs = fm[:B], [fm[B * (j + 1):B * (j + 2)] for j in range(N)]
-    poses = [pose_head(p, "pose_head.", torch.cat([fmap1, f], 1)) for f in frefs]
-    inv = depth_head(p, "depth_head.", fmap1, torch.sigmoid)
-    up = convex_upsample(inv, 0.25 * _conv(p, "upmask_net.mask.2",
-                                            F.relu(_conv(p, "upmask_net.mask.0", fmap1, 1, 1))), 8)
+    poses = [pose_head(p, "pose_head.", torch.cat([fmap1, f], 1), (cells, 0, (j, B))) for j, f in enumerate(frefs)]
+    inv = depth_head(p, "depth_head.", fmap1, torch.sigmoid, (cells, 0, None))
+    up = convex_upsample(inv, mask_head(p, "upmask_net.mask.", fmap1, (cells, 0, None)), 8)
     inv_preds, pose_preds = [scale(up)], [[q.clone() for q in poses]]
     ctx_d = resnet_encoder(p, "cnet_depth.", image, training, cells=cells)
-    h_d, x_d = torch.tanh(ctx_d[:, :hd]), torch.relu(ctx_d[:, hd:hd + cd])
+    h_d, x_d = torch.tanh(ctx_d[:, :hd]), relu_site(ctx_d[:, hd:hd + cd], (cells, 0, None), "ctx_d")
     ctx_p = resnet_encoder(p, "cnet_pose.", torch.cat([torch.cat([image, r], 1) for r in refs], 0),
                            training, cells=cells)
     h_p = [torch.tanh(ctx_p[B * j:B * (j + 1), :hd]) for j in range(N)]
-    x_p = [torch.relu(ctx_p[B * j:B * (j + 1), hd:hd + cd]) for j in range(N)]
+    x_p = [relu_site(ctx_p[B * j:B * (j + 1), hd:hd + cd], (cells, 0, (j, B)), "ctx_p") for j in range(N)]
     for it in range(cfg["outer"]):
         inv = inv.detach()
         poses = [q.detach() for q in poses]
@@ -550,7 +597,7 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
         cost_d = lambda x, ps=poses, it=it, sd=sd: depth_cost_calc(x, fmap1, frefs, ps, K, K, 1.0 / 8, cells,
                                                                   ("depth", it, next(sd)))
         h_d, masks, invs = update_block_depth(p, "update_block_depth.", h_d, cost_d, inv, x_d, S,
-                                              scale)
+                                              scale, cells, it)
         sel = range(S) if cfg["inter"] else [S - 1]
         for k in sel:
             inv_preds.append(scale(convex_upsample(invs[k], masks[k], 8)))
@@ -561,7 +608,7 @@ def depth_pose_net(p, version, min_depth, max_depth, image, refs, K, training=Tr
             cost_p = lambda q, j=j, it=it, sp=sp: get_cost_each(q, fmap1, frefs[j], depth_fixed, K, K, 1.0 / 8,
                                                                 cells, ("pose", it, next(sp), j))
             h_p[j], seqs = update_block_pose(p, "update_block_pose.", h_p[j], cost_p, poses[j],
-                                             x_p[j], S)
+                                             x_p[j], S, cells, it, (j, B))
             new_poses.append(seqs if cfg["inter"] else [seqs[-1]])
         for k in range(len(new_poses[0])):
             pose_preds.append([new_poses[j][k].clone() for j in range(N)])

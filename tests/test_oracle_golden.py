@@ -449,3 +449,27 @@ def test_cells_from_calls_keys():
     assert out[("photo", 1, 2)].shape == (1, 6, 8)
     assert out[("maxpool", "fnet")].dtype == torch.int64
     assert int(out[("relu", "fnet.layer1.0.bn1")].sum()) == 24
+
+
+def test_relu_site_calls_and_views():
+    """Conv ReLU sites: the product's ("relu_seq", name) records become
+    ("relu", (name, n)) for the n-th call; oracle.relu_site takes view j's rows
+    of a stacked record and pins only near-kinks (SEQ_RELU_TOL)."""
+    import torch.nn.functional as F
+    m0 = torch.ones(4, 2, 3, 3, dtype=torch.uint8)             # [N*B = 2*2, C, h, w]
+    m1 = m0.clone()
+    m1[2, 1, 0, 0] = 0                                           # view j=1, row 0
+    out = O.cells_from_calls([(("relu_seq", "u.convc1"), m0), (("relu_seq", "u.convc1"), m1)])
+    assert set(out) == {("relu", ("u.convc1", 0)), ("relu", ("u.convc1", 1))}
+    book = O.Cells(forced=out)
+    v = torch.full((2, 2, 3, 3), 0.5, dtype=torch.float64)
+    v[0, 1, 0, 0] = 1e-9                                         # at the kink, positive
+    a = v.clone().requires_grad_(True)
+    O.relu_site(a, (book, 1, (1, 2)), "u.convc1").sum().backward()
+    assert a.grad[0, 1, 0, 0] == 0 and a.grad.sum() == v.numel() - 1
+    b = v.clone().requires_grad_(True)
+    O.relu_site(b, (book, 1, (0, 2)), "u.convc1").sum().backward()      # view 0: natural
+    c = v.clone().requires_grad_(True)
+    F.relu(c).sum().backward()
+    assert torch.equal(b.grad, c.grad)
+    assert torch.equal(O.relu_site(v, (None, 0, None), "x"), F.relu(v))

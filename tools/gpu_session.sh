@@ -53,6 +53,7 @@ for step in "$@"; do
     envr:*) kv=${step#envr:}; run "roof_${kv%%=*}_${kv#*=}" 300 env "$kv" python bench.py --roofline-only ;;
     envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     k:*) kk=${step#k:}; run "pytest_k_${kk//[^a-zA-Z0-9]/_}" 900 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider -k "$kk" ;;
+    ns:*) kk=${step#ns:}; run "pytest_ns_${kk//[^a-zA-Z0-9]/_}" 900 env DRO_NATIVE_STRIDED=1 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider -k "$kk" ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -u -m pytest "$f" -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
