@@ -78,17 +78,39 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   const size_t HW = (size_t)H * W;
   const long long P = (long long)a.g.B * HW;
   const int T = a.g.KH * KW;
-  const int nchunks = (K + kBK - 1) / kBK;
+  // Parity classes (stride-2 data gradient): din[c, 2Y+cy, 2X+cx] takes only
+  // the taps with (cy + PH - ty) and (cx + PW - tx) even -- ty = ty0 + 2 iy,
+  // tx = tx0 + 2 ix -- so the block's columns are the pixels of one class and
+  // its K runs over (class tap, channel): the exact FLOPs, where the masked
+  // form multiplies every tap of every pixel (3/4 of them by zero)
+  const bool pcl = MODE == 1 && a.pclass;
+  const int cy = pcl ? (int)(blockIdx.z >> 1) : 0, cx = pcl ? (int)(blockIdx.z & 1) : 0;
+  const int ty0 = pcl ? (cy + PH) & 1 : 0, tx0 = pcl ? (cx + PW) & 1 : 0;
+  const int ntx = pcl ? (KW - tx0 + 1) >> 1 : KW;
+  const int nty = pcl ? (a.g.KH - ty0 + 1) >> 1 : a.g.KH;
+  const int Hc = pcl ? (H - cy + 1) >> 1 : H, Wc = pcl ? (W - cx + 1) >> 1 : W;
+  const long long HWc = (long long)Hc * Wc, Pc = (long long)a.g.B * HWc;
+  const int Kc = pcl ? nty * ntx * kch : K;
+  auto real_tap = [&](int tc) {   // class tap -> tap of the kernel
+    if (!pcl) return tc;
+    const int iy = tc / ntx;
+    return (ty0 + 2 * iy) * KW + tx0 + 2 * (tc - iy * ntx);
+  };
+  const int nchunks = (Kc + kBK - 1) / kBK;
   const int cbeg = blockIdx.y * a.chunks_per_split;
   const int cend = min(nchunks, cbeg + a.chunks_per_split);
 
   // staging roles: X column (pixel) fixed; W k-lane fixed
   const int col = tid & 63, krow = tid >> 6;
   const long long pg = p0 + col;
-  const bool pv = pg < P;
-  const int pb = pv ? (int)(pg / (long long)HW) : 0;
-  const int prem = pv ? (int)(pg - (long long)pb * HW) : 0;
-  const int py = prem / W, px = prem - py * W;
+  const bool pv = pg < Pc;
+  const int pb = pv ? (int)(pg / HWc) : 0;
+  const int prem = pv ? (int)(pg - (long long)pb * HWc) : 0;
+  int py = prem / Wc, px = prem - py * Wc;
+  if (pcl) {
+    py = 2 * py + cy;
+    px = 2 * px + cx;
+  }
   const int wkl = tid & 31, wrow = tid >> 5;
 
   float xr[8], wv[BM / 8];
@@ -100,9 +122,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
     for (int i = 0; i < 8; ++i) {
       // row decode: wave-uniform (scalar)
       const int k = __builtin_amdgcn_readfirstlane(k0 + krow + 4 * i);
-      const bool kv = k < K;
+      const bool kv = k < Kc;
       const int kk = kv ? k : 0;
-      const int tap = fdiv(kk, kdiv), ch = kk - tap * kch;
+      const int tc = fdiv(kk, kdiv), ch = kk - tc * kch;
+      const int tap = real_tap(tc);
       const int ty = fdiv(tap, kwdiv), dy = ty - PH, dx = tap - ty * KW - PW;
       // per lane.  Stride 2^sh: the forward reads input (S*y + dy, S*x + dx);
       // the data gradient of input pixel y takes G at (y - dy) / S where exact
@@ -122,8 +145,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
       }
     }
     const int k = k0 + wkl;
-    const bool kv = k < K;
-    const int tap = kv ? fdiv(k, kdiv) : 0, ch = kv ? k - tap * kch : 0;
+    const bool kv = k < Kc;
+    const int tc = kv ? fdiv(k, kdiv) : 0, ch = kv ? k - tc * kch : 0;
+    const int tap = real_tap(tc);
     wmask = 0;
 #pragma unroll
     for (int i = 0; i < BM / 8; ++i) {
@@ -178,8 +202,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
   }
 
   const long long pe = p0 + wc * 32 + (lane & 31);
-  if (pe >= P) return;
-  if (a.part) {   // split-K partial: [split][rows][P]
+  if (pe >= Pc) return;
+  if (a.part) {   // split-K partial: [split][rows][P] (not with parity classes)
     float* dst = a.part + (size_t)blockIdx.y * rows * P + pe;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -188,8 +212,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
     }
     return;
   }
-  const int eb = (int)(pe / (long long)HW);
-  const size_t epix = (size_t)(pe - (long long)eb * HW);
+  const int eb = (int)(pe / HWc);
+  size_t epix = (size_t)(pe - (long long)eb * HWc);
+  if (pcl) {
+    const int Y = (int)(epix / (unsigned)Wc), X = (int)epix - Y * Wc;
+    epix = (size_t)(2 * Y + cy) * W + 2 * X + cx;
+  }
   epi_tile<MODE, ACT, EPI>(a, acc, row0 + wr * 32 + 4 * (lane >> 5), eb, epix, HW);
 }
 
@@ -2382,7 +2410,27 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
     d.gsrc_ctot[0] = Cin;
     d.gsrc_coff[0] = 0;
     d.gsrc_acc[0] = grad_x_accumulate ? 1 : 0;
-    if ((st = launch_igemm<1, 0, 0>(d, (long long)B * Hi * Wi, ws, s))) return st;
+    static const bool masked = env_int("DRO_STRIDED_MASKED", 0) != 0;   // A/B: the 4x-masked form
+    if (stride == 2 && !masked) {
+      // parity classes: grid.z = class, columns = that class's pixels (at most
+      // ceil(Hi/2) x ceil(Wi/2) per image), K = its taps x Cout; no K split
+      d.pclass = 1;
+      d.kdiv = make_fdiv(Cout);
+      d.K = Cout * KH * KW;
+      const long long Pc = (long long)B * ((Hi + 1) / 2) * ((Wi + 1) / 2);
+      const int ptiles = (int)((Pc + kBN - 1) / kBN);
+      const int bm = (long long)((Cin + 63) / 64) * ptiles * 4 >= 448 ? 64 : 32;
+      d.row_tiles = (Cin + bm - 1) / bm;
+      d.chunks_per_split = 1 << 30;
+      d.part = nullptr;
+      const dim3 grid((unsigned)(d.row_tiles * ptiles), 1, 4);
+      conv_logf(2.0 * Cin * Cout * KH * KW * (double)B * Ho * Wo, "igemm_kernel<%d, 1, 0, 0> parity classes", bm);
+      if (bm == 64) hipLaunchKernelGGL((igemm_kernel<64, 1, 0, 0>), grid, dim3(256), 0, s, d);
+      else hipLaunchKernelGGL((igemm_kernel<32, 1, 0, 0>), grid, dim3(256), 0, s, d);
+      if ((st = launch_status("igemm_kernel (parity classes) launch failed"))) return st;
+    } else if ((st = launch_igemm<1, 0, 0>(d, (long long)B * Hi * Wi, ws, s))) {
+      return st;
+    }
   }
   if (grad_weight) {
     const long long P = (long long)B * Ho * Wo;

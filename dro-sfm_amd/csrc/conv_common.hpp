@@ -101,6 +101,8 @@ struct IgArgs {
   // weight gradient, the output gradient for the data gradient), log2 stride
   int Hs, Ws, sshift;
   int flat_only;                // 1: the flattened implicit GEMM (no halo / thin / split-bf16 paths)
+  int pclass;                   // igemm data gradient, stride 2: output pixels by parity class
+                                // (blockIdx.z = 2 * (y & 1) + (x & 1)), only that class's taps
   unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
   int dbg;                      // diagnostics with stamps on (env DRO_CONV_DBG): 1 skip the K
                                 // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)

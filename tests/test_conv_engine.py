@@ -334,6 +334,9 @@ def test_weight_split_exact(hip):
     (1, 6, 64, 47, 81, 7, 2, 3, False, None),        # cnet_pose stem, odd input size
     (2, 20, 24, 17, 23, 3, 2, 1, True, "relu"),      # odd sizes, bias + relu forward
     (2, 16, 40, 12, 20, 3, 1, 0, True, None),        # stride 1, no padding
+    (2, 20, 24, 17, 23, 3, 2, 1, True, None),        # odd sizes: parity classes of unequal size
+    (3, 10, 12, 9, 7, 1, 2, 0, False, None),         # 1x1/s2, odd: three classes get no tap
+    (2, 5, 8, 10, 13, 4, 2, 1, False, None),         # even kernel: every class has 2x2 taps
     # the ScanNet view5 fixture's fnet (5 frames of 64x96)
     (5, 3, 64, 64, 96, 7, 2, 3, False, None),
     (5, 64, 128, 16, 24, 3, 2, 1, False, None),
