@@ -451,8 +451,8 @@ def main():
                          "starts from decoded uint8 KITTI raw frames (375x1242) in pinned host memory and "
                          "runs the data pipeline (H2D, resize, colour jitter, to_tensor) on the GPU "
                          "(datasets/gpu_loader.py) inside the timed region")
-    ap.add_argument("--native-strided-convs", action="store_true",
-                    help="A/B: the encoders' stride-2 convs on the HIP engine instead of MIOpen")
+    ap.add_argument("--miopen-strided-convs", action="store_true",
+                    help="A/B: the encoders' stride-2 convs on MIOpen instead of the HIP engine")
     ap.add_argument("--miopen-encoder-convs", action="store_true",
                     help="A/B: the encoders' stride-1 3x3 convolutions on MIOpen instead of the HIP engine")
     ap.add_argument("--roofline-only", action="store_true",
@@ -472,7 +472,7 @@ def main():
         return
     from dro_sfm_amd.networks.optim import extractor as _extractor
     _extractor.set_native_convs(not args.miopen_encoder_convs)
-    _extractor.set_native_strided_convs(args.native_strided_convs)
+    _extractor.set_native_strided_convs(not args.miopen_strided_convs)
 
     from dro_sfm_amd.trainers.dp_trainer import (DataParallelTrainer, GraphedTrainStep,
                                                   init_distributed)
@@ -547,7 +547,7 @@ def main():
                    "optimizer": "Adam lr 2e-4", "execution": mode,
                    "update_blocks": "depth block + pose block (side stream, with both context encoders)",
                    "encoder_3x3_s1": "miopen" if args.miopen_encoder_convs else "hip",
-                   "encoder_strided": "hip" if args.native_strided_convs else "miopen",
+                   "encoder_strided": "miopen" if args.miopen_strided_convs else "hip",
                    "exchange": ("none (world 1)" if world == 1 else
                                 "bucketed all-reduce in the step graph, overlapping backward"
                                 if getattr(stepper, "in_graph", False) else

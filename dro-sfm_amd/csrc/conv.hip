@@ -203,12 +203,13 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs a) {
 
   const long long pe = p0 + wc * 32 + (lane & 31);
   if (pe >= Pc) return;
-  if (a.part) {   // split-K partial: [split][rows][P] (not with parity classes)
-    float* dst = a.part + (size_t)blockIdx.y * rows * P + pe;
+  if (a.part) {   // split-K partial: [split][rows][P]; parity classes [split][class][rows][pcmax]
+    const long long PS = pcl ? a.pcmax : P;
+    float* dst = a.part + ((size_t)blockIdx.y * (pcl ? 4 : 1) + (pcl ? blockIdx.z : 0)) * rows * PS + pe;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = row0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < rows) dst[(size_t)row * P] = acc[r];
+      if (row < rows) dst[(size_t)row * PS] = acc[r];
     }
     return;
   }
@@ -617,9 +618,13 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
 // of 64.  Lane = pixel; wave w stages rows o0+16w.. and columns n0+16w.., so
 // every row / column decode is wave-uniform.  Writes per-split partials
 // [split][Cout][NK+1].
+// One LDS stage (33 KB, 4 blocks per CU) with the next chunk held in
+// registers: the double-buffered 66 KB allowed 2 blocks per CU, too few waves
+// to cover the gathers' latency (the stems' weight gradients ran at 18-23 TF/s).
 __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
-  __shared__ float Gs[2][kWP][64 + 1];
-  __shared__ float Xs[2][kWP][64 + 1];
+  constexpr int NB = 1;
+  __shared__ float Gs[NB][kWP][64 + 1];
+  __shared__ float Xs[NB][kWP][64 + 1];
   const int cb1 = a.cbase[1], cb2 = a.cbase[2], cb3 = a.cbase[3];
   const int H = a.g.H, W = a.g.W, KW = a.g.KW, PH = a.g.PH, PW = a.g.PW;
   const int Hsrc = a.Hs, Wsrc = a.Ws, sh = a.sshift;   // input size, log2 stride
@@ -696,9 +701,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(IgArgs a) {
       const int kk = s * 2 + (lane >> 5);
       acc = mfma32(Gs[buf][kk][wo * 32 + (lane & 31)], Xs[buf][kk][wc * 32 + (lane & 31)], acc);
     }
-    if (more) store(buf ^ 1);
+    if (NB == 1) __syncthreads();          // every wave is done reading the stage
+    if (more) store(NB == 1 ? 0 : buf ^ 1);
     __syncthreads();
-    buf ^= 1;
+    buf = NB == 1 ? 0 : buf ^ 1;
   }
   float* wp = a.part + (size_t)blockIdx.y * Cout * (NK + 1);
   const int n = n0 + wc * 32 + (lane & 31);
@@ -1431,9 +1437,10 @@ IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W) {
   pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
   const int nchunks = (kch * T + kBK - 1) / kBK;
   const long long blocks = (long long)pl.row_tiles * pl.ptiles;
+  static const long long below = env_int("DRO_FLAT_BELOW", 240), target = env_int("DRO_FLAT_TARGET", 480);
   int ks = 1;
-  if (blocks < 240) {
-    ks = (int)((480 + blocks - 1) / blocks);
+  if (blocks < below) {
+    ks = (int)((target + blocks - 1) / blocks);
     if (ks > 16) ks = 16;
     if (ks > nchunks / 4) ks = nchunks / 4;
     if (ks < 1) ks = 1;
@@ -1456,10 +1463,13 @@ WgPlan plan_wgrad(int Cin, int Cout, int T, long long P) {
   pl.otiles = (Cout + 63) / 64;
   pl.ntiles = (NK + 1 + 63) / 64;
   const long long tiles = (long long)pl.otiles * pl.ntiles;
-  long long splits = (640 + tiles - 1) / tiles;
+  // ~4 blocks per CU: the stems (3 or 6 input channels, 7x7: 3-5 column tiles
+  // over 10^5 pixels) got 192 blocks at the old 64-split cap and ran at 18 TF/s
+  static const long long target = env_int("DRO_WG_TARGET", 1024), cap = env_int("DRO_WG_MAXSPLIT", 256);
+  long long splits = (target + tiles - 1) / tiles;
   const long long maxs = (P + 2 * kWP - 1) / (2 * kWP);   // >= 2 chunks per split
   if (splits > maxs) splits = maxs;
-  if (splits > 64) splits = 64;
+  if (splits > cap) splits = cap;
   if (splits < 1) splits = 1;
   pl.pchunk = ((P + splits - 1) / splits + kWP - 1) / kWP * kWP;
   pl.splits = (int)((P + pl.pchunk - 1) / pl.pchunk);
@@ -2274,6 +2284,30 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   return DRO_OK;
 }
 
+// split-K partials of the parity-class data gradient, [split][class][rows][pcmax]
+// -> the strided input gradient (fixed split order: deterministic)
+__global__ __launch_bounds__(256) void igemm_class_finish_kernel(IgArgs a, int ksplit) {
+  const int H = a.g.H, W = a.g.W;
+  const size_t HW = (size_t)H * W;
+  const long long pcm = a.pcmax;
+  const long long per_class = (long long)a.rows * pcm, total = 4 * per_class;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int z = (int)(i / per_class);
+    const long long r = i - (long long)z * per_class;
+    const int row = (int)(r / pcm);
+    const long long pe = r - (long long)row * pcm;
+    const int cy = z >> 1, cx = z & 1;
+    const int Hc = (H - cy + 1) >> 1, Wc = (W - cx + 1) >> 1;
+    const long long HWc = (long long)Hc * Wc;
+    if (pe >= (long long)a.g.B * HWc) continue;
+    const float v = split_sum(a.part + i, (size_t)total, ksplit);
+    const int eb = (int)(pe / HWc);
+    const int q = (int)(pe - (long long)eb * HWc), Y = q / Wc, X = q - Y * Wc;
+    epi_store<1, 0, 0>(a, row, eb, (size_t)(2 * Y + cy) * W + 2 * X + cx, HW, v);
+  }
+}
+
 // ------------------------------------------------------------------ strided convolutions
 // The ResNet encoders' stride-2 convolutions (extractor.py:7-107 /
 // torchvision BasicBlock + stem): 7x7/s2 pad 3 stems, 3x3/s2 pad 1 stage
@@ -2334,13 +2368,44 @@ int strided_setup(IgArgs& a, const float* x, int B, int Hi, int Wi, int Cin, int
 }
 }  // namespace
 
+// parity-class data gradient plan (stride 2): tiles over the largest class,
+// K split over grid.y until ~4 blocks per CU
+struct ClassPlan {
+  int bm, row_tiles, ptiles, ksplit, chunks_per_split;
+  long long pcmax;
+  size_t part_bytes;
+};
+
+static ClassPlan plan_class_dgrad(int B, int Hi, int Wi, int Cin, int Cout, int KH, int KW) {
+  ClassPlan cp = {};
+  cp.pcmax = (long long)B * ((Hi + 1) / 2) * ((Wi + 1) / 2);
+  cp.ptiles = (int)((cp.pcmax + kBN - 1) / kBN);
+  cp.bm = (long long)((Cin + 63) / 64) * cp.ptiles * 4 >= 448 ? 64 : 32;
+  cp.row_tiles = (Cin + cp.bm - 1) / cp.bm;
+  const int nck = (((KH + 1) / 2) * ((KW + 1) / 2) * Cout + kBK - 1) / kBK;   // the largest class
+  const long long blocks = 4LL * cp.row_tiles * cp.ptiles;
+  static const long long target = env_int("DRO_CLASS_TARGET", 1024);
+  int ks = 1;
+  if (blocks < target) {
+    ks = (int)((target + blocks - 1) / blocks);
+    if (ks > 16) ks = 16;
+    if (ks > nck / 4) ks = nck / 4;      // >= 4 chunks per split
+    if (ks < 1) ks = 1;
+  }
+  cp.chunks_per_split = (nck + ks - 1) / ks;
+  cp.ksplit = (nck + cp.chunks_per_split - 1) / cp.chunks_per_split;
+  cp.part_bytes = cp.ksplit > 1 ? align256((size_t)cp.ksplit * 4 * Cin * cp.pcmax * sizeof(float)) : 0;
+  return cp;
+}
+
 extern "C" size_t dro_conv2d_strided_workspace_bytes(int B, int Hi, int Wi, int Cin, int Cout, int KH, int KW,
                                                      int stride, int pad) {
   if (stride < 1) return 0;
   const int Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
   if (Ho < 1 || Wo < 1) return 0;
   const size_t fwd = plan_igemm_flat(Cout, Cin, KH, KW, B, Ho, Wo).part_bytes;
-  const size_t dg = plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes;
+  const size_t dg = std::max(plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes,
+                             stride == 2 ? plan_class_dgrad(B, Hi, Wi, Cin, Cout, KH, KW).part_bytes : (size_t)0);
   const size_t wg = plan_wgrad(Cin, Cout, KH * KW, (long long)B * Ho * Wo).part_bytes;
   return std::max(fwd, align256(dg) + wg);
 }
@@ -2413,21 +2478,28 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
     static const bool masked = env_int("DRO_STRIDED_MASKED", 0) != 0;   // A/B: the 4x-masked form
     if (stride == 2 && !masked) {
       // parity classes: grid.z = class, columns = that class's pixels (at most
-      // ceil(Hi/2) x ceil(Wi/2) per image), K = its taps x Cout; no K split
+      // ceil(Hi/2) x ceil(Wi/2) per image), K = its taps x Cout, split over
+      // grid.y when the grid is short (partials + class-aware finish)
+      const ClassPlan cp = plan_class_dgrad(B, Hi, Wi, Cin, Cout, KH, KW);
       d.pclass = 1;
+      d.pcmax = cp.pcmax;
       d.kdiv = make_fdiv(Cout);
       d.K = Cout * KH * KW;
-      const long long Pc = (long long)B * ((Hi + 1) / 2) * ((Wi + 1) / 2);
-      const int ptiles = (int)((Pc + kBN - 1) / kBN);
-      const int bm = (long long)((Cin + 63) / 64) * ptiles * 4 >= 448 ? 64 : 32;
-      d.row_tiles = (Cin + bm - 1) / bm;
-      d.chunks_per_split = 1 << 30;
-      d.part = nullptr;
-      const dim3 grid((unsigned)(d.row_tiles * ptiles), 1, 4);
-      conv_logf(2.0 * Cin * Cout * KH * KW * (double)B * Ho * Wo, "igemm_kernel<%d, 1, 0, 0> parity classes", bm);
-      if (bm == 64) hipLaunchKernelGGL((igemm_kernel<64, 1, 0, 0>), grid, dim3(256), 0, s, d);
+      d.row_tiles = cp.row_tiles;
+      d.chunks_per_split = cp.chunks_per_split;
+      d.part = cp.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
+      const dim3 grid((unsigned)(cp.row_tiles * cp.ptiles), (unsigned)cp.ksplit, 4);
+      conv_logf(2.0 * Cin * Cout * KH * KW * (double)B * Ho * Wo, "igemm_kernel<%d, 1, 0, 0> parity classes", cp.bm);
+      if (cp.bm == 64) hipLaunchKernelGGL((igemm_kernel<64, 1, 0, 0>), grid, dim3(256), 0, s, d);
       else hipLaunchKernelGGL((igemm_kernel<32, 1, 0, 0>), grid, dim3(256), 0, s, d);
       if ((st = launch_status("igemm_kernel (parity classes) launch failed"))) return st;
+      if (cp.ksplit > 1) {
+        const long long total = 4LL * Cin * cp.pcmax;
+        long long blocks = (total + 255) / 256;
+        if (blocks > 2048) blocks = 2048;
+        hipLaunchKernelGGL(igemm_class_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d, cp.ksplit);
+        if ((st = launch_status("igemm_class_finish_kernel launch failed"))) return st;
+      }
     } else if ((st = launch_igemm<1, 0, 0>(d, (long long)B * Hi * Wi, ws, s))) {
       return st;
     }
@@ -2442,7 +2514,9 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
     a.K = Cin * T;
     a.otiles = pl.otiles;
     a.pchunk = pl.pchunk;
-    a.part = reinterpret_cast<float*>(ws + align256(plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes));
+    a.part = reinterpret_cast<float*>(
+        ws + align256(std::max(plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes,
+                               stride == 2 ? plan_class_dgrad(B, Hi, Wi, Cin, Cout, KH, KW).part_bytes : (size_t)0)));
     conv_log("wgrad_kernel(", 2.0 * Cout * Cin * T * (double)P);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits), dim3(256), 0,
                        s, a);

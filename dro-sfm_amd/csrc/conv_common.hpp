@@ -103,6 +103,7 @@ struct IgArgs {
   int flat_only;                // 1: the flattened implicit GEMM (no halo / thin / split-bf16 paths)
   int pclass;                   // igemm data gradient, stride 2: output pixels by parity class
                                 // (blockIdx.z = 2 * (y & 1) + (x & 1)), only that class's taps
+  long long pcmax;              // parity classes: pixels of the largest class (partials' row stride)
   unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
   int dbg;                      // diagnostics with stamps on (env DRO_CONV_DBG): 1 skip the K
                                 // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)

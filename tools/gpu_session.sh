@@ -31,11 +31,11 @@ for step in "$@"; do
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchab) run bench_a 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     benche) run bench_eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --eager ;;
-    benchns) run bench_native_strided 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --native-strided-convs ;;
+    benchms) run bench_miopen_strided 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --miopen-strided-convs ;;
     benchpipe) run bench_pipeline 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --pipeline gpu ;;
     dp2) run bench_dp2_gloo_onegpu 600 env DRO_DIST_BACKEND=gloo DRO_BENCH_DEVICE=0 python bench.py --gpus 2 --steps 10 --warmup 3 --no-roofline ;;
     prof) run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ;;
-    profns) run rocprof_ns 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profns" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --native-strided-convs ;;
+    profms) run rocprof_ms 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profms" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --miopen-strided-convs ;;
     roof) run roofline_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/roof" -o run -- python bench.py --roofline-only ;;
     roofonly) run roofonly 300 python bench.py --roofline-only ;;
     pmc) run pmc_fetch 600 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python bench.py --roofline-only &&
@@ -53,7 +53,7 @@ for step in "$@"; do
     envr:*) kv=${step#envr:}; run "roof_${kv%%=*}_${kv#*=}" 300 env "$kv" python bench.py --roofline-only ;;
     envb:*) kv=${step#envb:}; run "bench_${kv%%=*}" 600 env "$kv" python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
     k:*) kk=${step#k:}; run "pytest_k_${kk//[^a-zA-Z0-9]/_}" 900 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider -k "$kk" ;;
-    ns:*) kk=${step#ns:}; run "pytest_ns_${kk//[^a-zA-Z0-9]/_}" 900 env DRO_NATIVE_STRIDED=1 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider -k "$kk" ;;
+    ms:*) kk=${step#ms:}; run "pytest_ms_${kk//[^a-zA-Z0-9]/_}" 900 env DRO_NATIVE_STRIDED=0 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider -k "$kk" ;;
     t:*) f=${step#t:}; run "pytest_$(basename "$f" .py)" 900 python -u -m pytest "$f" -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
     py:*) f=${step#py:}; run "py_$(basename "$f" .py)" 600 python "$f" ;;
     *) echo "unknown step $step" ;;
