@@ -1437,7 +1437,7 @@ IgPlan plan_igemm_flat(int rows, int kch, int KH, int KW, int B, int H, int W) {
   pl.row_tiles = (rows + pl.bm - 1) / pl.bm;
   const int nchunks = (kch * T + kBK - 1) / kBK;
   const long long blocks = (long long)pl.row_tiles * pl.ptiles;
-  static const long long below = env_int("DRO_FLAT_BELOW", 240), target = env_int("DRO_FLAT_TARGET", 480);
+  static const long long below = env_int("DRO_FLAT_BELOW", 960), target = env_int("DRO_FLAT_TARGET", 480);
   int ks = 1;
   if (blocks < below) {
     ks = (int)((target + blocks - 1) / blocks);
