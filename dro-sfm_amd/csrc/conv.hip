@@ -1293,17 +1293,34 @@ __global__ __launch_bounds__(256) void wgrad_halo_finish_kernel(IgArgs a, int sp
 
 // dW[o][c][tap] = sum_s part[s][o][tap*Cin + c]; db[o] = sum_s part[s][o][NK].
 // Threads walk the partials in their (coalesced) [o][n] order.
+// Q lanes share an output element (lane group q sums the q-th contiguous
+// range of splits, the Q range sums meet in a fixed shuffle tree, as in
+// wgrad2_finish_kernel): with 240 splits one lane per element was a serial
+// 240-load chain per element (9 us at the stems' 9.5 K elements)
+template <int Q>
 __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits) {
+  constexpr int EPW = 64 / Q;
   const int Cin = a.g.Cin, T = a.g.KH * a.g.KW, NK = a.K, Cout = a.g.Cout;
   const int NC = a.gbias ? NK + 1 : NK;
   const long long total = (long long)Cout * NC;
   const size_t sstride = (size_t)Cout * (NK + 1);
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const int o = (int)(e / NC), n = (int)(e - (long long)o * NC);
+  const int lane = threadIdx.x & 63, q = lane / EPW, le = lane - q * EPW;
+  const int per = (splits + Q - 1) / Q;
+  const int s0 = min(splits, q * per), ns = min(splits, s0 + per) - s0;
+  const long long wstride = (long long)gridDim.x * (blockDim.x / 64) * EPW;
+  for (long long eb = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * EPW; eb < total;
+       eb += wstride) {
+    const long long e = eb + le;
+    const bool ok = e < total;
+    const int o = ok ? (int)(e / NC) : 0, n = ok ? (int)(e - (long long)o * NC) : 0;
     const size_t src = (size_t)o * (NK + 1) + n;
-    float v = 0.f;
-    v = split_sum(a.part + src, sstride, splits);
+    float v = ok ? split_sum(a.part + (size_t)s0 * sstride + src, sstride, ns) : 0.f;
+    if (Q >= 4) v += __shfl_xor(v, 2 * EPW);
+    if (Q >= 2) {
+      const float w = __shfl_xor(v, EPW);
+      v = q & 1 ? w + v : v + w;
+    }
+    if (!ok || q != 0) continue;
     if (n == NK) {
       a.gbias[o] = a.wacc ? a.gbias[o] + v : v;
     } else {
@@ -1312,6 +1329,16 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(IgArgs a, int splits)
       *d = a.wacc ? *d + v : v;
     }
   }
+}
+
+static void launch_wgrad_finish(const IgArgs& a, int splits, hipStream_t s) {
+  const long long total = (long long)a.g.Cout * (a.K + 1);
+  const int Q = splits >= 32 ? 4 : splits >= 8 ? 2 : 1;
+  long long blocks = (total * Q + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (Q == 4) hipLaunchKernelGGL(wgrad_finish_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
+  else if (Q == 2) hipLaunchKernelGGL(wgrad_finish_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
+  else hipLaunchKernelGGL(wgrad_finish_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
 }
 
 // G = alpha * dout * act'(y) (only when act != none or alpha != 1)
@@ -2275,10 +2302,7 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits),
                        dim3(256), 0, s, a);
     if ((st = launch_status("wgrad_kernel launch failed"))) return st;
-    const long long total = (long long)Cout * (a.K + 1);
-    long long blocks = (total + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pl.splits);
+    launch_wgrad_finish(a, pl.splits, s);
     if ((st = launch_status("wgrad_finish_kernel launch failed"))) return st;
   }
   return DRO_OK;
@@ -2521,10 +2545,7 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits), dim3(256), 0,
                        s, a);
     if ((st = launch_status("wgrad_kernel launch failed"))) return st;
-    const long long total = (long long)Cout * (a.K + 1);
-    long long blocks = (total + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pl.splits);
+    launch_wgrad_finish(a, pl.splits, s);
     if ((st = launch_status("wgrad_finish_kernel launch failed"))) return st;
   }
   return DRO_OK;
