@@ -542,22 +542,24 @@ def _(x, weight, bias, stride, pad, act):
 @torch.library.custom_op("dro::conv2d_strided_backward", mutates_args=("grad_x", "grad_weight", "grad_bias"))
 def _conv2d_strided_bwd_op(x: Tensor, weight: Tensor, grad_out: Tensor, stride: int, pad: int,
                            grad_x: Optional[Tensor], grad_weight: Optional[Tensor], grad_bias: Optional[Tensor],
-                           weight_accumulate: int) -> None:
-    """Data gradient into grad_x, weight (+ bias) gradient into grad_weight /
-    grad_bias (added when weight_accumulate); act none only."""
+                           weight_accumulate: int, grad_x_accumulate: int = 0) -> None:
+    """Data gradient into grad_x (added when grad_x_accumulate), weight (+ bias)
+    gradient into grad_weight / grad_bias (added when weight_accumulate); act
+    none only."""
     lib = _lib.load()
     B, Cin, Hi, Wi = x.shape
     Cout, _, KH, KW = weight.shape
     nws = int(lib.dro_conv2d_strided_workspace_bytes(B, Hi, Wi, Cin, Cout, KH, KW, stride, pad))
     ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
     check(lib.dro_conv2d_strided_backward(ptr(x.contiguous()), ptr(weight.contiguous()), ptr(grad_out.contiguous()),
-                                          B, Hi, Wi, Cin, Cout, KH, KW, stride, pad, ptr(grad_x), 0, ptr(grad_weight),
+                                          B, Hi, Wi, Cin, Cout, KH, KW, stride, pad, ptr(grad_x), int(grad_x_accumulate),
+                                          ptr(grad_weight),
                                           ptr(grad_bias), weight_accumulate, ptr(ws), nws, stream_of(grad_out)),
           "dro_conv2d_strided_backward")
 
 
 @_conv2d_strided_bwd_op.register_fake
-def _(x, weight, grad_out, stride, pad, grad_x, grad_weight, grad_bias, weight_accumulate):
+def _(x, weight, grad_out, stride, pad, grad_x, grad_weight, grad_bias, weight_accumulate, grad_x_accumulate=0):
     return None
 
 
@@ -568,6 +570,7 @@ def _conv2d_strided_setup(ctx, inputs, output):
     ctx.meta = (stride, pad, act, has_bias, x.requires_grad, weight.requires_grad,
                 has_bias and bias.requires_grad)
     ctx.direct = _direct_targets((weight,), (bias,) if has_bias else (), mark=False, in_setup=True)
+    ctx.xsink = _sink_of(x) if x.requires_grad else None
 
 
 def _conv2d_strided_backward(ctx, gout):
@@ -576,7 +579,13 @@ def _conv2d_strided_backward(ctx, gout):
     if act:
         raise RuntimeError("conv2d_strided: backward through a fused activation is not supported")
     Cout = weight.shape[0]
-    gx = torch.empty_like(x) if need_x else None
+    # an input with a gradient sink (a ResNet block's input: its stride-2 conv1
+    # and downsample both read it) is written / added in place and gets None
+    xacc = 0
+    if ctx.xsink is not None:
+        gx, xacc = ctx.xsink.target()
+    else:
+        gx = torch.empty_like(x) if need_x else None
     direct = ctx.direct
     if direct is not None:                 # in place into the trainer's flat .grad views
         gw, gb, wacc = direct[2], direct[3] if has_bias else None, 1
@@ -586,7 +595,9 @@ def _conv2d_strided_backward(ctx, gout):
         wacc = 0
     if gw is None and gb is not None:
         gw = torch.empty_like(weight)
-    torch.ops.dro.conv2d_strided_backward(x, weight, gout, stride, pad, gx, gw, gb, wacc)
+    torch.ops.dro.conv2d_strided_backward(x, weight, gout, stride, pad, gx, gw, gb, wacc, xacc)
+    if ctx.xsink is not None:
+        gx = None
     if direct is not None:
         return gx, None, None, None, None, None
     return gx, (gw if need_w else None), (gb if has_bias and need_b else None), None, None, None

@@ -1030,6 +1030,10 @@ class _BatchNormAct(torch.autograd.Function):
             ptr(smean), ptr(sinv), ptr(ws), nws, stream_of(x)), "dro_batchnorm_relu_forward")
         ctx.save_for_backward(x, y, weight, smean, sinv)
         ctx.relu, ctx.has_skip = int(relu), skip is not None
+        # a skip input with a gradient sink (a ResNet block's input, also read
+        # by the block's conv1): this backward runs before conv1's, so it writes
+        # the sink first -- straight into its buffer, no add launch
+        ctx.skipsink = _sink_of(skip) if skip is not None and skip.requires_grad else None
         ctx.affine = (weight is not None, bias is not None)
         return y
 
@@ -1043,13 +1047,16 @@ class _BatchNormAct(torch.autograd.Function):
         gw = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[0] else None
         gb = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.affine[1] else None
         gs = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
+        in_sink = gs is not None and ctx.skipsink is not None and not ctx.skipsink.written
+        if in_sink:
+            gs = ctx.skipsink.target()[0]
         nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
         ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
         check(lib.dro_batchnorm_relu_backward(
             ptr(gy), ptr(x), ptr(y), ptr(weight), ptr(smean), ptr(sinv), ctx.relu, N, C, H * W,
             ptr(gx), ptr(gw), ptr(gb), ptr(gs), ptr(ws), nws, stream_of(gy)),
             "dro_batchnorm_relu_backward")
-        return gx, gw, gb, gs, None, None, None, None, None, None
+        return gx, gw, gb, (None if in_sink else gs), None, None, None, None, None, None
 
 
 def batchnorm_act(x, bn, skip=None, relu=True):

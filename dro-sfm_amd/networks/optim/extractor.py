@@ -127,6 +127,9 @@ class BasicBlock(nn.Module):
                                             BatchNorm2d(cout))
 
     def forward(self, x):
+        # conv1, the skip (or the downsample) all read x: their input gradients
+        # meet in place in a sink (the skip's BN backward writes it first)
+        x = hip.grad_sink(x)
         y = self.bn1.act(conv3x3(self.conv1, x))
         if self.downsample is None:
             skip = x
