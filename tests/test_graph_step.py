@@ -191,23 +191,27 @@ def test_step_repeatable_with_native_encoders():
     state give gradients equal to fp32 atomics reordering (the warp-cost
     backward's scatter is the only atomic accumulation): every tensor within
     1e-5 of its max, the whole gradient within 1e-6 relative L2.  A missing
-    stream join or a race on a shared gradient sink would show here."""
+    stream join or a race on a shared gradient sink would show here.  The
+    forward has no atomics at all: the two losses are bitwise equal (round 4:
+    with MIOpen's stride-2 convolutions they were not)."""
     import dro_sfm_amd.networks.optim.extractor as ex
     batch = _batch()
     K0 = batch["intrinsics"].clone()
     prev = ex._NATIVE_STRIDED[0]
-    grads = []
+    grads, losses = [], []
     try:
         ex.set_native_strided_convs(True)
         for _ in range(2):
             m = _setup()
             batch["intrinsics"].copy_(K0)
             out = m(batch, flip=False)
+            losses.append(out["loss"].detach().clone())
             out["loss"].sum().backward()
             torch.cuda.synchronize()
             grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None})
     finally:
         ex.set_native_strided_convs(prev)
+    assert torch.equal(losses[0], losses[1]), (losses[0], losses[1])
     a, b = grads
     assert a.keys() == b.keys()
     for k in a:
