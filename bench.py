@@ -198,7 +198,8 @@ def _event_loop(fn, iters, device):
 
 def roofline_plane_sweep(device, D=64, B=2, C=128, iters=20):
     """D = 64 depth-hypothesis stress of configs[1]: one
-    plane_sweep_wide_kernel launch builds the cost volume [B, D, C, h, w] of D
+    plane_sweep_lds_kernel launch (plane_sweep_wide_kernel for shapes the LDS
+    kernel's 4-pixel vectors do not tile) builds the cost volume [B, D, C, h, w] of D
     fronto-parallel planes (disp = linspace(0, 1, D) through disp_to_depth) at
     the feature resolution.  Algorithmic bytes per launch: fmap + fmap_ref read
     once (2 * 4 * B*C*P) + the volume written once (4 * B*D*C*P)."""
@@ -217,7 +218,7 @@ def roofline_plane_sweep(device, D=64, B=2, C=128, iters=20):
     P = h * w
     nbytes = 2 * 4 * B * C * P + 4 * B * D * C * P
     achieved = nbytes / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": f"plane_sweep_wide_kernel (D={D}, B={B}, C={C}, {h}x{w})",
+    return {"bound": "hbm", "kernel": f"plane_sweep_lds_kernel (D={D}, B={B}, C={C}, {h}x{w})",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "algorithmic_bytes": int(nbytes), "avg_launch_us": round(ms * 1e3, 2), "launches": iters}
