@@ -1494,7 +1494,8 @@ WgPlan plan_wgrad(int Cin, int Cout, int T, long long P) {
   // over 10^5 pixels) got 192 blocks at the old 64-split cap and ran at 18 TF/s
   static const long long target = env_int("DRO_WG_TARGET", 1024), cap = env_int("DRO_WG_MAXSPLIT", 256);
   long long splits = (target + tiles - 1) / tiles;
-  const long long maxs = (P + 2 * kWP - 1) / (2 * kWP);   // >= 2 chunks per split
+  static const long long minch = env_int("DRO_WG_MINCHUNKS", 1);   // pixel chunks per split, at least
+  const long long maxs = (P + minch * kWP - 1) / (minch * kWP);
   if (splits > maxs) splits = maxs;
   if (splits > cap) splits = cap;
   if (splits < 1) splits = 1;
