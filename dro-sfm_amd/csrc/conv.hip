@@ -2312,25 +2312,21 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
 // split-K partials of the parity-class data gradient, [split][class][rows][pcmax]
 // -> the strided input gradient (fixed split order: deterministic)
 __global__ __launch_bounds__(256) void igemm_class_finish_kernel(IgArgs a, int ksplit) {
+  // grid (pixel blocks of the largest class, 4 * rows): class and row are
+  // block-uniform, 32-bit index arithmetic (4 * rows * pcmax < 2^31, checked
+  // by the launcher)
   const int H = a.g.H, W = a.g.W;
   const size_t HW = (size_t)H * W;
-  const long long pcm = a.pcmax;
-  const long long per_class = (long long)a.rows * pcm, total = 4 * per_class;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int z = (int)(i / per_class);
-    const long long r = i - (long long)z * per_class;
-    const int row = (int)(r / pcm);
-    const long long pe = r - (long long)row * pcm;
-    const int cy = z >> 1, cx = z & 1;
-    const int Hc = (H - cy + 1) >> 1, Wc = (W - cx + 1) >> 1;
-    const long long HWc = (long long)Hc * Wc;
-    if (pe >= (long long)a.g.B * HWc) continue;
-    const float v = split_sum(a.part + i, (size_t)total, ksplit);
-    const int eb = (int)(pe / HWc);
-    const int q = (int)(pe - (long long)eb * HWc), Y = q / Wc, X = q - Y * Wc;
-    epi_store<1, 0, 0>(a, row, eb, (size_t)(2 * Y + cy) * W + 2 * X + cx, HW, v);
-  }
+  const unsigned pcm = (unsigned)a.pcmax, rows = (unsigned)a.rows;
+  const unsigned zr = blockIdx.y, z = zr / rows, row = zr - z * rows;
+  const int cy = (int)(z >> 1), cx = (int)(z & 1);
+  const unsigned Hc = (unsigned)((H - cy + 1) >> 1), Wc = (unsigned)((W - cx + 1) >> 1), HWc = Hc * Wc;
+  const unsigned pe = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pe >= (unsigned)a.g.B * HWc) return;
+  const size_t total = (size_t)4 * rows * pcm;
+  const float v = split_sum(a.part + (size_t)zr * pcm + pe, total, ksplit);
+  const unsigned eb = pe / HWc, q = pe - eb * HWc, Y = q / Wc, X = q - Y * Wc;
+  epi_store<1, 0, 0>(a, (int)row, (int)eb, (size_t)(2 * Y + cy) * W + 2 * X + cx, HW, v);
 }
 
 // ------------------------------------------------------------------ strided convolutions
@@ -2519,10 +2515,8 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
       else hipLaunchKernelGGL((igemm_kernel<32, 1, 0, 0>), grid, dim3(256), 0, s, d);
       if ((st = launch_status("igemm_kernel (parity classes) launch failed"))) return st;
       if (cp.ksplit > 1) {
-        const long long total = 4LL * Cin * cp.pcmax;
-        long long blocks = (total + 255) / 256;
-        if (blocks > 2048) blocks = 2048;
-        hipLaunchKernelGGL(igemm_class_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d, cp.ksplit);
+        const dim3 fgrid((unsigned)((cp.pcmax + 255) / 256), (unsigned)(4 * Cin));
+        hipLaunchKernelGGL(igemm_class_finish_kernel, fgrid, dim3(256), 0, s, d, cp.ksplit);
         if ((st = launch_status("igemm_class_finish_kernel launch failed"))) return st;
       }
     } else if ((st = launch_igemm<1, 0, 0>(d, (long long)B * Hi * Wi, ws, s))) {

@@ -314,6 +314,15 @@ __global__ __launch_bounds__(256) void igemm_finish_kernel(IgArgs a, int ksplit)
   const long long P = (long long)a.g.B * HW;
   const long long total = (long long)a.rows * P;
   const long long stride = (long long)gridDim.x * blockDim.x;
+  if (total < (1LL << 31)) {   // 32-bit index arithmetic (a 64-bit division is ~4x the instructions)
+    const unsigned P32 = (unsigned)P, HW32 = (unsigned)HW;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)total; i += (unsigned)stride) {
+      const float v = split_sum(a.part + i, (size_t)total, ksplit);
+      const unsigned row = i / P32, p = i - row * P32, eb = p / HW32;
+      epi_store<MODE, ACT, EPI>(a, (int)row, (int)eb, (size_t)(p - eb * HW32), HW, v);
+    }
+    return;
+  }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     float v = 0.f;
     v = split_sum(a.part + i, (size_t)total, ksplit);
