@@ -7,11 +7,12 @@ upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  Pretrained ImageNet
 weights are never downloaded -- load a checkpoint instead.
 
 Training-mode batch normalisation runs fused with the ReLU / residual add that
-follows it (hip.batchnorm_act, csrc/batchnorm.hip: two launches each way with
-fixed-order fp64 statistics, against 6-9 PyTorch launches per site).  Not
-MIOpen's BN: measured on MI355X (tools/diag_miopen2.py), its one-pass
-variance put 1e-2 relative error on encoder gradients against the fp64
-oracle.  Eval mode and CPU tensors use PyTorch's native kernels.
+follows it (hip.batchnorm_act, csrc/batchnorm.hip: one launch each way where a
+channel fits one block, two otherwise, with fixed-order fp64 statistics,
+against 6-9 PyTorch launches per site).  Not MIOpen's BN: measured on MI355X
+in round 2, its one-pass variance put 1e-2 relative error on encoder gradients
+against the fp64 oracle.  Eval mode and CPU tensors use PyTorch's native
+kernels.
 The 2x bilinear upsampling of the fusion head is a HIP kernel
 (hip.bilinear_upsample2x): ATen's loops over all planes per output pixel.  So
 is the stem's 3x3/s2 max pooling (hip.maxpool3x3s2, bit-identical to
