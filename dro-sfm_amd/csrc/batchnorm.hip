@@ -334,7 +334,9 @@ __global__ __launch_bounds__(kFusedThreads) void bn_fused_bwd_kernel(BnBwdArgs a
     const long long q = e < L ? chan_off(e, c, g) : 0;
     const float d = a.dy[q], v = a.x[q], yy = ysrc[q];
     gv[k] = e < L ? grad_in(d, yy, a.relu) : 0.f;
-    xh[k] = (v - mean) * invstd;
+    // lanes past the channel read element 0 (in bounds) but must add nothing:
+    // 0 * xh would be NaN for an Inf/NaN x[0]
+    xh[k] = e < L ? (v - mean) * invstd : 0.f;
   }
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {

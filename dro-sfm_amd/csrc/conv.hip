@@ -2515,6 +2515,11 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
       else hipLaunchKernelGGL((igemm_kernel<32, 1, 0, 0>), grid, dim3(256), 0, s, d);
       if ((st = launch_status("igemm_kernel (parity classes) launch failed"))) return st;
       if (cp.ksplit > 1) {
+        // the finish indexes one split's [class][rows][pcmax] slab in 32 bits
+        if (4LL * Cin * (long long)cp.pcmax >= (1LL << 31)) {
+          set_error("conv2d_strided: data-gradient partial slab exceeds 32-bit indexing");
+          return DRO_E_SHAPE;
+        }
         const dim3 fgrid((unsigned)((cp.pcmax + 255) / 256), (unsigned)(4 * Cin));
         hipLaunchKernelGGL(igemm_class_finish_kernel, fgrid, dim3(256), 0, s, d, cp.ksplit);
         if ((st = launch_status("igemm_class_finish_kernel launch failed"))) return st;

@@ -2,8 +2,9 @@
 //
 // Replaces MultiViewPhotometricDecayLoss.forward
 // (dro_sfm/losses/multiview_photometric_loss_mf.py:303-361) for the
-// configuration every reference yaml uses (clip_loss 0, padding 'zeros',
-// full-resolution predictions): per (prediction i, ref j) view_synthesis
+// configuration every reference yaml uses (padding 'zeros', full-resolution
+// predictions) and clip_loss >= 0 (the reference constructor's default 0.5:
+// two forward passes around per-map thresholds, photo_clip_stats_kernel): per (prediction i, ref j) view_synthesis
 // (geometry/camera_utils.py:23-56), SSIM 3x3 with reflection padding (:15-54),
 // 0.85*SSIM + 0.15*L1 channel means (:194-229), automask (:346-351), min (or
 // mean) reduction over the 2N maps with 0.85^(n-i-1) decay (:231-269), and the
@@ -62,6 +63,13 @@ struct PhotoArgs {
   float* part_sm;   // [n,B,tiles,2]
   double* part_pose; // [N,n,B,tiles,12] fp64 (block_sum_d)
   int* cells;        // backward test hook: bilinear cell per (j, i, b, pixel) (pack_cell), or NULL
+  // clip_loss > 0 (multiview_photometric_loss_mf.py:223-227): every candidate
+  // map is clamped from above at float(mean + clip * std) of itself
+  float clip;
+  float* pm;         // clip: [N,n,B,HW] warped photometric maps (forward pass 1)
+  float* thr;        // clip: [N*n] warped + [N] unwarped clamp thresholds
+  signed char* l1s;  // backward test hook: sign of est - tgt per (j, i, b, c, pixel) the L1 term used
+                     // (1 / -1, 2 = zero), or NULL
 };
 
 __device__ __forceinline__ int reflect_idx(int y, int H) {
@@ -364,6 +372,13 @@ __device__ __forceinline__ void block_tile(const PhotoArgs& a, int& tile, int& p
 }
 
 // ------------------------------------------------------------------ forward tile kernel
+// MODE 0: the whole forward (clip_loss == 0).  With clip_loss > 0 the
+// thresholds depend on whole maps, so the forward runs in two passes around
+// photo_clip_stats_kernel: MODE 1 synthesises the warped maps and stores them
+// (pm), MODE 2 reads them back clamped (no second warp) and reduces as MODE 0.
+enum { kPhotoFull = 0, kPhotoStore = 1, kPhotoSelect = 2 };
+
+template <int MODE>
 __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
   constexpr int PL = H1 * W1;
   __shared__ float tgt[3 * PL];
@@ -404,15 +419,28 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
     float R[9], t[3];
     load_pose(a.pose + ((size_t)(j * a.n + i) * a.B + b) * ps, a.pose_mode, R, t);
     const float* ctx = a.context + ((size_t)j * a.B + b) * 3 * HW;
-    if (j) __syncthreads();  // previous j's readers are done with est
-    stage_warp<PL, W1, 1>(a, ctx, invt, ki, kr, R, t, x0, y0, est);
-    __syncthreads();
+    if (MODE != kPhotoSelect) {
+      if (j) __syncthreads();  // previous j's readers are done with est
+      stage_warp<PL, W1, 1>(a, ctx, invt, ki, kr, R, t, x0, y0, est);
+      __syncthreads();
+    }
+    float* pmj = MODE != kPhotoFull ? a.pm + ((size_t)(j * a.n + i) * a.B + b) * HW : nullptr;
 #pragma unroll
     for (int r = 0; r < kPxPerThread; ++r) {
       const int ly = threadIdx.x / TW + r * (kThreads / TW), lx = threadIdx.x % TW;
       if (y0 + ly >= H || x0 + lx >= W) continue;
       const int o = (ly + 1) * W1 + (lx + 1);
-      const float vw = photo_value(a, est, tgt, o, W1, PL);
+      const size_t gp = (size_t)(y0 + ly) * W + x0 + lx;
+      float vw;
+      if (MODE == kPhotoSelect) {
+        vw = fminf(pmj[gp], a.thr[j * a.n + i]);          // torch.clamp(max=...)
+      } else {
+        vw = photo_value(a, est, tgt, o, W1, PL);
+        if (MODE == kPhotoStore) {
+          pmj[gp] = vw;
+          continue;
+        }
+      }
       // candidate order of torch.cat(losses, 1): [warped_0, unwarped_0, warped_1, ...]
       const int kw = a.automask ? 2 * j : j;
       if (a.reduce_min) {
@@ -424,7 +452,8 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
         accm[r] += vw;
       }
       if (a.automask) {
-        const float vu = a.am[((size_t)j * a.B + b) * HW + (size_t)(y0 + ly) * W + x0 + lx];
+        float vu = a.am[((size_t)j * a.B + b) * HW + gp];
+        if (MODE == kPhotoSelect) vu = fminf(vu, a.thr[a.N * a.n + j]);
         if (a.reduce_min) {
           if (vu < best[r]) {
             best[r] = vu;
@@ -436,6 +465,7 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
       }
     }
   }
+  if (MODE == kPhotoStore) return;
 
   // selection map + tile partials of the reduced photometric map, the
   // smoothness sums (unnormalised: the mean of the inverse depth is a common
@@ -479,6 +509,43 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
     a.part_sm[((size_t)ib * tiles + tile) * 2 + 0] = v3[1];
     a.part_sm[((size_t)ib * tiles + tile) * 2 + 1] = v3[2];
     a.part_inv[(size_t)ib * tiles + tile] = v3[3];
+  }
+}
+
+// ------------------------------------------------------------------ clip thresholds (clip_loss > 0)
+// One block per candidate map (N*n warped from pm, then N unwarped from am):
+// mean and unbiased std over its B*H*W values in fp64 (two passes, fixed
+// reduction order), rounded to fp32, and the threshold formed in fp32 as the
+// reference does: float(mean + clip_loss * std) of fp32 tensors
+// (multiview_photometric_loss_mf.py:225-227; no fused multiply-add).
+__device__ __forceinline__ double block_sum_1d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void photo_clip_stats_kernel(PhotoArgs a) {
+  __shared__ double red[16];
+  const int m = blockIdx.x;
+  const size_t M = (size_t)a.B * a.H * a.W;
+  const float* src = m < a.N * a.n ? a.pm + (size_t)m * M : a.am + (size_t)(m - a.N * a.n) * M;
+  double s = 0.0;
+  for (size_t k = threadIdx.x; k < M; k += blockDim.x) s += src[k];
+  const double mean = block_sum_1d(s, red) / (double)M;
+  double q = 0.0;
+  for (size_t k = threadIdx.x; k < M; k += blockDim.x) {
+    const double d = (double)src[k] - mean;
+    q += d * d;
+  }
+  const double var = block_sum_1d(q, red) / (double)(M - 1);
+  if (threadIdx.x == 0) {
+    const float mean32 = (float)mean, std32 = (float)sqrt(var);
+    a.thr[m] = __fadd_rn(mean32, __fmul_rn(a.clip, std32));
   }
 }
 
@@ -542,6 +609,10 @@ __global__ __launch_bounds__(1024) void photo_finalize_kernel(PhotoArgs a, float
 }
 
 // ------------------------------------------------------------------ backward tile kernel
+// REC: the test hooks (bilinear cells, L1 signs) are compiled in; the
+// production instantiation carries neither (their address arithmetic costs
+// registers in a kernel at its 128-VGPR budget)
+template <bool REC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
                                                              float* __restrict__ ginv) {
   constexpr int PL2 = H2 * W2;  // est / tgt with 2-px halo
@@ -550,6 +621,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ float est[3 * PL2];
   __shared__ float adj[3 * PL1];  // one channel: dL/dmu_x, dL/dE[x^2], dL/dE[xy]
   __shared__ unsigned char selt[PL1];
+  __shared__ unsigned char ont[PL1];    // this ref's warped candidate passes a gradient at the pixel
   __shared__ float invt[PL2];
   __shared__ double dscratch[12 * (kThreads / kWave)];
 
@@ -605,12 +677,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     } else if (j) {
       __syncthreads();
     }
+    {
+      // per pixel of the tile + ring: does ref j's warped candidate pass a
+      // gradient -- selected (min) or in the image (mean), and with clip_loss
+      // not clamped (clamp(x, max=t)' = [x <= t])
+      const float* pmj = a.clip > 0.f ? a.pm + ((size_t)(j * a.n + i) * a.B + b) * HW : nullptr;
+      const float tj = a.clip > 0.f ? a.thr[j * a.n + i] : 0.f;
+      for (int k = threadIdx.x; k < PL1; k += kThreads) {
+        const int gy = y0 + k / W1 - 1, gx = x0 + k % W1 - 1;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        bool on = a.reduce_min ? selt[k] == kw : in;
+        if (pmj && on) on = pmj[(size_t)gy * W + gx] <= tj;
+        ont[k] = on;
+      }
+    }
     // (1) the warped tile and, from the same gathers, the bilinear derivative
     // terms of the thread's own pixels (the projection is recomputed for the
     // chain rule in (3))
     float dxc[kPxPerThread][3], dyc[kPxPerThread][3];
     stage_warp_bwd(a, ctx, invt, ki, kr, R, t, x0, y0, est, dxc, dyc,
-                   a.cells ? a.cells + ((size_t)(j * a.n + i) * a.B + b) * HW : nullptr);
+                   REC && a.cells ? a.cells + ((size_t)(j * a.n + i) * a.B + b) * HW : nullptr);
     __syncthreads();
     float gix[kPxPerThread], giy[kPxPerThread];
 #pragma unroll
@@ -624,8 +710,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       // adjoint of the SSIM term of channel c at every real pixel of the tile + 1-px ring
       for (int k = threadIdx.x; k < PL1; k += kThreads) {
         const int ly = k / W1, lx = k % W1;
-        const bool on = a.reduce_min ? (selt[k] == kw) : (y0 + ly - 1 >= 0 && y0 + ly - 1 < H &&
-                                                          x0 + lx - 1 >= 0 && x0 + lx - 1 < W);
+        const bool on = ont[k];
         const int o2 = (ly + 1) * W2 + (lx + 1);
         float A = 0.f, Bv = 0.f, Cv = 0.f;
         if (on) {
@@ -694,10 +779,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         }
         const float xv = est[c * PL2 + o2], yv = tgt[c * PL2 + o2];
         float ge = (s0 + 2.f * xv * s1 + yv * s2) * (1.f / 9.f);
-        if (a.reduce_min ? (selt[o1] == kw) : true) {
+        if (ont[o1]) {
           const float df = xv - yv;
           const float sg = df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f);
           ge += gsel * (a.l1_w / 3.f) * sg;
+          if (REC && a.l1s)
+            a.l1s[(((size_t)(j * a.n + i) * a.B + b) * 3 + c) * HW + (size_t)gy * W + gx] =
+                (signed char)(df > 0.f ? 1 : (df < 0.f ? -1 : 2));
         }
         // (3a) chain through the bilinear sample, channel by channel
         gix[r] += ge * dxc[r][c];
@@ -771,10 +859,10 @@ using namespace dro;
 
 namespace {
 struct PhotoLayout {
-  size_t sel, am, part_inv, mean, U, part_ph, part_sm, part_pose, total;
+  size_t sel, am, part_inv, mean, U, part_ph, part_sm, part_pose, pm, thr, total;
 };
 
-PhotoLayout photo_layout(int B, int N, int n, int H, int W) {
+PhotoLayout photo_layout(int B, int N, int n, int H, int W, bool clip) {
   const size_t HW = (size_t)H * W;
   const size_t tiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -796,6 +884,10 @@ PhotoLayout photo_layout(int B, int N, int n, int H, int W) {
   off = al(off + sizeof(float) * n * B * tiles * 2);
   L.part_pose = off;
   off = al(off + sizeof(double) * N * n * B * tiles * 12);
+  L.pm = off;
+  if (clip) off = al(off + sizeof(float) * N * n * B * HW);
+  L.thr = off;
+  if (clip) off = al(off + sizeof(float) * (N * n + N));
   L.total = off;
   return L;
 }
@@ -803,7 +895,7 @@ PhotoLayout photo_layout(int B, int N, int n, int H, int W) {
 int photo_setup(PhotoArgs& a, const float* image, const float* context, const float* inv_depths,
                 const float* K, const float* ref_K, const float* pose, int pose_mode, int B, int N,
                 int n, int H, int W, float ssim_w, float C1, float C2, float smooth_w,
-                int automask, int reduce_min, void* workspace) {
+                int automask, int reduce_min, float clip_loss, void* workspace) {
   if (!image || !context || !inv_depths || !K || !ref_K || !pose || !workspace) {
     set_error("photometric: NULL pointer argument");
     return DRO_E_NULL;
@@ -820,7 +912,12 @@ int photo_setup(PhotoArgs& a, const float* image, const float* context, const fl
     set_error("photometric: automask requires the min reduction (multiview_photometric_loss_mf.py:117-119)");
     return DRO_E_MODE;
   }
-  PhotoLayout L = photo_layout(B, N, n, H, W);
+  if (!(clip_loss == clip_loss)) {
+    set_error("photometric: clip_loss is NaN");
+    return DRO_E_MODE;
+  }
+  const bool clip = clip_loss > 0.f;     // the reference clips only for clip_loss > 0 (:223)
+  PhotoLayout L = photo_layout(B, N, n, H, W, clip);
   char* ws = (char*)workspace;
   a.image = image;
   a.context = context;
@@ -852,23 +949,32 @@ int photo_setup(PhotoArgs& a, const float* image, const float* context, const fl
   a.part_sm = (float*)(ws + L.part_sm);
   a.part_pose = (double*)(ws + L.part_pose);
   a.cells = nullptr;
+  a.clip = clip ? clip_loss : 0.f;
+  a.pm = clip ? (float*)(ws + L.pm) : nullptr;
+  a.thr = clip ? (float*)(ws + L.thr) : nullptr;
+  a.l1s = nullptr;
   return DRO_OK;
 }
 }  // namespace
 
-extern "C" size_t dro_photometric_workspace_bytes(int B, int N, int n, int H, int W) {
-  return photo_layout(B, N, n, H, W).total;
+extern "C" size_t dro_photometric_workspace_bytes(int B, int N, int n, int H, int W, float clip_loss) {
+  return photo_layout(B, N, n, H, W, clip_loss > 0.f).total;
+}
+
+extern "C" size_t dro_photometric_clip_offset(int B, int N, int n, int H, int W, int which) {
+  const PhotoLayout L = photo_layout(B, N, n, H, W, true);
+  return which ? L.thr : L.pm;
 }
 
 extern "C" int dro_photometric_forward(const float* image, const float* context,
                                        const float* inv_depths, const float* K, const float* ref_K,
                                        const float* pose, int pose_mode, int B, int N, int n, int H,
                                        int W, float ssim_w, float C1, float C2, float smooth_w,
-                                       int automask, int reduce_min, float* out, void* workspace,
-                                       void* stream) {
+                                       int automask, int reduce_min, float clip_loss, float* out,
+                                       void* workspace, void* stream) {
   PhotoArgs a;
   int st = photo_setup(a, image, context, inv_depths, K, ref_K, pose, pose_mode, B, N, n, H, W,
-                       ssim_w, C1, C2, smooth_w, automask, reduce_min, workspace);
+                       ssim_w, C1, C2, smooth_w, automask, reduce_min, clip_loss, workspace);
   if (st) return st;
   if (!out) {
     set_error("photometric_forward: NULL out");
@@ -879,7 +985,16 @@ extern "C" int dro_photometric_forward(const float* image, const float* context,
     hipLaunchKernelGGL(photo_automask_kernel, dim3(a.tiles_x, a.tiles_y, N * B), dim3(kThreads), 0, s, a);
     if ((st = launch_status("photo_automask_kernel launch failed"))) return st;
   }
-  hipLaunchKernelGGL(photo_fwd_kernel, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a);
+  const dim3 tgrid(a.tiles_x * a.tiles_y * n * B);
+  if (a.clip > 0.f) {
+    hipLaunchKernelGGL(photo_fwd_kernel<kPhotoStore>, tgrid, dim3(kThreads), 0, s, a);
+    if ((st = launch_status("photo_fwd_kernel (store) launch failed"))) return st;
+    hipLaunchKernelGGL(photo_clip_stats_kernel, dim3(N * n + (automask ? N : 0)), dim3(1024), 0, s, a);
+    if ((st = launch_status("photo_clip_stats_kernel launch failed"))) return st;
+    hipLaunchKernelGGL(photo_fwd_kernel<kPhotoSelect>, tgrid, dim3(kThreads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(photo_fwd_kernel<kPhotoFull>, tgrid, dim3(kThreads), 0, s, a);
+  }
   if ((st = launch_status("photo_fwd_kernel launch failed"))) return st;
   hipLaunchKernelGGL(photo_finalize_kernel, dim3(1), dim3(1024), 0, s, a, out);
   return launch_status("photo_finalize_kernel launch failed");
@@ -890,11 +1005,12 @@ extern "C" int dro_photometric_backward(const float* image, const float* context
                                         const float* ref_K, const float* pose, int pose_mode,
                                         int B, int N, int n, int H, int W, float ssim_w, float C1,
                                         float C2, float smooth_w, int automask, int reduce_min,
-                                        const float* grad_out, float* grad_inv_depths,
-                                        float* grad_pose, void* workspace, int* cells, void* stream) {
+                                        float clip_loss, const float* grad_out, float* grad_inv_depths,
+                                        float* grad_pose, void* workspace, int* cells,
+                                        signed char* l1_signs, void* stream) {
   PhotoArgs a;
   int st = photo_setup(a, image, context, inv_depths, K, ref_K, pose, pose_mode, B, N, n, H, W,
-                       ssim_w, C1, C2, smooth_w, automask, reduce_min, workspace);
+                       ssim_w, C1, C2, smooth_w, automask, reduce_min, clip_loss, workspace);
   if (st) return st;
   if (!grad_out || !grad_inv_depths) {
     set_error("photometric_backward: NULL grad_out/grad_inv_depths");
@@ -902,8 +1018,13 @@ extern "C" int dro_photometric_backward(const float* image, const float* context
   }
   if (!grad_pose) a.part_pose = nullptr;
   a.cells = cells;
+  a.l1s = l1_signs;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(photo_bwd_kernel, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a,
+  if (cells || l1_signs)
+    hipLaunchKernelGGL(photo_bwd_kernel<true>, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a,
+                       grad_out, grad_inv_depths);
+  else
+    hipLaunchKernelGGL(photo_bwd_kernel<false>, dim3(a.tiles_x * a.tiles_y * n * B), dim3(kThreads), 0, s, a,
                      grad_out, grad_inv_depths);
   if ((st = launch_status("photo_bwd_kernel launch failed"))) return st;
   if (grad_pose) {

@@ -43,6 +43,8 @@ struct WarpArgs {
   int reduce_mean;
   int acc_fmap;      // backward: add into grad_fmap
   int* cells;        // backward test hook: bilinear cell per (n, b, p) (pack_cell), or NULL
+  int merge;         // backward: merge runs of lanes sharing a cell before the scatter (default 1;
+                     // DRO_WARP_NOMERGE=1 for A/B measurements)
 };
 
 __device__ __forceinline__ void cams(const WarpArgs& a, int b, float ki[9], float kr[9]) {
@@ -178,8 +180,40 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
     float* gr = gfref ? gfref + (((size_t)n * a.B + b) * a.C + cb) * P : nullptr;
     const float omy = 1.f - T.ty, omx = 1.f - T.tx;
     float gix = 0.f, giy = 0.f;
+    // Scatter contention: where the warp compresses the image (consecutive
+    // pixels of the wave sampling one cell of the reference), up to 64 lanes'
+    // atomics hit the same four addresses and serialise in L2 (measured: the
+    // same launch 8 -> 69 us with the state of the network).  Lanes are
+    // consecutive pixels, so lanes sharing a cell form runs: when the wave has
+    // any, each run's contributions are summed by a segmented suffix scan
+    // over the lanes and only the run's first lane issues the atomics.
+    const bool taps_in = T.ok[0] || T.ok[1] || T.ok[2] || T.ok[3];
+    // the cell (floor ix, floor iy) in [-1, w-1] x [-1, h-1] when any tap is in
+    // the image; T.idx[0] alone is not unique there: cell (-1, y+1) and cell
+    // (w-1, y) share it, and a row's last and the next row's first pixel are
+    // neighbouring lanes that hit exactly that pair at the image's side borders
+    const int key = (taps_in && cn > 0)
+                        ? ((int)floorf(q.iy) + 1) * (a.w + 1) + (int)floorf(q.ix) + 1 : -(lane + 1);
+    const int key_next = __shfl_down(key, 1, kWave);
+    const int key_prev = __shfl_up(key, 1, kWave);
+    const bool run_cont = lane < kWave - 1 && key_next == key;    // the run goes on past this lane
+    const bool merge = a.merge && gr != nullptr && __any(run_cont);
+    const bool head = lane == 0 || key_prev != key;
+    unsigned addm = 0u;                                            // scan steps that add the next partial
+    if (merge) {
+      bool e = !run_cont;
+#pragma unroll
+      for (int s_ = 0; s_ < 6; ++s_) {
+        const bool en = __shfl_down((int)e, 1 << s_, kWave) != 0;
+        if (!e) {
+          addm |= 1u << s_;
+          e = en;
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < kCPT; ++c) {
+      float gw = 0.f;
       if (c < cn) {
         const float* pl = fr + (size_t)c * P;
         const float v0 = T.ok[0] ? pl[T.idx[0]] : 0.f;
@@ -189,8 +223,8 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
         const float val = v0 * T.wgt[0] + v1 * T.wgt[1] + v2 * T.wgt[2] + v3 * T.wgt[3];
         const float gd = SAMPLE ? 0.f : 2.f * (f[c] - val) * g[c];  // d cost / d fmap
         gf[c] += gd;
-        const float gw = SAMPLE ? g[c] : -gd;         // d loss / d warped
-        if (gr) {
+        gw = SAMPLE ? g[c] : -gd;                     // d loss / d warped
+        if (gr && !merge) {
           float* gpl = gr + (size_t)c * P;
           if (T.ok[0]) atomicAdd(gpl + T.idx[0], gw * T.wgt[0]);
           if (T.ok[1]) atomicAdd(gpl + T.idx[1], gw * T.wgt[1]);
@@ -199,6 +233,25 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
         }
         gix += gw * ((v1 - v0) * omy + (v3 - v2) * T.ty);
         giy += gw * ((v2 - v0) * omx + (v3 - v1) * T.tx);
+      }
+      if (merge) {                                    // wave-uniform: every lane shuffles
+        float w4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w4[q] = gw * T.wgt[q];
+#pragma unroll
+        for (int s_ = 0; s_ < 6; ++s_) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float o = __shfl_down(w4[q], 1 << s_, kWave);
+            if (addm & (1u << s_)) w4[q] += o;
+          }
+        }
+        if (head && c < cn) {
+          float* gpl = gr + (size_t)c * P;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (T.ok[q]) atomicAdd(gpl + T.idx[q], w4[q]);
+        }
       }
     }
     if (gxy) {
@@ -561,6 +614,8 @@ static int warp_backward(WarpArgs a, const float* grad_out, float* grad_fmap, fl
   int st;
   a.acc_fmap = accumulate & 1;
   a.cells = cells;
+  static const int nomerge = env_int("DRO_WARP_NOMERGE", 0);
+  a.merge = nomerge ? 0 : 1;
   const int P = h * w;
   float* gxy = geo ? (float*)workspace : nullptr;
   const int nblk = (P + kGeoThreads - 1) / kGeoThreads;

@@ -45,11 +45,12 @@ def load():
     _sig(lib.dro_view_synthesis_forward, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, P, S)
     _sig(lib.dro_view_synthesis_backward, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, P, P, P, P, P, P, S)
     _sig(lib.dro_plane_sweep_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, P, S)
-    _sig(lib.dro_photometric_workspace_bytes, I, I, I, I, I, restype=Z)
-    _sig(lib.dro_photometric_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I,
+    _sig(lib.dro_photometric_workspace_bytes, I, I, I, I, I, F, restype=Z)
+    _sig(lib.dro_photometric_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I, F,
          P, P, S)
-    _sig(lib.dro_photometric_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I,
-         P, P, P, P, P, S)
+    _sig(lib.dro_photometric_clip_offset, I, I, I, I, I, I, restype=Z)
+    _sig(lib.dro_photometric_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, F, F, I, I, F,
+         P, P, P, P, P, P, S)
     _sig(lib.dro_supervised_workspace_bytes, I, I, I, I, I, restype=Z)
     _sig(lib.dro_supervised_forward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, S)
     _sig(lib.dro_supervised_backward, P, P, P, P, P, P, I, I, I, I, I, I, F, F, P, P, P, P, S)
@@ -107,7 +108,7 @@ EXPORTED = (
     "dro_warp_cost_forward", "dro_warp_cost_workspace_bytes", "dro_warp_cost_backward",
     "dro_view_synthesis_forward", "dro_view_synthesis_backward",
     "dro_plane_sweep_forward",
-    "dro_photometric_workspace_bytes", "dro_photometric_forward", "dro_photometric_backward",
+    "dro_photometric_workspace_bytes", "dro_photometric_clip_offset", "dro_photometric_forward", "dro_photometric_backward",
     "dro_supervised_workspace_bytes", "dro_supervised_forward", "dro_supervised_backward",
     "dro_convex_upsample_forward", "dro_convex_upsample_backward",
     "dro_convex_upsample_many_forward", "dro_convex_upsample_many_workspace_bytes",

@@ -153,6 +153,18 @@ def _wsplit(weight):
     return ent[1], ent[2]
 
 
+def _wsplit_bwd(weight):
+    """The backward split copy `_wsplit` made for this weight in the forward
+    (a cache lookup: no launch), or None -- the backward then runs the f32
+    engine.  setup_context reads it here instead of from the forward's
+    side channel (a module-global hand-off breaks when tracing
+    runs a setup without its implementation)."""
+    if not _XCONV[0] or _XPOLICY[0] == "3x3fwd" or not weight.is_contiguous():
+        return None
+    ent = _SPLITS.get((weight.data_ptr(), tuple(weight.shape), weight.device))
+    return ent[2] if ent is not None and ent[0] == _GEN[0] else None
+
+
 def current_scope():
     return _SCOPE[0]
 
@@ -357,7 +369,6 @@ def _dense_out(srcs, C):
 
 
 Tensor = torch.Tensor
-_LAST_WSPLIT = []   # split-bf16 backward copy of the weight a forward op made (xconv engine), for its setup
 
 
 def _placeholder(t, device):
@@ -426,7 +437,6 @@ def _conv2d_op(srcs: list[Tensor], weight: Tensor, bias: Optional[Tensor], act: 
     check(lib.dro_conv2d_forward(_slices(srcs), len(srcs), ptr(weight), ptr(bias), B, H, W, Cout, KH, KW, act,
                                  ctypes.c_float(alpha), ptr(out), Cout, 0, ptr(wf), ptr(ws), nws, stream_of(out)),
           "dro_conv2d_forward")
-    _LAST_WSPLIT[:] = [wb]
     return out
 
 
@@ -438,7 +448,7 @@ def _(srcs, weight, bias, act, alpha, params, nweight):
 
 def _conv2d_setup(ctx, inputs, output):
     srcs, weight, bias, act, alpha, params, nweight = inputs
-    ctx.wsplit = _LAST_WSPLIT.pop() if _LAST_WSPLIT else None
+    ctx.wsplit = _wsplit_bwd(weight)
     ctx.save_for_backward(weight.contiguous(), output if act else None, *srcs)
     ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in srcs]
     ctx.need_src = [x.requires_grad for x in srcs]
@@ -671,7 +681,6 @@ def _sepgru_op(h: Tensor, wz: Tensor, bz: Tensor, wr: Tensor, br: Tensor, wq: Te
                                         B, H, W, hd, KH, KW, ctypes.byref(z_sl), ctypes.byref(h_sl),
                                         ptr(q), ptr(hn), hd, 0, ptr(qf), ptr(wsq), nwsq, st),
           "dro_convgru_blend_forward")
-    _LAST_WSPLIT[:] = [(zb, qb, wzr)]
     return hn, zr, rh, q
 
 
@@ -684,8 +693,10 @@ def _(h, wz, bz, wr, br, wq, bq, xs, wzr, bzr):
 def _sepgru_setup(ctx, inputs, output):
     h, wz, bz, wr, br, wq, bq, xs, wzr_in, bzr_in = inputs
     hn, zr, rh, q = output
-    zb, qb, wzr = _LAST_WSPLIT.pop()
-    ctx.wsplit = (zb, qb)
+    # the fused z|r weight the implementation ran with (sepconvgru_half always
+    # passes one; a direct op call without it gets the same concatenation)
+    wzr = wzr_in if wzr_in is not None else torch.cat([wz, wr], 0).detach().contiguous()
+    ctx.wsplit = (_wsplit_bwd(wzr), _wsplit_bwd(wq.contiguous()))
     ctx.save_for_backward(h.contiguous(), rh, wzr, wq.contiguous(), zr, q, *xs)
     ctx.mark_non_differentiable(zr, rh, q)
     ctx.set_materialize_grads(False)     # no zero-filled gradients for the three saved outputs
@@ -764,15 +775,16 @@ def sepconvgru_half(h, convz, convr, convq, xs):
             direct = ((zr[0], zr[1]), (zr[2], zr[3]), (qd[2], qd[3]))
             _mark_direct([convz.weight, convz.bias, convr.weight, convr.bias, convq.weight, convq.bias])
     scope = current_scope()
-    wzr = bzr = None
     if direct is not None:
         wzr, bzr = direct[0]
-    elif scope is not None:
+    else:
         key = ("zr", convz.weight.data_ptr(), convr.weight.data_ptr())
-        ent = scope.cats.get(key)
+        ent = scope.cats.get(key) if scope is not None else None
         if ent is None:
-            ent = scope.cats[key] = (torch.cat([convz.weight, convr.weight], 0).detach().contiguous(),
-                                     torch.cat([convz.bias, convr.bias], 0).detach().contiguous())
+            ent = (torch.cat([convz.weight, convr.weight], 0).detach().contiguous(),
+                   torch.cat([convz.bias, convr.bias], 0).detach().contiguous())
+            if scope is not None:
+                scope.cats[key] = ent
         wzr, bzr = ent
     _SEPGRU_DIRECT[:] = [direct] if direct is not None else []
     try:

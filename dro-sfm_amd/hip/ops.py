@@ -127,8 +127,8 @@ class CellRecord:
     def __init__(self):
         self.calls = []
 
-    def new(self, tag, shape, device):
-        cells = torch.full(shape, -1, dtype=torch.int32, device=device)
+    def new(self, tag, shape, device, dtype=torch.int32, fill=-1):
+        cells = torch.full(shape, fill, dtype=dtype, device=device)
         self.calls.append((tag, cells))
         return cells
 
@@ -166,12 +166,12 @@ def record_relu(y, mod):
     return y
 
 
-def _new_cells(tag, shape, device, *inputs):
+def _new_cells(tag, shape, device, *inputs, dtype=torch.int32, fill=-1):
     """A cell map (-1 filled) when recording and a backward will run."""
     rec = _CELLS[0]
     if rec is None or not torch.is_grad_enabled() or not any(t is not None and t.requires_grad for t in inputs):
         return None
-    return rec.new(tag, shape, device)
+    return rec.new(tag, shape, device, dtype, fill)
 
 
 def _opt(t):
@@ -462,38 +462,43 @@ def plane_sweep_cost(fmap, fmap_ref, disp, pose, K, ref_K=None, *, min_depth, ma
 @torch.library.custom_op("dro::photometric_loss", mutates_args=())
 def _photometric_op(image: Tensor, context: Tensor, inv_depths: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
                     pose_mode: int, ssim_w: float, C1: float, C2: float, smooth_w: float, automask: bool,
-                    reduce_min: bool, cells: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor]:
+                    reduce_min: bool, clip_loss: float, cells: Optional[Tensor],
+                    l1_signs: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor]:
     """MultiViewPhotometricDecayLoss (multiview_photometric_loss_mf.py:303-361):
     image [B,3,H,W], context [N,B,3,H,W], inv_depths [n,B,1,H,W], pose
     [N,n,B,6|12] -> (loss [1], metrics [2] (photometric, smoothness), the
     forward state [bytes] the backward reads; its first n*B*H*W bytes are the
-    per-pixel min selection).  `cells` (int32 [N,n,B,H,W] or None): the
-    backward's test hook."""
+    per-pixel min selection).  clip_loss > 0: every candidate map clamped at
+    mean + clip_loss * std of itself (:223-227).  `cells` (int32 [N,n,B,H,W])
+    and `l1_signs` (int8 [N,n,B,3,H,W]), or None: the backward's test hooks
+    (the clip thresholds are in the state: photometric_clip_thresholds)."""
     lib = _lib.load()
     require_device(image, context, inv_depths, pose, K, ref_K, what="photometric_loss")
     n, B, _, H, W = inv_depths.shape
     N = context.shape[0]
-    ws = torch.empty(lib.dro_photometric_workspace_bytes(B, N, n, H, W), device=image.device, dtype=torch.uint8)
+    ws = torch.empty(lib.dro_photometric_workspace_bytes(B, N, n, H, W, clip_loss), device=image.device,
+                     dtype=torch.uint8)
     out = torch.empty(3, device=image.device)
     check(lib.dro_photometric_forward(ptr(image.contiguous()), ptr(context.contiguous()), ptr(inv_depths.contiguous()),
                                       ptr(K.contiguous()), ptr(ref_K.contiguous()), ptr(pose.contiguous()), pose_mode,
                                       B, N, n, H, W, ssim_w, C1, C2, smooth_w, int(automask), int(reduce_min),
-                                      ptr(out), ptr(ws), stream_of(image)), "dro_photometric_forward")
+                                      clip_loss, ptr(out), ptr(ws), stream_of(image)), "dro_photometric_forward")
     return out[0:1].clone(), out[1:].clone(), ws
 
 
 @_photometric_op.register_fake
-def _(image, context, inv_depths, pose, K, ref_K, pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min, cells):
+def _(image, context, inv_depths, pose, K, ref_K, pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min,
+      clip_loss, cells, l1_signs):
     n, B, _, H, W = inv_depths.shape
-    nb = _lib.load().dro_photometric_workspace_bytes(B, context.shape[0], n, H, W)
+    nb = _lib.load().dro_photometric_workspace_bytes(B, context.shape[0], n, H, W, clip_loss)
     return image.new_empty(1), image.new_empty(2), image.new_empty(nb, dtype=torch.uint8)
 
 
-@torch.library.custom_op("dro::photometric_loss_backward", mutates_args=("cells",))
+@torch.library.custom_op("dro::photometric_loss_backward", mutates_args=("cells", "l1_signs"))
 def _photometric_bwd_op(image: Tensor, context: Tensor, inv_depths: Tensor, pose: Tensor, K: Tensor,
                         ref_K: Tensor, state: Tensor, grad_loss: Tensor, pose_mode: int, ssim_w: float, C1: float,
-                        C2: float, smooth_w: float, automask: bool, reduce_min: bool, need_pose: bool,
-                        cells: Optional[Tensor]) -> list[Tensor]:
+                        C2: float, smooth_w: float, automask: bool, reduce_min: bool, clip_loss: float,
+                        need_pose: bool, cells: Optional[Tensor], l1_signs: Optional[Tensor]) -> list[Tensor]:
     """Backward of dro::photometric_loss: [g_inv_depths, g_pose (empty unless need_pose)]."""
     lib = _lib.load()
     n, B, _, H, W = inv_depths.shape
@@ -504,22 +509,24 @@ def _photometric_bwd_op(image: Tensor, context: Tensor, inv_depths: Tensor, pose
     g_pose = torch.empty_like(pose) if need_pose else None
     check(lib.dro_photometric_backward(ptr(image), ptr(context), ptr(inv_depths), ptr(K), ptr(ref_K), ptr(pose),
                                        pose_mode, B, N, n, H, W, ssim_w, C1, C2, smooth_w, int(automask),
-                                       int(reduce_min), ptr(grad_loss.contiguous()), ptr(g_inv), ptr(g_pose),
-                                       ptr(state), ptr(cells), stream_of(image)), "dro_photometric_backward")
+                                       int(reduce_min), clip_loss, ptr(grad_loss.contiguous()), ptr(g_inv),
+                                       ptr(g_pose), ptr(state), ptr(cells), ptr(l1_signs), stream_of(image)),
+          "dro_photometric_backward")
     return [g_inv, g_pose if g_pose is not None else _none_like(image.device)]
 
 
 @_photometric_bwd_op.register_fake
 def _(image, context, inv_depths, pose, K, ref_K, state, grad_loss, pose_mode, ssim_w, C1, C2, smooth_w, automask,
-      reduce_min, need_pose, cells):
+      reduce_min, clip_loss, need_pose, cells, l1_signs):
     return [inv_depths.new_empty(inv_depths.shape), pose.new_empty(pose.shape) if need_pose else pose.new_empty(0)]
 
 
 def _photometric_setup(ctx, inputs, output):
-    image, context, inv_depths, pose, K, ref_K, pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min, cells = inputs
+    (image, context, inv_depths, pose, K, ref_K, pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min, clip_loss,
+     cells, l1_signs) = inputs
     _, metrics, state = output
-    ctx.save_for_backward(image, context, inv_depths, pose, K, ref_K, state, cells)
-    ctx.cfg = (pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min)
+    ctx.save_for_backward(image, context, inv_depths, pose, K, ref_K, state, cells, l1_signs)
+    ctx.cfg = (pose_mode, ssim_w, C1, C2, smooth_w, automask, reduce_min, clip_loss)
     ctx.need = (inv_depths.requires_grad, pose.requires_grad)
     ctx.mark_non_differentiable(metrics, state)
     ctx.set_materialize_grads(False)     # no zero-filled gradients for the non-differentiable outputs
@@ -527,22 +534,23 @@ def _photometric_setup(ctx, inputs, output):
 
 def _photometric_backward(ctx, gloss, _gmetrics, _gstate):
     if gloss is None:
-        return (None,) * 14
-    image, context, inv_depths, pose, K, ref_K, state, cells = ctx.saved_tensors
+        return (None,) * 16
+    image, context, inv_depths, pose, K, ref_K, state, cells, l1_signs = ctx.saved_tensors
     g_inv, g_pose = torch.ops.dro.photometric_loss_backward(image, context, inv_depths, pose, K, ref_K, state, gloss,
-                                                            *ctx.cfg, ctx.need[1], cells)
-    # one entry per forward input: image, context, inv_depths, pose, then ten non-differentiable ones
-    return (None, None, g_inv if ctx.need[0] else None, _opt(g_pose), None, None, None, None, None, None, None,
-            None, None, None)
+                                                            *ctx.cfg, ctx.need[1], cells, l1_signs)
+    # one entry per forward input: image, context, inv_depths, pose, then twelve non-differentiable ones
+    return (None, None, g_inv if ctx.need[0] else None, _opt(g_pose)) + (None,) * 12
 
 
 torch.library.register_autograd("dro::photometric_loss", _photometric_backward, setup_context=_photometric_setup)
 
 
 def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=0.85, C1=1e-4,
-                     C2=9e-4, smooth_w=0.001, automask=True, reduce_min=True,
+                     C2=9e-4, smooth_w=0.001, automask=True, reduce_min=True, clip_loss=0.0,
                      return_selection=False):
     """Fused MultiViewPhotometricDecayLoss (multiview_photometric_loss_mf.py:303-361).
+    clip_loss > 0: each candidate map is clamped at float(mean + clip_loss * std)
+    of itself before the reduction (:223-227).
 
     image [B,3,H,W]; context [N,B,3,H,W]; inv_depths [n,B,1,H,W];
     pose [N,n,B,6] euler vectors or [N,n,B,3|4,4] matrices.
@@ -560,9 +568,20 @@ def photometric_loss(image, context, inv_depths, pose, K, ref_K=None, *, ssim_w=
     pose_flat, pose_mode = _pose_layout(pose, (N, n, B))
     require_device(pose_flat, what="photometric_loss")
     cells = _new_cells("photo", (N, n, B, H, W), image.device, inv_depths, pose_flat)
+    signs = _new_cells("photo_l1", (N, n, B, 3, H, W), image.device, inv_depths, pose_flat, dtype=torch.int8, fill=0)
     loss, metrics, state = torch.ops.dro.photometric_loss(
         image, context, inv_depths, pose_flat, K, K if ref_K is None else ref_K, pose_mode, float(ssim_w),
-        float(C1), float(C2), float(smooth_w), bool(automask), bool(reduce_min), cells)
+        float(C1), float(C2), float(smooth_w), bool(automask), bool(reduce_min), float(clip_loss), cells, signs)
+    if clip_loss > 0 and _CELLS[0] is not None:
+        # the forward's clip thresholds and clamp decisions (in its state), for
+        # the oracle's branch
+        lib = _lib.load()
+        o_pm, o_thr = (lib.dro_photometric_clip_offset(B, N, n, H, W, w) for w in (0, 1))
+        thr = state[o_thr:o_thr + 4 * (N * n + N)].view(torch.float32).clone()
+        pm = state[o_pm:o_pm + 4 * N * n * B * H * W].view(torch.float32).view(N, n, B, H, W)
+        keep = (pm <= thr[:N * n].view(N, n, 1, 1, 1)).to(torch.uint8)
+        _CELLS[0].calls.append(("photo_clip", thr))
+        _CELLS[0].calls.append(("photo_clipmask", keep))
     if return_selection:
         return loss, metrics, state[:n * B * H * W].view(n, B, H, W)
     return loss, metrics

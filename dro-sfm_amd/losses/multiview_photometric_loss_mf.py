@@ -6,9 +6,12 @@ automask, min/mean reduction with the 0.85^(n-i-1) decay and the edge-aware
 smoothness term -- is one fused HIP op (hip.photometric_loss): 3 launches
 forward, 2 backward, in place of ~50 ATen launches per (prediction, ref) pair.
 
-Supported: clip_loss == 0 and padding_mode 'zeros' (every reference yaml), and
-inverse-depth predictions at the image resolution (what DepthPoseNet emits).
-Anything else raises NotImplementedError rather than running a slow path.
+Supported: any clip_loss >= 0 (every reference yaml sets 0; the constructor's
+default 0.5 clamps each candidate map at mean + 0.5 std of itself, :223-227 --
+two forward passes around per-map thresholds in the kernel), padding_mode
+'zeros' (every yaml), and inverse-depth predictions at the image resolution
+(what DepthPoseNet emits).  Anything else raises NotImplementedError rather
+than running a slow path.
 """
 import torch
 
@@ -45,8 +48,6 @@ class MultiViewPhotometricDecayLoss(LossBase):
         return {"num_scales": self.n}
 
     def _check_supported(self, image, inv_depths):
-        if self.clip_loss > 0.0:
-            raise NotImplementedError("clip_loss > 0 is not implemented by the fused kernel")
         if self.padding_mode != "zeros":
             raise NotImplementedError("only padding_mode='zeros' is implemented")
         if self.ssim_loss_weight <= 0.0:
@@ -66,7 +67,8 @@ class MultiViewPhotometricDecayLoss(LossBase):
         loss, metrics, sel = photometric_loss(
             image, ctx, invs, pose_t, K.float(), ref_K.float(), ssim_w=self.ssim_loss_weight,
             C1=self.C1, C2=self.C2, smooth_w=self.smooth_loss_weight, automask=self.automask_loss,
-            reduce_min=self.photometric_reduce_op == "min", return_selection=True)
+            reduce_min=self.photometric_reduce_op == "min", clip_loss=max(float(self.clip_loss), 0.0),
+            return_selection=True)
         self.last_selection = sel.clone() if self.keep_selection else None
         # The reference stores a detached alias of the photometric loss and then adds
         # the smoothness in place (:268, :356), so its 'photometric_loss' metric

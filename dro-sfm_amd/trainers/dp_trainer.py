@@ -303,6 +303,66 @@ class GradBuckets:
             self.flat.div_(self.world)
 
 
+def agree_all(ok, group=None, device=None):
+    """True iff `ok` holds on every rank: one MIN all-reduce, issued outside any
+    graph capture.  Ranks that must take the same branch (GraphedTrainStep's
+    choice of exchange path) decide on the agreed value, never on their own."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def capture_with_agreement(try_in_graph, fallback, group=None, device=None, sync=None, log=None):
+    """Run `try_in_graph()` (a capture with the collectives inside); every rank
+    then learns whether it succeeded on ALL ranks and, if not, every rank runs
+    `fallback()` (the capture without collectives, exchange after replay).
+    A rank deciding alone could leave it reducing after replay while its peers
+    run collectives inside their graphs: a deadlock.  Capturing a
+    collective does not communicate, so a rank that fails mid-capture cannot
+    block one that succeeded before both reach the agreement.  Returns True
+    when the in-graph path was kept."""
+    ok, err = True, None
+    try:
+        try_in_graph()
+    except RuntimeError as e:
+        ok, err = False, e
+    if sync is not None:
+        sync()
+    if agree_all(ok, group, device):
+        return True
+    if log is not None:
+        log(f"capture with in-graph all-reduces failed on {'this rank' if not ok else 'another rank'}"
+            + (f" ({err})" if err is not None else "") + "; every rank falls back to the exchange after each replay")
+    fallback()
+    return False
+
+
+def collective_signature(grads):
+    """The sequence of collectives the last backward issued: (bucket, flat
+    offset, length) per all-reduce, in issue order."""
+    out = []
+    for b in grads.issued:
+        s = grads._slice(grads.buckets[b])
+        out.append((int(b), int(s.storage_offset()), int(s.numel())))
+    return tuple(out)
+
+
+def check_same_across_ranks(sig, group=None, device=None, what="collective sequence"):
+    """Raise unless `sig` (any repr-able value) is identical on every rank: a
+    CRC of its repr, MIN- and MAX-reduced."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    import zlib
+    h = zlib.crc32(repr(sig).encode())
+    t = torch.tensor([h, -h], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    if int(t[0]) != h or -int(t[1]) != h:
+        raise RuntimeError(f"{what} differs between ranks (rank {dist.get_rank(group)}: crc {h}, "
+                           f"min {int(t[0])}, max {-int(t[1])})")
+
+
 def _direct_used(p):
     return getattr(p, "_dro_direct_used", False)
 
@@ -621,23 +681,32 @@ class GraphedTrainStep:
         cur.wait_stream(side)
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle() if share_pool else None
-        try:
+        group, dev = trainer.grads.group, trainer.grads.flat.device
+        if not self.in_graph:
             self._capture_all(flips)
-        except RuntimeError as e:
-            if not self.in_graph:
-                raise
-            # a capture that fails with the collectives inside fails the same way on
-            # every rank (same program, same point): all ranks fall back together to
-            # the exchange after each replay, and say so
-            print(f"[GraphedTrainStep] capture with in-graph all-reduces failed ({e}); "
-                  "falling back to the exchange after each replay", file=sys.stderr, flush=True)
-            torch.cuda.synchronize()
-            self.in_graph, self.outside = False, True
-            self.pool = torch.cuda.graph_pool_handle() if share_pool else None
-            self._capture_all(flips)
+        else:
+            def fallback():
+                self.graphs = {}
+                torch.cuda.synchronize()
+                self.in_graph, self.outside = False, True
+                self.pool = torch.cuda.graph_pool_handle() if share_pool else None
+                self._capture_all(flips)
+
+            # every rank falls back together or none does (capture_with_agreement)
+            capture_with_agreement(lambda: self._capture_all(flips), fallback, group, dev,
+                                   sync=torch.cuda.synchronize,
+                                   log=lambda m: print(f"[GraphedTrainStep] {m}", file=sys.stderr, flush=True))
+        # each rank replays the flip graph its own draw picks (as the reference
+        # flips per rank, SfmModelMF.py:110): every graph must issue the same
+        # collectives in the same order, on every rank
+        seqs = set(self.issue_seq.values())
+        if len(seqs) != 1:
+            raise RuntimeError(f"GraphedTrainStep: the flip graphs issue different collective sequences: "
+                               f"{self.issue_seq}")
+        check_same_across_ranks(next(iter(seqs)), group, dev, "captured collective sequence")
 
     def _capture_all(self, flips):
-        self.graphs = {}
+        self.graphs, self.issue_seq = {}, {}
         for f in flips:
             g = torch.cuda.CUDAGraph()
             # thread_local: the RCCL watchdog thread queries the events of the
@@ -647,6 +716,10 @@ class GraphedTrainStep:
             with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                 out = self._captured(f)
             self.graphs[f] = (g, out)
+            # in-graph: the buckets the hooks issued inside this capture; after
+            # replay: reduce_now's fixed runs (the same for every graph)
+            self.issue_seq[f] = (collective_signature(self.tr.grads) if not self.outside
+                                 else ("after-replay", tuple(map(tuple, getattr(self.tr.grads, "_runs", [])))))
         torch.cuda.synchronize()
 
     def _body(self, flip):

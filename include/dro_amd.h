@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -130,22 +130,32 @@ int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref, const floa
 /* ------------------------------------------------------------------------
  * Multi-view photometric decay loss + edge-aware smoothness.
  * Replaces MultiViewPhotometricDecayLoss.forward
- * (losses/multiview_photometric_loss_mf.py:303-361) with clip_loss == 0 and
- * padding_mode 'zeros': view_synthesis (geometry/camera_utils.py:23-56), SSIM
- * (:15-54), L1, automask (:346-351), min/mean reduce and 0.85^(n-i-1) decay
+ * (losses/multiview_photometric_loss_mf.py:303-361) with padding_mode
+ * 'zeros': view_synthesis (geometry/camera_utils.py:23-56), SSIM (:15-54), L1,
+ * clip_loss (:223-227: each candidate map clamped at mean + clip_loss * std of
+ * itself; 0 = off, as in every reference yaml; the constructor's default is
+ * 0.5), automask (:346-351), min/mean reduce and 0.85^(n-i-1) decay
  * (:231-269), calc_smoothness (utils/depth.py:166-199) (:273-299).
  *   image [B,3,H,W]; context [N,B,3,H,W]; inv_depths [n,B,1,H,W];
  *   K, ref_K [B,3,3] (scaled by DW/W = 1 -> unscaled); pose [N,n,B,6|12].
  *   out [3] = {loss, photometric_loss metric, smoothness_loss metric}.
  * `workspace` (dro_photometric_workspace_bytes) carries the forward state the
  * backward needs; keep it alive and unmodified in between. */
-size_t dro_photometric_workspace_bytes(int B, int N, int n, int H, int W);
+size_t dro_photometric_workspace_bytes(int B, int N, int n, int H, int W, float clip_loss);
+
+/* With clip_loss > 0: byte offsets in that workspace, after the forward, of
+ * which = 0: the warped photometric maps, fp32 [N,n,B,H,W] (unclamped);
+ * which = 1: the fp32 clamp thresholds -- N*n for the warped maps (index
+ * j*n + i), then N for the unwarped (automask) maps.  The tests pin the fp64
+ * oracle to the kernel's clamp decisions (a pixel within rounding of its
+ * map's threshold is clamped or not by rounding). */
+size_t dro_photometric_clip_offset(int B, int N, int n, int H, int W, int which);
 
 int dro_photometric_forward(const float* image, const float* context, const float* inv_depths,
                             const float* K, const float* ref_K, const float* pose, int pose_mode,
                             int B, int N, int n, int H, int W,
                             float ssim_w, float C1, float C2, float smooth_w,
-                            int automask, int reduce_min,
+                            int automask, int reduce_min, float clip_loss,
                             float* out, void* workspace, void* stream);
 
 /* grad_out: device pointer to d(total)/d(loss) (1 float).  Writes
@@ -153,14 +163,17 @@ int dro_photometric_forward(const float* image, const float* context, const floa
  * cells (test hook, NULL in production): int32 [N,n,B,H,W], the bilinear cell
  * of every pixel's warp whose derivative this backward used (packed as in
  * dro_warp_cost_backward; pixels of a (ref, tile) with no selected candidate
- * are skipped and left as they were). */
+ * are skipped and left as they were).  l1_signs (test hook, NULL in
+ * production): int8 [N,n,B,3,H,W], the sign of (warped - target) the L1
+ * term's derivative used, 1 / -1 / 2 (zero), at every pixel whose candidate
+ * passed a gradient (others left as they were). */
 int dro_photometric_backward(const float* image, const float* context, const float* inv_depths,
                              const float* K, const float* ref_K, const float* pose, int pose_mode,
                              int B, int N, int n, int H, int W,
                              float ssim_w, float C1, float C2, float smooth_w,
-                             int automask, int reduce_min,
+                             int automask, int reduce_min, float clip_loss,
                              const float* grad_out, float* grad_inv_depths, float* grad_pose,
-                             void* workspace, int* cells, void* stream);
+                             void* workspace, int* cells, signed char* l1_signs, void* stream);
 
 /* ------------------------------------------------------------------------
  * Supervised depth + pose loss (sparse-l1).

@@ -109,7 +109,7 @@ def sample_grid(depth, K, ref_K, pose, scale):
 
 # diagnostics: how many positions each kind of pinning actually moved off the
 # natural branch in the evaluations since the last clear (tools/diag_*)
-PIN_STATS = {"cells": 0, "maxpool": 0, "relu": 0}
+PIN_STATS = {"cells": 0, "maxpool": 0, "relu": 0, "l1": 0}
 
 
 class Cells:
@@ -124,7 +124,11 @@ class Cells:
     evaluated on the branch another implementation took (the HIP kernels
     record theirs: hip.record_bilinear_cells); with record=True the natural
     cells of every call are kept in `recorded`.  Keys: ("depth", it, s, j),
-    ("pose", it, s, j), ("photo", j, i)."""
+    ("pose", it, s, j), ("photo", j, i).  With record=True the ReLU masks
+    (("relu", key)) and stem-pooling argmaxes (("maxpool", encoder)) are
+    recorded too, in the product record's layout (`as_forced()`), so that a
+    second evaluation can be put on this one's whole branch
+    (tools/conditioning.py)."""
 
     def __init__(self, forced=None, record=False):
         self.forced = forced or {}
@@ -132,6 +136,20 @@ class Cells:
 
     def sample(self, img, grid, key):
         return grid_sample_cells(img, grid, self.forced.get(key), self, key)
+
+    def record(self, key, value, part=None):
+        if self.recorded is None:
+            return
+        if part is None:
+            self.recorded[key] = value
+        else:                             # view `part` of a site the product runs stacked
+            self.recorded.setdefault(key, {})[part] = value
+
+    def as_forced(self):
+        """The recorded branch as a `forced` dict (stacked views concatenated
+        along the batch in view order, as the product records them)."""
+        return {k: (torch.cat([v[j] for j in sorted(v)], 0) if isinstance(v, dict) else v)
+                for k, v in self.recorded.items()}
 
 
 def pack_cells(x0, y0):
@@ -154,6 +172,16 @@ def cells_from_calls(calls):
             for j in range(c.shape[0]):
                 for i in range(c.shape[1]):
                     out[("photo", j, i)] = c[j, i]
+        elif tag == "photo_clip":             # float [N*n + N] clip thresholds (photometric_map)
+            out[("clip", "thr")] = cells.cpu()
+        elif tag == "photo_clipmask":         # uint8 [N,n,B,H,W]: value <= threshold (not clamped)
+            for j in range(c.shape[0]):
+                for i in range(c.shape[1]):
+                    out[("clipkeep", (j, i))] = c[j, i]
+        elif tag == "photo_l1":               # int8 [N,n,B,3,H,W] L1 signs (l1_pinned)
+            for j in range(c.shape[0]):
+                for i in range(c.shape[1]):
+                    out[("l1", (j, i))] = c[j, i]
         elif isinstance(tag, tuple) and tag[0] in ("maxpool", "relu"):
             out[tag] = c         # maxpool: [B,C,Ho,Wo] window index dy * 3 + dx; relu: y > 0 of a BN site
         elif isinstance(tag, tuple) and tag[0] == "relu_seq":     # y > 0 of the n-th call of a conv ReLU site
@@ -166,6 +194,17 @@ def cells_from_calls(calls):
             for j in range(c.shape[0]):
                 out[(tag[0], tag[1], s_, j)] = c[j]
     return out
+
+
+# pixels: how close to a grid line a coordinate must be for a recorded cell on
+# the line's other side to be taken (grid_sample_cells)
+CELL_TOL = 1e-3
+
+
+def _near_line(v, v0, f):
+    """f (a recorded floor) is v's own floor v0, or the neighbour across the
+    grid line nearest v within CELL_TOL."""
+    return (f == v0) | ((f == v0 - 1) & (v - v0 <= CELL_TOL)) | ((f == v0 + 1) & (v0 + 1 - v <= CELL_TOL))
 
 
 def grid_sample_cells(img, grid, cells=None, book=None, key=None):
@@ -185,11 +224,12 @@ def grid_sample_cells(img, grid, cells=None, book=None, key=None):
         c = cells.to(torch.int64).reshape(x0.shape)
         fx = ((c & 0xFFFF) - 32768).to(x0.dtype)
         fy = (((c >> 16) & 0xFFFF) - 32768).to(y0.dtype)
-        # a cell is taken only where it is this coordinate's own cell or a
-        # neighbour (|t - 1/2| <= 1: the other side of a nearby grid line);
-        # where another evaluation's trajectory has diverged further (an
-        # ill-conditioned recurrence), the natural cell stays
-        near = ((ix.detach() - fx - 0.5).abs() <= 1.0) & ((iy.detach() - fy - 0.5).abs() <= 1.0)
+        # a cell is taken only where it is this coordinate's own cell or the
+        # neighbour across a grid line within CELL_TOL pixels of the
+        # coordinate (a cell edge rounding decides); anything further keeps
+        # the natural cell (a wider band would let the oracle
+        # extrapolate from a wrong cell instead of bounding cell-choice errors)
+        near = _near_line(ix.detach(), x0, fx) & _near_line(iy.detach(), y0, fy)
         forced = (c != -1) & near
         PIN_STATS["cells"] += int((forced & ((fx != x0) | (fy != y0))).sum())
         x0 = torch.where(forced, fx, x0)
@@ -257,13 +297,71 @@ def ssim(x, y, C1=1e-4, C2=9e-4):
     return num / den
 
 
-def photometric_map(est, tgt, ssim_w, C1, C2):
-    """calc_photometric_loss (multiview_photometric_loss_mf.py:194-229), clip_loss == 0."""
-    l1 = (est - tgt).abs()
+# near-kink band of the L1 term |est - tgt| (images in [0, 1]): where the
+# difference is this small a recorded sign is taken (l1_pinned)
+L1_TOL = 1e-5
+
+
+def l1_pinned(d, cells=None, key=None):
+    """|d| (d = est - tgt, [B,3,H,W]); with a Cells book holding ("l1", key) --
+    another evaluation's sign of d per element (int8: 1 / -1 / 2 for zero, 0 =
+    not recorded) -- that sign is taken where |d| <= L1_TOL (a kink rounding
+    decides): there the value is d * sign (within L1_TOL of |d|), the
+    derivative the recorded one.  The product records the elements its
+    gradient used (photometric backward's l1_signs hook)."""
+    if cells is None or key is None:
+        return d.abs()
+    cells.record(("l1", key), _sign_code(d.detach()))
+    forced = cells.forced.get(("l1", key))
+    if forced is None:
+        return d.abs()
+    f = forced.to(torch.int64).reshape(d.shape)
+    sg = torch.where(f == 2, torch.zeros_like(d), f.to(d.dtype))
+    use = (f != 0) & (d.detach().abs() <= L1_TOL) & (sg != torch.sign(d.detach()))
+    PIN_STATS["l1"] = PIN_STATS.get("l1", 0) + int(use.sum())
+    return torch.where(use, d * sg, d.abs())
+
+
+def _sign_code(d):
+    return torch.where(d > 0, 1, torch.where(d < 0, -1, 2)).to(torch.int8)
+
+
+# relative band around a clip threshold in which a recorded clamp decision is taken
+CLIP_TOL = 1e-5
+
+
+def photometric_map(est, tgt, ssim_w, C1, C2, clip_loss=0.0, cells=None, key=None, clip_index=None):
+    """calc_photometric_loss (multiview_photometric_loss_mf.py:194-229) of one
+    [B,3,H,W] pair.  clip_loss > 0 (:223-227): the map is clamped from above
+    at float(mean + clip_loss * std) of itself (unbiased std, a detached
+    constant computed in the map's dtype); with a Cells book holding
+    ("clip", "thr") -- another evaluation's thresholds -- entry clip_index is
+    used instead (a pixel within rounding of its map's threshold is clamped or
+    not by rounding: the oracle then takes the other evaluation's side)."""
+    l1 = l1_pinned(est - tgt, cells, key)
     if ssim_w <= 0.0:
-        return l1
-    s = torch.clamp((1.0 - ssim(est, tgt, C1, C2)) / 2.0, 0.0, 1.0)
-    return ssim_w * s.mean(1, True) + (1 - ssim_w) * l1.mean(1, True)
+        out = l1
+    else:
+        s = torch.clamp((1.0 - ssim(est, tgt, C1, C2)) / 2.0, 0.0, 1.0)
+        out = ssim_w * s.mean(1, True) + (1 - ssim_w) * l1.mean(1, True)
+    if clip_loss > 0.0:
+        forced = cells.forced.get(("clip", "thr")) if cells is not None else None
+        if forced is not None and clip_index is not None:
+            thr = float(forced[clip_index])
+        else:
+            mean, std = out.mean(), out.std()
+            thr = float(mean + clip_loss * std)
+        keep = cells.forced.get(("clipkeep", key)) if cells is not None and key is not None else None
+        if keep is not None:
+            # the other evaluation's clamp decision where the value is within
+            # rounding of the threshold
+            k = keep.to(torch.bool).reshape(out.shape)
+            near = (out.detach() - thr).abs() <= CLIP_TOL * abs(thr)
+            PIN_STATS["clip"] = PIN_STATS.get("clip", 0) + int((near & (k != (out.detach() <= thr))).sum())
+            out = torch.where(near, torch.where(k, out, torch.full_like(out, thr)), torch.clamp(out, max=thr))
+        else:
+            out = torch.clamp(out, max=thr)
+    return out
 
 
 def smoothness(inv_depths, image, smooth_w):
@@ -285,21 +383,23 @@ LAST_SELECTION = []   # per prediction, the natural min-candidate map of the las
 
 def photometric_decay_loss(image, context, inv_depths, K, ref_K, poses, *, ssim_w=0.85, C1=1e-4,
                            C2=9e-4, smooth_w=0.001, automask=True, reduce="min",
-                           forced_selection=None, cells=None):
+                           forced_selection=None, cells=None, clip_loss=0.0):
     """MultiViewPhotometricDecayLoss.forward (multiview_photometric_loss_mf.py:303-361).
 
     context: list of N [B,3,H,W]; inv_depths: list of n [B,1,H,W] (full res);
     poses[j][i]: euler [B,6] or transform [B,4,4] for ref j, prediction i.
-    cells: a Cells book (keys ("photo", j, i)) -- test hook.
+    cells: a Cells book (keys ("photo", j, i), ("l1", (j, i))) -- test hook.
+    clip_loss: the reference constructor's per-map clamp (:93, :223-227).
     """
     n = len(inv_depths)
     per_pred = [[] for _ in range(n)]
     for j, ref in enumerate(context):
         for i in range(n):
             est = view_synthesis(ref, inv2depth(inv_depths[i]), poses[j][i], K, ref_K, cells, ("photo", j, i))
-            per_pred[i].append(photometric_map(est, image, ssim_w, C1, C2))
+            per_pred[i].append(photometric_map(est, image, ssim_w, C1, C2, clip_loss, cells, (j, i),
+                                               j * n + i))
         if automask:
-            unwarped = photometric_map(ref, image, ssim_w, C1, C2)
+            unwarped = photometric_map(ref, image, ssim_w, C1, C2, clip_loss, cells, None, len(context) * n + j)
             for i in range(n):
                 per_pred[i].append(unwarped)
     photo = 0.0
@@ -396,6 +496,17 @@ def max_pool_3x3s2(x, forced=None):
     return torch.where(tie, picked, y)
 
 
+def max_pool_argmax(x):
+    """The window index dy * 3 + dx of F.max_pool2d(x, 3, 2, 1)'s maximum
+    ([B,C,Ho,Wo] uint8, the product record's layout; the first maximum in
+    window order on exact ties)."""
+    B, C, H, W = x.shape
+    xp = F.pad(x.detach(), (1, 1, 1, 1), value=float("-inf"))
+    win = F.unfold(xp.reshape(B * C, 1, H + 2, W + 2), 3, stride=2)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    return torch.argmax(win.reshape(B, C, 9, Ho, Wo), 2).to(torch.uint8)
+
+
 def relu_pinned(v, cells=None, key=None):
     """F.relu(v); with a Cells book holding ("relu", key) -- another
     evaluation's mask y > 0 at this site -- the forced mask is taken where it
@@ -403,6 +514,8 @@ def relu_pinned(v, cells=None, key=None):
     magnitude from zero (a kink that rounding decides): there the output is
     v * mask (the value stays within that margin of relu(v), the derivative
     is the forced one)."""
+    if cells is not None:
+        cells.record(("relu", key), v.detach() > 0)
     forced = cells.forced.get(("relu", key)) if cells is not None else None
     if forced is None:
         return F.relu(v)
@@ -435,6 +548,7 @@ def relu_site(v, rk, name):
     if rk is None or rk[0] is None:
         return F.relu(v)
     cells, n, part = rk
+    cells.record(("relu", (name, n)), v.detach() > 0, None if part is None else part[0])
     forced = cells.forced.get(("relu", (name, n)))
     if forced is None:
         return F.relu(v)
@@ -451,6 +565,8 @@ def resnet_encoder(p, pre, x, training, stride=8, cells=None):
     pooling's argmax (test hook)."""
     x = relu_pinned(_bn(p, pre + "bn1", _conv(p, pre + "conv1", x, 2, 3), training), cells, pre + "bn1")
     forced = cells.forced.get(("maxpool", pre.rstrip("."))) if cells is not None else None
+    if cells is not None and cells.recorded is not None:
+        cells.record(("maxpool", pre.rstrip(".")), max_pool_argmax(x))
     x = max_pool_3x3s2(x, forced)
     feats = {}
     for li, s in ((1, 1), (2, 2), (3, 2)):

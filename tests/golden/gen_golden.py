@@ -344,6 +344,40 @@ def gen_geometry_loss():
          g_poses=vecs_.grad, min_depth=np.float32(0.2), max_depth=np.float32(80.0))
 
 
+def gen_clip():
+    """MultiViewPhotometricDecayLoss with clip_loss > 0 (the constructor's
+    default 0.5, multiview_photometric_loss_mf.py:93, :223-227): min reduction
+    with automask, and mean reduction without."""
+    from dro_sfm.geometry.pose import Pose
+    from dro_sfm.losses.multiview_photometric_loss_mf import MultiViewPhotometricDecayLoss
+    g = torch.Generator().manual_seed(7)
+    B, H, W = 2, 48, 160
+    K = kitti_K(B, W=W, H=H)
+    for name, kw in {"photo_loss_clip": dict(),
+                     "photo_loss_clip_mean": dict(automask_loss=False, photometric_reduce_op="mean")}.items():
+        n, N = 3, 2
+        image = smooth_images(B, H, W, 61)
+        ctx = [smooth_images(B, H, W, 62 + j) for j in range(N)]
+        invs = [0.05 + 0.5 * torch.rand(B, 1, H, W, generator=g) for _ in range(n)]
+        vecs = torch.stack([torch.stack([rand_pose(B, g) for _ in range(n)], 1) for _ in range(N)], 1)  # [B,N,n,6]
+        args = dict(ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4,
+                    C2=9e-4, photometric_reduce_op="min", disp_norm=True, clip_loss=0.5,
+                    progressive_scaling=0.0, padding_mode="zeros", automask_loss=True)
+        args.update(kw)
+        loss_fn = MultiViewPhotometricDecayLoss(**args)
+        invs_ = [i.clone().requires_grad_(True) for i in invs]
+        vecs_ = vecs.clone().requires_grad_(True)
+        poses = [[Pose.from_vec(vecs_[:, j, i], "euler") for i in range(n)] for j in range(N)]
+        out = loss_fn(image, ctx, invs_, K, K, poses)
+        out["loss"].sum().backward()
+        save(name, image=image, context=torch.stack(ctx), inv_depths=torch.stack(invs), poses=vecs,
+             K=K, loss=out["loss"], photometric_loss=out["metrics"]["photometric_loss"],
+             smoothness_loss=out["metrics"]["smoothness_loss"],
+             g_inv_depths=torch.stack([i.grad for i in invs_]), g_poses=vecs_.grad,
+             automask=np.int32(args["automask_loss"]),
+             reduce_min=np.int32(args["photometric_reduce_op"] == "min"), clip_loss=np.float32(0.5))
+
+
 def gen_network_parts():
     from dro_sfm.networks.depth_pose.DepthPoseNet import DepthPoseNet
     from dro_sfm.networks.optim.update import SepConvGRU, BasicUpdateBlockDepth, BasicUpdateBlockPose
@@ -636,6 +670,8 @@ if __name__ == "__main__":
         gen_cost()
     if "geom" in which:
         gen_geometry_loss()
+    if "clip" in which:
+        gen_clip()
     if "parts" in which:
         gen_network_parts()
     if "full" in which:

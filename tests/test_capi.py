@@ -34,7 +34,7 @@ def test_header_matches_exports(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dro_abi_version() == 5
+    assert lib.dro_abi_version() == 6
 
 
 def test_null_arguments_rejected(lib):
@@ -44,7 +44,7 @@ def test_null_arguments_rejected(lib):
     assert st == -1
     assert b"NULL" in lib.dro_last_error()
     st = lib.dro_photometric_forward(NULL, NULL, NULL, NULL, NULL, NULL, 0, 1, 1, 1, 8, 8, 0.85,
-                                     1e-4, 9e-4, 1e-3, 1, 1, NULL, NULL, NULL)
+                                     1e-4, 9e-4, 1e-3, 1, 1, 0.0, NULL, NULL, NULL)
     assert st == -1
     st = lib.dro_convex_upsample_forward(NULL, NULL, 1, 2, 2, 8, 0.0, 1.0, NULL, NULL)
     assert st == -1
@@ -61,13 +61,22 @@ def test_bad_sizes_and_modes_rejected(lib):
                                      p, None) == -3
     # automask needs the min reduction
     assert lib.dro_photometric_forward(p, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.85, 1e-4, 9e-4, 1e-3,
-                                       1, 0, p, p, None) == -3
+                                       1, 0, 0.0, p, p, None) == -3
+    # clip_loss NaN
+    assert lib.dro_photometric_forward(p, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.85, 1e-4, 9e-4, 1e-3,
+                                       1, 1, float("nan"), p, p, None) == -3
     assert lib.dro_convex_upsample_forward(p, p, 1, 2, 2, 9, 0.0, 1.0, p, None) == -2
 
 
 def test_workspace_sizes(lib):
     assert lib.dro_warp_cost_workspace_bytes(2, 2, 24, 80) >= 2 * 2 * 24 * 80 * 2 * 4
-    assert lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640) >= 9 * 2 * 192 * 640
+    assert lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640, 0.0) >= 9 * 2 * 192 * 640
+    # clip_loss > 0 keeps the N*n warped maps between the two forward passes
+    assert (lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640, 0.5)
+            >= lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640, 0.0) + 4 * 2 * 9 * 2 * 192 * 640)
+    pm, thr = (lib.dro_photometric_clip_offset(2, 2, 9, 192, 640, w) for w in (0, 1))
+    assert pm + 4 * 2 * 9 * 2 * 192 * 640 <= thr and pm % 4 == 0 and thr % 4 == 0
+    assert thr + 4 * (2 * 9 + 2) <= lib.dro_photometric_workspace_bytes(2, 2, 9, 192, 640, 0.5)
     # conv: at least the pre-activation gradient and the weight-gradient partials
     P = 2 * 24 * 80
     assert lib.dro_conv2d_workspace_bytes(2, 24, 80, 320, 256, 1, 5) >= 256 * P * 4 + 256 * 320 * 5 * 4

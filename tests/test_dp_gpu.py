@@ -157,8 +157,9 @@ def _rccl_graph_worker(rank, port, out, in_graph):
         m = _model()
         tr = DataParallelTrainer(m, capturable=True, bucket_mb=4.0, always_reduce=True)
         stage(f"trainer built; capturing (in_graph={in_graph})")
-        gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False,), reduce_in_graph=in_graph)
+        gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False, True), reduce_in_graph=in_graph)
         stage("captured")
+        seqs = dict(gs.issue_seq)
         assert gs.in_graph == in_graph and gs.outside == (not in_graph)
         nb, issued = len(tr.grads.buckets), list(tr.grads.issued)
         in_bwd = tr.grads.issued_in_backward
@@ -183,7 +184,8 @@ def _rccl_graph_worker(rank, port, out, in_graph):
         le = tr.step(batch, flip=False)[0].clone()
         ge = tr.grads.flat.clone()
         torch.cuda.synchronize()
-        out["res"] = (nb, issued, in_bwd, O.rel_err(lg.cpu(), le.cpu()), float((gg - ge).norm() / ge.norm()))
+        out["res"] = (nb, issued, in_bwd, O.rel_err(lg.cpu(), le.cpu()), float((gg - ge).norm() / ge.norm()),
+                      seqs)
     stage("results recorded; teardown")
     # the graphs hold RCCL kernels of this communicator: release them first
     del gs
@@ -204,8 +206,12 @@ def test_rccl_exchange_with_captured_graph_step(in_graph):
     with mp.Manager() as mgr:
         out = mgr.dict()
         mp.spawn(_rccl_graph_worker, args=(_free_port(), out, in_graph), nprocs=1, join=True)
-        nb, issued, in_bwd, loss_err, grad_err = out["res"]
+        nb, issued, in_bwd, loss_err, grad_err, seqs = out["res"]
     assert nb > 2 and issued == list(range(nb))
+    # both flip graphs captured, with the same collective sequence
+    assert set(seqs) == {False, True} and seqs[False] == seqs[True], seqs
+    if in_graph:
+        assert [b for b, _, _ in seqs[False]] == list(range(nb))
     if in_graph:
         assert in_bwd == nb, (in_bwd, nb)
     assert loss_err < 1e-5

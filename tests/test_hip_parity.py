@@ -10,7 +10,8 @@ import os
 import pytest
 import torch
 
-from common import fval, grad_errors, kitti_K, load_fixture, load_spec, params_from_spec, smooth_images
+from common import (condition_params, fval, grad_errors, kitti_K, load_fixture, load_spec, params_from_spec,
+                    smooth_images)
 from oracle import dro_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -141,6 +142,41 @@ def test_warp_cost_kitti_size_vs_oracle(hip):
     assert rel(pg.grad, pc.grad) < TOL
 
 
+def test_warp_cost_backward_converging_warp(hip):
+    """A warp that compresses the reference ~10x (camera moved back 9 depths:
+    ten consecutive target pixels sample one reference cell) next to an
+    ordinary one: the fmap_ref scatter merges each run of lanes sharing a cell
+    before its atomics (warp_cost_bwd_feat_kernel).  Every gradient vs the
+    fp64 oracle at 1e-4, for the depth-mean and the per-ref cost."""
+    g = torch.Generator().manual_seed(17)
+    B, C, h, w, N = 2, 128, 24, 80, 2
+    K = kitti_K(B)
+    fmap, frefs = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    depth = 1.0 + 0.01 * torch.rand(B, 1, h, w, generator=g)
+    poses = torch.zeros(N, B, 6)
+    poses[0, :, 2] = 9.0                                   # ref 0: 10x compression
+    poses[1, :, :3] = 0.1 * torch.randn(B, 3, generator=g)  # ref 1: an ordinary warp
+    poses[:, :, 3:] = 0.01 * torch.randn(N, B, 3, generator=g)
+    Gm, Gp = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    dt = torch.float64
+    dc, fc, rc, pc = (t.to(dt).requires_grad_(True) for t in (depth, fmap, frefs, poses))
+    cm = O.depth_cost_calc(1.0 / dc, fc, list(rc), list(poses.to(dt)), K.to(dt), K.to(dt), 1 / 8)
+    cp = torch.stack([O.get_cost_each(pc[j], fc, rc[j], depth.to(dt), K.to(dt), K.to(dt), 1 / 8)
+                      for j in range(N)])
+    ((cm * Gm.to(dt)).sum() + (cp * Gp.to(dt)).sum()).backward()
+    dg, fg, rg, pg = (t.to(DEV).requires_grad_(True) for t in (depth, fmap, frefs, poses))
+    Kd = K.to(DEV)
+    hm = hip.warp_cost(fg, rg, dg, poses.to(DEV), Kd, reduce_mean=True)
+    hp = hip.warp_cost(fg, rg, depth.to(DEV), pg, Kd, reduce_mean=False)
+    ((hm * Gm.to(DEV)).sum() + (hp * Gp.to(DEV)).sum()).backward()
+    assert rel(hm, cm) < TOL and rel(hp, cp) < TOL
+    for got, ref in ((dg.grad, dc.grad), (fg.grad, fc.grad), (rg.grad, rc.grad), (pg.grad, pc.grad)):
+        assert rel(got.double(), ref) < TOL, rel(got.double(), ref)
+    # the compressed ref's gradient really is concentrated: > 4 target pixels per touched cell
+    touched = int((rc.grad[0].abs().sum((0, 1)) > 0).sum())
+    assert touched * 4 < B * h * w, touched
+
+
 def test_warp_cost_forward_deterministic(hip):
     d = fx("cost_each_small")
     a = hip.warp_cost(d["fmap"], d["fmap_ref"], d["depth"], d["pose"], d["K"], reduce_mean=False)
@@ -241,12 +277,18 @@ def _oracle_photometric(d, dt, forced_selection=None, cells=None):
                                    automask=bool(int(d["automask"])),
                                    reduce="min" if int(d["reduce_min"]) else "mean",
                                    forced_selection=forced_selection,
-                                   cells=O.Cells(forced=cells) if cells is not None else None)
+                                   cells=O.Cells(forced=cells) if cells is not None else None,
+                                   clip_loss=_clip(d))
     out["loss"].sum().backward()
     return torch.stack([i.grad for i in invs]).double(), vecs.grad.double(), out["loss"].detach().double()
 
 
-@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean", "photo_loss_n4"])
+def _clip(d):
+    return float(d["clip_loss"]) if "clip_loss" in d else 0.0
+
+
+@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean", "photo_loss_n4",
+                                  "photo_loss_clip", "photo_loss_clip_mean"])
 def test_photometric_loss_golden(hip, name):
     """MultiViewPhotometricDecayLoss vs the reference's own outputs and input
     gradients (multiview_photometric_loss_mf.py:194-361).  Loss scalar and
@@ -266,7 +308,9 @@ def test_photometric_loss_golden(hip, name):
     The inverse-depth map also gets twice the fp32 oracle's own per-pixel
     error: SSIM's E[x^2]-E[x]^2 on smooth 3x3 windows cancels in any fp32
     evaluation.  And the kernel against the exact gradient of its own branch:
-    pose 1e-4 of max|x64|."""
+    pose 1e-4 of max|x64|.  The *_clip fixtures: clip_loss = 0.5, the
+    reference constructor's default (:93, :223-227), with min + automask and
+    with mean reduction."""
     d = fx(name)
     invs = d["inv_depths"].clone().requires_grad_(True)           # [n,B,1,H,W]
     vec = d["poses"].clone().requires_grad_(True)                 # [B,N,n,6]
@@ -274,7 +318,7 @@ def test_photometric_loss_golden(hip, name):
     with hip.record_bilinear_cells() as rec:
         loss, metrics, sel = hip.photometric_loss(d["image"], d["context"], invs, pose, d["K"],
                                                   automask=bool(int(d["automask"])),
-                                                  reduce_min=bool(int(d["reduce_min"])),
+                                                  reduce_min=bool(int(d["reduce_min"])), clip_loss=_clip(d),
                                                   return_selection=True)
         loss.sum().backward()
     cells = cells_from_record(rec)
@@ -504,10 +548,12 @@ def test_convex_upsample_many(hip):
 
 
 # ------------------------------------------------------------------ network level
-def _load_net(tag, version, mind, maxd):
+def _load_net(tag, version, mind, maxd, params=None):
     from dro_sfm_amd.networks.depth_pose.DepthPoseNet import DepthPoseNet
     net = DepthPoseNet(version=version, min_depth=mind, max_depth=maxd)
-    net.load_state_dict(params_from_spec(load_spec(os.path.join(G, f"depthposenet_{tag}_keys.json"))))
+    if params is None:
+        params = params_from_spec(load_spec(os.path.join(G, f"depthposenet_{tag}_keys.json")))
+    net.load_state_dict(params)
     return net.to(DEV)
 
 
@@ -538,8 +584,9 @@ def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=
     """Oracle loss and parameter gradients (and, want_preds, the net's
     predictions (inv_depths [n,B,1,H,W], poses [B,N,n,6])), on the branch
     given by the min-selection `forced` and the bilinear cells `cells` (a dict
-    of cells_from_record, or None for the natural ones)."""
-    p = params_from_spec(spec)
+    of cells_from_record, or None for the natural ones).  spec: a {name: shape}
+    weights spec (params_from_spec) or the parameter dict itself."""
+    p = spec if any(torch.is_tensor(v) for v in spec.values()) else params_from_spec(spec)
     p = {k: (v.to(dt).requires_grad_(True) if v.is_floating_point() and "running" not in k
              else (v.to(dt) if v.is_floating_point() else v)) for k, v in p.items()}
     b = {k: (v.clone().to(dt) if torch.is_tensor(v) and v.is_floating_point() else
@@ -662,20 +709,20 @@ def _run_step(model, batch, flip=None):
     return out, cells_from_record(rec)
 
 
-def _selfsup_model(mind, maxd, tag, version):
+def _selfsup_model(mind, maxd, tag, version, params=None):
     from dro_sfm_amd.models.SelfSupModelMF import SelfSupModelMF
     m = SelfSupModelMF(ssim_loss_weight=0.85, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
                        photometric_reduce_op="min", clip_loss=0.0, automask_loss=True, flip_lr_prob=0.0,
                        min_depth=mind, max_depth=maxd)
     m._photometric_loss.keep_selection = True
-    m.add_depth_net(_load_net(tag, version, mind, maxd))
+    m.add_depth_net(_load_net(tag, version, mind, maxd, params))
     return m.train()
 
 
-def _sup_model(mind, maxd, tag, version):
+def _sup_model(mind, maxd, tag, version, params=None):
     from dro_sfm_amd.models.SupModelMF import SupModelMF
     model = SupModelMF(supervised_method="sparse-l1", flip_lr_prob=0.0, min_depth=mind, max_depth=maxd)
-    model.add_depth_net(_load_net(tag, version, mind, maxd))
+    model.add_depth_net(_load_net(tag, version, mind, maxd, params))
     return model.train()
 
 
@@ -735,6 +782,40 @@ def _scannet_K(B, W=320, H=240):
     return K.unsqueeze(0).repeat(B, 1, 1).contiguous()
 
 
+REF_MIX = float(os.environ.get("DRO_REF_MIX", "0.1"))
+
+
+def full_size_case(case):
+    """The full-size train-step parity inputs (CPU tensors): "kitti" -- BASELINE
+    configs[1] (KITTI 192x640, it8-seq4-inter-out, B=2, N=2, self-sup);
+    "sup_view3" -- configs[2] (ScanNet 240x320, it12-h-out, N=2, supervised,
+    B=1); "selfsup_view5" -- configs[4]'s model (240x320, it12-h-out, N=4,
+    self-sup, B=1).  Returns (tag, version, kind, min_depth, max_depth, batch)."""
+    if case == "kitti":
+        B, N, H, W = 2, 2, 192, 640
+        img = smooth_images(B, H, W, 51, detail=0.3)
+        refs = [torch.roll(img, 3 * (j + 1), 3) * (1 - REF_MIX) + REF_MIX * smooth_images(B, H, W, 52 + j, detail=0.3)
+                for j in range(N)]
+        batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
+                 "intrinsics": kitti_K(B)}
+        return "it8", "it8-seq4-inter-out", "selfsup", 0.5, 80.0, batch
+    B, H, W = 1, 240, 320
+    N = 4 if case == "selfsup_view5" else 2
+    img = smooth_images(B, H, W, 81, detail=0.3)
+    refs = [torch.roll(img, 2 * (j + 1), 3) * (1 - REF_MIX) + REF_MIX * smooth_images(B, H, W, 82 + j, detail=0.3)
+            for j in range(N)]
+    batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
+             "intrinsics": _scannet_K(B)}
+    if case == "sup_view3":
+        g = torch.Generator().manual_seed(83)
+        batch["depth"] = 0.5 + 9.5 * torch.rand(B, 1, H, W, generator=g)
+        batch["pose_context"] = [O.vec_to_transform(torch.cat([0.05 * torch.randn(B, 3, generator=g),
+                                                               0.01 * torch.randn(B, 3, generator=g)], 1))
+                                 for _ in range(N)]
+        return "it12h", "it12-h-out", "sup", 0.2, 10.0, batch
+    return "it12h", "it12-h-out", "selfsup", 0.2, 10.0, batch
+
+
 def test_train_step_view5_n4_golden(hip):
     """configs[4] model on the reference's fixture: SelfSupModelMF it12-h-out,
     N=4 refs (ScanNet view5, depth 0.2-10), 64x96: loss 1e-4, gradients as in
@@ -759,68 +840,49 @@ def test_train_step_view5_n4_golden(hip):
     assert not fbad, fbad[:5]
 
 
-@pytest.mark.parametrize("kind", ["selfsup_view5", "sup_view3"])
-def test_train_step_scannet_size_vs_oracle(hip, kind):
-    """BASELINE configs[4] (SelfSupModelMF it12-h-out, N=4) and configs[2]
-    (SupModelMF it12-h-out, N=2, dense GT) at the ScanNet training shape
-    240x320, B=1: product step vs the fp64 oracle on the same weights and
-    inputs (kernel's min-selection); loss 1e-4, gradients as in
-    test_train_step_golden."""
-    B, H, W = 1, 240, 320
-    N = 4 if kind == "selfsup_view5" else 2
-    mind, maxd = 0.2, 10.0
-    spec = load_spec(os.path.join(G, "depthposenet_it12h_keys.json"))
-    img = smooth_images(B, H, W, 81, detail=0.3)
-    refs = [torch.roll(img, 2 * (j + 1), 3) * 0.9 + 0.1 * smooth_images(B, H, W, 82 + j, detail=0.3)
-            for j in range(N)]
-    batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
-             "intrinsics": _scannet_K(B)}
-    if kind == "sup_view3":
-        g = torch.Generator().manual_seed(83)
-        batch["depth"] = 0.5 + 9.5 * torch.rand(B, 1, H, W, generator=g)
-        from oracle.dro_oracle import vec_to_transform
-        batch["pose_context"] = [vec_to_transform(torch.cat([0.05 * torch.randn(B, 3, generator=g),
-                                                             0.01 * torch.randn(B, 3, generator=g)], 1))
-                                 for _ in range(N)]
-    model = (_selfsup_model if kind == "selfsup_view5" else _sup_model)(mind, maxd, "it12h", "it12-h-out")
+# the update heads' output convolutions are damped by this factor in the
+# full-size train-step tests (common.condition_params): at random init the
+# it8 / it12-h recurrences at 192x640 and 240x320 amplify fp32 rounding by
+# orders of magnitude (tools/conditioning.py: the fp32 reference algorithm
+# lands 1.4 (ScanNet sup) / 3.3 (ScanNet view5) / 1.8e-2 (KITTI) from fp64 in
+# relative L2 undamped), so no fixed bound could tell a bug from rounding
+FULL_DAMP = float(os.environ.get("DRO_FULL_DAMP", "0.03"))
+
+
+def _full_size_step(case):
+    """One product training step at a full BASELINE size on damped weights vs
+    the fp64 oracle on the kernels' branch; FIXED bounds:
+    loss 1e-4, every parameter gradient within GRAD_TENSOR_TOL, the whole
+    gradient within GRAD_L2_TOL -- no term computed from an fp32 evaluation or
+    from the product's own spread."""
+    tag, version, kind, mind, maxd, batch = full_size_case(case)
+    params = condition_params(params_from_spec(load_spec(os.path.join(G, f"depthposenet_{tag}_keys.json"))),
+                              FULL_DAMP)
+    model = (_selfsup_model if kind == "selfsup" else _sup_model)(mind, maxd, tag, version, params)
     gb = {k: (v.to(DEV) if torch.is_tensor(v) else [t.to(DEV) for t in v]) for k, v in batch.items()}
     out, cells = _run_step(model, gb)
-    forced = model._photometric_loss.last_selection.cpu().unsqueeze(2) if kind == "selfsup_view5" else None
-    okind = "selfsup" if kind == "selfsup_view5" else "sup"
-    loss64, g64 = _oracle_grads(spec, "it12-h-out", mind, maxd, batch, okind, torch.float64, forced, False, cells)
-    # the untrained it12-h recurrence at 240x320 amplifies fp32 rounding itself:
-    # the reference algorithm evaluated in fp32 (_fp32_floor) is the measure of
-    # what any fp32 evaluation can reach; the bounds are the fixed ones or 4x
-    # that distance, whichever is larger
-    c_loss, g32 = _fp32_floor(spec, "it12-h-out", mind, maxd, batch, okind, forced, cells, loss64, g64)
-    assert rel(out["loss"], loss64) < max(TOL, 4 * c_loss), (rel(out["loss"], loss64), c_loss)
-    bad, l2 = _grad_check(model, g64, tensor_tol=GRAD_TENSOR_TOL, l2_tol=GRAD_L2_TOL, ref32=g32)
+    forced = model._photometric_loss.last_selection.cpu().unsqueeze(2) if kind == "selfsup" else None
+    for k_ in list(O.PIN_STATS):
+        O.PIN_STATS[k_] = 0
+    loss64, g64, p64 = _oracle_grads(params, version, mind, maxd, batch, kind, torch.float64, forced, False, cells,
+                                     want_preds=True)
+    d_hip = _l2(torch.stack([d.detach() for d in out["inv_depths"]]), p64[0])
+    _log_margins("full_size", case=case, loss=rel(out["loss"], loss64), preds=d_hip, pinned=dict(O.PIN_STATS))
+    assert rel(out["loss"], loss64) < TOL, rel(out["loss"], loss64)
+    assert d_hip < TOL, d_hip
+    bad, l2 = _grad_check(model, g64)
     assert not bad, (bad[:5], l2)
+
+
+@pytest.mark.parametrize("case", ["selfsup_view5", "sup_view3"])
+def test_train_step_scannet_size_vs_oracle(hip, case):
+    """BASELINE configs[4] (SelfSupModelMF it12-h-out, N=4) and configs[2]
+    (SupModelMF it12-h-out, N=2, dense GT) at the ScanNet training shape
+    240x320, B=1 (_full_size_step)."""
+    _full_size_step(case)
 
 
 def test_train_step_kitti_metric_config(hip):
-    """Metric config (KITTI 192x640, it8-seq4-inter-out, B=2, N=2): product step vs
-    fp64 oracle step on the same weights/inputs with the same min-selection and
-    bilinear cells: loss 1e-4; gradients as in test_train_step_scannet_size_vs_oracle
-    (fixed bounds or 4x the fp32 oracle's distance on the same branch)."""
-    B, N, H, W = 2, 2, 192, 640
-    spec = load_spec(os.path.join(G, "depthposenet_it8_keys.json"))
-    img = smooth_images(B, H, W, 51, detail=0.3)
-    refs = [torch.roll(img, 3 * (j + 1), 3) * 0.9 + 0.1 * smooth_images(B, H, W, 52 + j, detail=0.3)
-            for j in range(N)]
-    K = kitti_K(B)
-    batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
-             "intrinsics": K}
-    model = _selfsup_model(0.5, 80.0, "it8", "it8-seq4-inter-out")
-    gb = {k: (v.to(DEV) if torch.is_tensor(v) else [t.to(DEV) for t in v]) for k, v in batch.items()}
-    out, cells = _run_step(model, gb)
-    forced = model._photometric_loss.last_selection.cpu().unsqueeze(2)
-    loss64, g64 = _oracle_grads(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", torch.float64, forced,
-                                False, cells)
-    assert rel(out["loss"], loss64) < TOL
-    # at 192x640 the untrained it8 recurrence amplifies fp32 rounding (the fp32
-    # oracle on the same branch lands 1.8e-2 from fp64 in relative L2): the
-    # bounds become the fixed ones or 4x that distance, as at ScanNet size
-    _, g32 = _fp32_floor(spec, "it8-seq4-inter-out", 0.5, 80.0, batch, "selfsup", forced, cells, loss64, g64)
-    bad, l2 = _grad_check(model, g64, ref32=g32)
-    assert not bad, (bad[:5], l2)
+    """Metric config (KITTI 192x640, it8-seq4-inter-out, B=2, N=2, self-sup;
+    _full_size_step)."""
+    _full_size_step("kitti")

@@ -23,7 +23,8 @@ SCHEMAS = {
                    "float min_disp, float max_disp, float scale, SymInt pose_mode) -> Tensor",
     "photometric_loss": "dro::photometric_loss(Tensor image, Tensor context, Tensor inv_depths, Tensor pose, "
                         "Tensor K, Tensor ref_K, SymInt pose_mode, float ssim_w, float C1, float C2, float smooth_w, "
-                        "bool automask, bool reduce_min, Tensor? cells) -> (Tensor, Tensor, Tensor)",
+                        "bool automask, bool reduce_min, float clip_loss, Tensor? cells, Tensor? l1_signs) -> "
+                        "(Tensor, Tensor, Tensor)",
     "supervised_loss": "dro::supervised_loss(Tensor gt_inv, Tensor inv_depths, Tensor pose, Tensor gt_pose, Tensor K, "
                        "Tensor ref_K, SymInt pose_mode, float min_depth, float max_depth) -> (Tensor, Tensor)",
     "convex_upsample": "dro::convex_upsample(Tensor inv, Tensor mask, SymInt ratio, float add, float mul) -> Tensor",

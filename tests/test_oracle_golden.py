@@ -78,7 +78,8 @@ def test_ssim():
     assert O.rel_err(x.grad, d["g_x"]) < 1e-4
 
 
-@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean", "photo_loss_n4"])
+@pytest.mark.parametrize("name", ["photo_loss", "photo_loss_noauto", "photo_loss_mean", "photo_loss_n4",
+                                  "photo_loss_clip", "photo_loss_clip_mean"])
 def test_photometric_loss(name):
     d = fx(name)
     invs = [i.clone().requires_grad_(True) for i in d["inv_depths"]]
@@ -87,7 +88,8 @@ def test_photometric_loss(name):
     poses = [[vecs[:, j, i] for i in range(n)] for j in range(N)]
     out = O.photometric_decay_loss(d["image"], list(d["context"]), invs, d["K"], d["K"], poses,
                                    automask=bool(d["automask"]),
-                                   reduce="min" if int(d["reduce_min"]) else "mean")
+                                   reduce="min" if int(d["reduce_min"]) else "mean",
+                                   clip_loss=float(d["clip_loss"]) if "clip_loss" in d else 0.0)
     assert O.rel_err(out["loss"], d["loss"]) < TOL
     assert O.rel_err(out["photometric_loss"], d["photometric_loss"]) < TOL
     assert O.rel_err(out["smoothness_loss"], d["smoothness_loss"]) < TOL
