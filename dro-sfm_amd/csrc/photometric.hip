@@ -260,6 +260,9 @@ __device__ __forceinline__ void synth(const PhotoArgs& a, const float* __restric
 
 // SSIM (multiview_photometric_loss_mf.py:15-54) of one channel from a 3x3
 // window of two LDS images with row pitch `pitch`, centred at offset o.
+// (Round 5: moments about the window's centre value and a centred adjoint were
+// measured -- no change in any parity margin, photometric backward 8 % slower;
+// not kept.)
 struct SsimStats {
   float mx, my, sxx, syy, sxy;  // pooled E[x], E[y], E[x^2], E[y^2], E[xy]
 };
@@ -612,8 +615,11 @@ __global__ __launch_bounds__(1024) void photo_finalize_kernel(PhotoArgs a, float
 // REC: the test hooks (bilinear cells, L1 signs) are compiled in; the
 // production instantiation carries neither (their address arithmetic costs
 // registers in a kernel at its 128-VGPR budget)
+#ifndef DRO_PHOTO_BWD_WAVES
+#define DRO_PHOTO_BWD_WAVES 4   // waves per SIMD the register budget targets (4: 128 VGPRs)
+#endif
 template <bool REC>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DRO_PHOTO_BWD_WAVES))) void photo_bwd_kernel(PhotoArgs a, const float* __restrict__ gout,
                                                              float* __restrict__ ginv) {
   constexpr int PL2 = H2 * W2;  // est / tgt with 2-px halo
   constexpr int PL1 = H1 * W1;  // adjoint image with 1-px halo
@@ -749,16 +755,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         // see exactly the 3x3 neighbourhood (same summation order as the
         // general path, which handles the reflected taps explicitly).
         float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        auto tap = [&](int kk) {
+          s0 += adj[0 * PL1 + kk];
+          s1 += adj[1 * PL1 + kk];
+          s2 += adj[2 * PL1 + kk];
+        };
         if (gy >= 2 && gy <= H - 3 && gx >= 2 && gx <= W - 3) {
 #pragma unroll
           for (int u = 0; u < 3; ++u)
 #pragma unroll
-            for (int v = 0; v < 3; ++v) {
-              const int kk = (ly + u) * W1 + (lx + v);
-              s0 += adj[0 * PL1 + kk];
-              s1 += adj[1 * PL1 + kk];
-              s2 += adj[2 * PL1 + kk];
-            }
+            for (int v = 0; v < 3; ++v) tap((ly + u) * W1 + (lx + v));
         } else {
           int rows[4], nr = 0, cols[4], nc = 0;
           for (int d = -1; d <= 1; ++d) {
@@ -770,12 +776,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
           if (gx == 1) cols[nc++] = lx;
           if (gx == W - 2) cols[nc++] = lx + 2;
           for (int u = 0; u < nr; ++u)
-            for (int v = 0; v < nc; ++v) {
-              const int kk = rows[u] * W1 + cols[v];
-              s0 += adj[0 * PL1 + kk];
-              s1 += adj[1 * PL1 + kk];
-              s2 += adj[2 * PL1 + kk];
-            }
+            for (int v = 0; v < nc; ++v) tap(rows[u] * W1 + cols[v]);
         }
         const float xv = est[c * PL2 + o2], yv = tgt[c * PL2 + o2];
         float ge = (s0 + 2.f * xv * s1 + yv * s2) * (1.f / 9.f);
@@ -805,7 +806,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       const float depth = decode_depth(invt[(ly + 2) * W2 + (lx + 2)], DRO_DEPTH_INV, 0.f, 0.f, &dd);
       Proj q;
       project(ki, kr, R, t, (float)gx, (float)gy, depth, H, W, q);
-      gdep[r] += project_backward(q, kr, R, gix[r], giy[r], acc, acc + 9);
+      gdep[r] += project_backward_pt(q, kr, R, t, depth, gix[r], giy[r], acc, acc + 9);
     }
     if (a.part_pose) {
       double sum[12];

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
       Proj q;
       project(ki, kr, R, t, u, v, depth, a.h, a.w, q);
       const float* g = gxy + ((size_t)(n * a.B + b) * P + p) * 2;
-      gd_total += project_backward(q, kr, R, g[0], g[1], acc, acc + 9);
+      gd_total += project_backward_pt(q, kr, R, t, depth, g[0], g[1], acc, acc + 9);
     }
     if (partial) {
       double sum[12];

@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "libdro_amd.so"))
+# DRO_LIB_PATH: an alternative build of the same library (A/B measurements)
+LIB_PATH = os.environ.get("DRO_LIB_PATH") or os.path.normpath(os.path.join(_HERE, "..", "libdro_amd.so"))
 
 _c_float_p = ctypes.c_void_p
 _lib = None

@@ -26,6 +26,7 @@ Execution plan (what changes versus the reference, never the math):
   * no host synchronisation anywhere: the step can be captured in a hipGraph.
 """
 import contextlib
+import os
 import logging
 
 import torch
@@ -68,13 +69,35 @@ def set_concurrent_blocks(enabled):
     _CONCURRENT_BLOCKS[0] = bool(enabled)
 
 
-def _pose_stream(device):
-    """The pose block's persistent side stream (created once, never during a
-    capture: the eager warm-up steps create it)."""
-    st = _SIDE_STREAMS.get(device)
+def _pose_stream(device, name="pose"):
+    """A persistent side stream: the pose block's, or cnet_depth's (created
+    once, never during a capture: the eager warm-up steps create them)."""
+    st = _SIDE_STREAMS.get((device, name))
     if st is None:
-        st = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+        # DRO_STREAM_PRIO=1 (A/B): the pose block's latency-bound chain at high
+        # priority, cnet_depth's own stream at the lowest
+        prio = 0
+        if os.environ.get("DRO_STREAM_PRIO", "0") == "1":
+            lo, hi = torch.cuda.Stream.priority_range()
+            prio = hi if name == "pose" else lo
+        st = _SIDE_STREAMS[(device, name)] = torch.cuda.Stream(device=device, priority=prio)
     return st
+
+
+# where cnet_depth runs: "pose" (default) -- first on the pose block's stream
+# (round 3), so its backward queues behind cnet_pose's there; "own" -- a stream
+# of its own, so its backward can start as soon as the depth block's gradient
+# reaches it.  Measured (round 5, A/B on one box): own 17.5-18.0 vs pose
+# 14.9-15.0 ms/step -- the third stream's encoder kernels starve the pose
+# block's latency-bound backward chain (5.7 instead of 1.6 ms in the in-graph
+# timeline, gpurun_out/r5e/timeline_own.log)
+_CNET_DEPTH_STREAM = [os.environ.get("DRO_CNET_DEPTH_STREAM", "pose")]
+
+
+def set_cnet_depth_stream(mode):
+    if mode not in ("pose", "own"):
+        raise ValueError(mode)
+    _CNET_DEPTH_STREAM[0] = mode
 
 
 class DepthPoseNet(nn.Module):
@@ -178,6 +201,8 @@ class DepthPoseNet(nn.Module):
         if self.iters > 0 and cuda:
             if pside is not None:
                 p_stream = d_stream = pside
+                if _CNET_DEPTH_STREAM[0] == "own":
+                    d_stream = _pose_stream(target_image.device, "cnet_depth")
             main = torch.cuda.current_stream(target_image.device)
             for st in {d_stream, p_stream} - {None}:
                 st.wait_stream(main)
@@ -190,7 +215,7 @@ class DepthPoseNet(nn.Module):
                 h_d, x_d = torch.tanh(h_d), torch.relu(x_d)
                 hip.ops.record_branch(("relu_seq", "ctx_d"), lambda: (x_d > 0).to(torch.uint8), x_d)
                 stamp("fwd:cnet_depth")
-                if d_stream is not None and d_stream is p_stream:
+                if d_stream is not None:
                     d_event = torch.cuda.Event()
                     d_event.record(d_stream)
             with torch.cuda.stream(p_stream) if p_stream is not None else _null():

@@ -42,9 +42,24 @@ import torch
 import torch.distributed as dist
 
 
+def graph_safe_nccl_env():
+    """Environment for RCCL collectives captured in hipGraphs, set before the
+    process group is created (explicit settings win).  The ProcessGroupNCCL
+    watchdog thread queries the events of the collectives it tracks; with the
+    flight recorder on (TORCH_NCCL_TRACE_BUFFER_SIZE > 0) it also tracks the
+    collectives issued inside a capture, and querying an event recorded in a
+    capturing stream aborts the process (measured round 5: 'operation not
+    permitted on an event last recorded in a capturing stream' in the
+    watchdog while the second flip graph was captured).  Events are also not
+    recycled between eager and captured collectives (the event cache)."""
+    os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "0")
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
 def init_distributed(backend=None):
     """Initialise the default process group from torchrun's env (no-op for 1 rank).
     Returns (rank, world_size, local_rank)."""
+    graph_safe_nccl_env()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

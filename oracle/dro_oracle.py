@@ -327,7 +327,7 @@ def _sign_code(d):
 
 
 # relative band around a clip threshold in which a recorded clamp decision is taken
-CLIP_TOL = 1e-5
+CLIP_TOL = 1e-4
 
 
 def photometric_map(est, tgt, ssim_w, C1, C2, clip_loss=0.0, cells=None, key=None, clip_index=None):

@@ -146,9 +146,10 @@ def _rccl_graph_worker(rank, port, out, in_graph):
     def stage(msg):
         print(f"[rccl-graph worker] {msg}", file=sys.stderr, flush=True)
 
-    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer, GraphedTrainStep, graph_safe_nccl_env
     from oracle import dro_oracle as O
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    graph_safe_nccl_env()
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     with torch.backends.cudnn.flags(enabled=False):
