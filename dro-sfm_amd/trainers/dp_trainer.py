@@ -45,15 +45,20 @@ import torch.distributed as dist
 def graph_safe_nccl_env():
     """Environment for RCCL collectives captured in hipGraphs, set before the
     process group is created (explicit settings win).  The ProcessGroupNCCL
-    watchdog thread queries the events of the collectives it tracks; with the
-    flight recorder on (TORCH_NCCL_TRACE_BUFFER_SIZE > 0) it also tracks the
-    collectives issued inside a capture, and querying an event recorded in a
-    capturing stream aborts the process (measured round 5: 'operation not
-    permitted on an event last recorded in a capturing stream' in the
-    watchdog while the second flip graph was captured).  Events are also not
-    recycled between eager and captured collectives (the event cache)."""
+    watchdog thread polls the events of the collectives it tracks; while a
+    step is being captured it has been seen to query an event last recorded
+    inside the capture and, with the default settings, to abort the process
+    from the watchdog thread ('operation not permitted on an event last
+    recorded in a capturing stream'; round 5, the world-1 RCCL capture test,
+    about 1 run in 7).  The flight recorder and the event cache (event
+    objects recycled between eager and captured collectives) are off, and a
+    HIP error seen by the watchdog's event queries is logged instead of
+    rethrown (TORCH_NCCL_RETHROW_CUDA_ERRORS=0): the collective itself is
+    unaffected, and a real device error still surfaces at the step's next
+    synchronisation."""
     os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "0")
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
 
 
 def init_distributed(backend=None):
