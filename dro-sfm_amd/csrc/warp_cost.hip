@@ -280,6 +280,279 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
   }
 }
 
+// ------------------------------------------------------------------ channels-last reference maps
+// The same cost and backward with the reference maps channel-contiguous
+// ([N,B,h,w,C], ref_layout 1).  The NCHW kernels above put one pixel on each
+// lane: a tap gather (and a scatter atomic) of a wave is coalesced only where
+// neighbouring pixels sample neighbouring reference pixels.  Where the warp
+// shears or folds the reference -- a state the untrained recurrence reaches
+// within a few steps -- every lane's tap lands on its own cache line, and the
+// backward went from 12 to 90 us per launch at the metric config
+// (tools/warp_state_probe.py: pixels per occupied cell 1.7, no compression,
+// only the locality is gone).  Here the lanes span 64 channels of ONE pixel:
+// each tap gather is one 256-B row and each scatter instruction one coalesced
+// row of atomics, whatever the geometry.  The target-side maps (fmap, the
+// incoming gradient, cost, d fmap) stay NCHW and pass through an LDS tile of
+// kClTP pixels x 64 channels with pixel-contiguous (coalesced) global accesses.
+// The projection is computed once per (pixel, ref) by the tile's first kClTP
+// threads; tap weights of out-of-image taps are 0 with clamped indices (the
+// sum is bit-identical to the guarded one, fma(x, 0, v) == v).
+constexpr int kClTP = 16;                 // pixels per block (4 per wave)
+constexpr int kClCH = kWave;              // channels per block (one per lane)
+constexpr int kClPPW = kClTP / 4;         // pixels per wave
+constexpr int kClNC = 4;                  // refs whose taps one phase computes (kClNC * kClTP threads)
+
+struct ClTaps {
+  int idx[kClTP][4];
+  float wgt[kClTP][4];
+  float tx[kClTP], ty[kClTP];
+  int key[kClTP];                         // bilinear cell, -1 - j when no tap is in the image
+  int ok[kClTP];                          // in-image taps (bit e), a property of the cell
+};
+
+// taps of refs n0 .. n0 + nc - 1: thread t < nc * kClTP takes (n0 + t / kClTP, pixel t % kClTP)
+__device__ __forceinline__ void cl_taps(const WarpArgs& a, int b, int n0, int nc, int p0, int pn,
+                                        int cells_block, ClTaps* L) {
+  const int t = threadIdx.x;
+  if (t >= nc * kClTP) return;
+  const int dn = t / kClTP, j = t - dn * kClTP, n = n0 + dn;
+  const int P = a.h * a.w;
+  int key = -1 - j;
+  float wg[4] = {0.f, 0.f, 0.f, 0.f}, tx = 0.f, ty = 0.f;
+  int ix4[4] = {0, 0, 0, 0}, okm = 0;
+  if (j < pn) {
+    const int p = p0 + j;
+    float ki[9], kr[9];
+    cams(a, b, ki, kr);
+    float dd;
+    const float depth = decode_depth(a.depth[b * P + p], a.depth_mode, a.min_disp, a.span, &dd);
+    float R[9], tt[3];
+    load_pose(a.pose + (size_t)(n * a.B + b) * pose_stride(a.pose_mode), a.pose_mode, R, tt);
+    Proj q;
+    project(ki, kr, R, tt, (float)(p % a.w), (float)(p / a.w), depth, a.h, a.w, q);
+    Taps T;
+    bilinear_taps(q.ix, q.iy, a.h, a.w, T);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ix4[e] = T.ok[e] ? T.idx[e] : 0;
+      wg[e] = T.ok[e] ? T.wgt[e] : 0.f;
+      okm |= T.ok[e] ? 1 << e : 0;
+    }
+    tx = T.tx;
+    ty = T.ty;
+    if (okm) key = ((int)floorf(q.iy) + 1) * (a.w + 1) + (int)floorf(q.ix) + 1;
+    if (a.cells && cells_block) a.cells[(size_t)(n * a.B + b) * P + p] = pack_cell(q.ix, q.iy);
+  }
+  ClTaps& Ln = L[dn];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    Ln.idx[j][e] = ix4[e];
+    Ln.wgt[j][e] = wg[e];
+  }
+  Ln.tx[j] = tx;
+  Ln.ty[j] = ty;
+  Ln.key[j] = key;
+  Ln.ok[j] = okm;
+}
+
+// tile[c][j] <- src[c * P + j] (c < cn, j < pn; 0 elsewhere), scaled
+__device__ __forceinline__ void cl_load_tile(float (*tile)[kClTP + 1], const float* __restrict__ src, int P,
+                                             int cn, int pn, float scale) {
+  for (int i = threadIdx.x; i < kClCH * kClTP; i += blockDim.x) {
+    const int c = i / kClTP, j = i - c * kClTP;
+    tile[c][j] = (c < cn && j < pn) ? src[(size_t)c * P + j] * scale : 0.f;
+  }
+}
+
+__device__ __forceinline__ void cl_store_tile(float (*tile)[kClTP + 1], float* __restrict__ dst, int P, int cn,
+                                              int pn, bool add) {
+  for (int i = threadIdx.x; i < kClCH * kClTP; i += blockDim.x) {
+    const int c = i / kClTP, j = i - c * kClTP;
+    if (c < cn && j < pn) {
+      float* o = dst + (size_t)c * P + j;
+      *o = add ? *o + tile[c][j] : tile[c][j];
+    }
+  }
+}
+
+// Sums of 8 per-lane values over the wave in 10 shuffles (a reduce-scatter
+// butterfly: halve the value set at lane distances 32, 16, 8, then sum within
+// 8 lanes): lane l ends with the total of value l >> 3 when (l & 7) == 0.
+__device__ __forceinline__ float wave_sum8(const float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+  float a4[4], a2[2], a1;
+  const bool u32 = lane & 32, u16 = lane & 16, u8 = lane & 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {             // keep 0..3 (lower half) or 4..7 (upper)
+    const float send = u32 ? v[i] : v[i + 4];
+    const float mine = u32 ? v[i + 4] : v[i];
+    a4[i] = mine + __shfl_xor(send, 32, kWave);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = u16 ? a4[i] : a4[i + 2];
+    const float mine = u16 ? a4[i + 2] : a4[i];
+    a2[i] = mine + __shfl_xor(send, 16, kWave);
+  }
+  {
+    const float send = u8 ? a2[0] : a2[1];
+    const float mine = u8 ? a2[1] : a2[0];
+    a1 = mine + __shfl_xor(send, 8, kWave);
+  }
+#pragma unroll
+  for (int o = 4; o >= 1; o >>= 1) a1 += __shfl_xor(a1, o, kWave);
+  return a1;
+}
+
+__global__ __launch_bounds__(256) void warp_cost_fwd_cl_kernel(WarpArgs a, float* __restrict__ cost) {
+  __shared__ float f_l[kClCH][kClTP + 1];
+  __shared__ float o_l[kClCH][kClTP + 1];
+  __shared__ ClTaps L[kClNC];
+  const int P = a.h * a.w;
+  const int p0 = blockIdx.x * kClTP, c0 = blockIdx.y * kClCH, b = blockIdx.z;
+  const int cn = min(kClCH, a.C - c0), pn = min(kClTP, P - p0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  cl_load_tile(f_l, a.fmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f);
+  float acc[kClPPW];
+#pragma unroll
+  for (int k = 0; k < kClPPW; ++k) acc[k] = 0.f;
+  for (int n0 = 0; n0 < a.N; n0 += kClNC) {
+    const int nc = min(kClNC, a.N - n0);
+    __syncthreads();                        // previous taps / output tile consumed
+    cl_taps(a, b, n0, nc, p0, pn, 0, L);
+    __syncthreads();
+    for (int dn = 0; dn < nc; ++dn) {
+      const int n = n0 + dn;
+      const ClTaps& T = L[dn];
+      const float* fr = a.fmap_ref + ((size_t)(n * a.B + b) * P) * a.C + c0 + lane;
+#pragma unroll
+      for (int k = 0; k < kClPPW; ++k) {
+        const int j = wave * kClPPW + k;
+        if (j < pn && lane < cn) {
+          float val = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) val += fr[(size_t)T.idx[j][e] * a.C] * T.wgt[j][e];
+          const float d = f_l[lane][j] - val;
+          if (a.reduce_mean)
+            acc[k] += d * d;
+          else
+            o_l[lane][j] = d * d;
+        }
+      }
+      if (!a.reduce_mean) {
+        __syncthreads();
+        cl_store_tile(o_l, cost + (((size_t)n * a.B + b) * a.C + c0) * P + p0, P, cn, pn, false);
+        __syncthreads();
+      }
+    }
+  }
+  if (a.reduce_mean) {
+    const float invN = (float)a.N;
+#pragma unroll
+    for (int k = 0; k < kClPPW; ++k) o_l[lane][wave * kClPPW + k] = acc[k] / invN;
+    __syncthreads();
+    cl_store_tile(o_l, cost + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, false);
+  }
+}
+
+// d/dfmap (NCHW, through the tile), d/dfmap_ref (channels-last, coalesced
+// atomics; consecutive pixels of a wave that share a bilinear cell are summed
+// in registers first) and gxy (the channel sums of a wave's 4 pixels in one
+// butterfly, one atomic per value and channel block).
+__global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, const float* __restrict__ gcost,
+                                                                    float* __restrict__ gfmap,
+                                                                    float* __restrict__ gfref,
+                                                                    float* __restrict__ gxy) {
+  __shared__ float f_l[kClCH][kClTP + 1];
+  __shared__ float g_l[kClNC][kClCH][kClTP + 1];
+  __shared__ ClTaps L[kClNC];
+  const int P = a.h * a.w;
+  const int p0 = blockIdx.x * kClTP, c0 = blockIdx.y * kClCH, b = blockIdx.z;
+  const int cn = min(kClCH, a.C - c0), pn = min(kClTP, P - p0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool live = lane < cn;
+  cl_load_tile(f_l, a.fmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f);
+  if (a.reduce_mean)
+    cl_load_tile(g_l[0], gcost + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f / (float)a.N);
+  float gf[kClPPW];
+#pragma unroll
+  for (int k = 0; k < kClPPW; ++k) gf[k] = 0.f;
+  for (int n0 = 0; n0 < a.N; n0 += kClNC) {
+    const int nc = min(kClNC, a.N - n0);
+    __syncthreads();
+    if (!a.reduce_mean)
+      for (int dn = 0; dn < nc; ++dn)
+        cl_load_tile(g_l[dn], gcost + (((size_t)(n0 + dn) * a.B + b) * a.C + c0) * P + p0, P, cn, pn, 1.f);
+    cl_taps(a, b, n0, nc, p0, pn, blockIdx.y == 0, L);
+    __syncthreads();
+    for (int dn = 0; dn < nc; ++dn) {
+      const ClTaps& T = L[dn];
+      const float (*g_t)[kClTP + 1] = g_l[a.reduce_mean ? 0 : dn];
+      const size_t img = (size_t)((n0 + dn) * a.B + b) * P;
+      const float* fr = a.fmap_ref + img * a.C + c0 + lane;
+      float* gr = gfref ? gfref + img * a.C + c0 + lane : nullptr;
+      int pkey = -1;                        // cell of the pending scatter (wave-uniform)
+      int pidx[4] = {0, 0, 0, 0}, pok = 0;
+      float pend[4] = {0.f, 0.f, 0.f, 0.f};
+      float gxy8[8];
+#pragma unroll
+      for (int k = 0; k < kClPPW; ++k) {
+        const int j = wave * kClPPW + k;
+        float v[4], gw = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)   // out-of-image taps read 0 (their values enter d/d(ix,iy))
+          v[e] = (live && j < pn && ((T.ok[j] >> e) & 1)) ? fr[(size_t)T.idx[j][e] * a.C] : 0.f;
+        if (live && j < pn) {
+          // one expression, as warp_cost_bwd_feat_kernel (the same contraction)
+          const float val = v[0] * T.wgt[j][0] + v[1] * T.wgt[j][1] + v[2] * T.wgt[j][2] + v[3] * T.wgt[j][3];
+          const float gd = 2.f * (f_l[lane][j] - val) * g_t[lane][j];
+          gf[k] += gd;
+          gw = -gd;
+        }
+        const float ty = T.ty[j], tx = T.tx[j];
+        gxy8[2 * k] = gw * ((v[1] - v[0]) * (1.f - ty) + (v[3] - v[2]) * ty);
+        gxy8[2 * k + 1] = gw * ((v[2] - v[0]) * (1.f - tx) + (v[3] - v[1]) * tx);
+        if (gr && j < pn) {
+          const int key = T.key[j];
+          if (key != pkey) {                // flush the previous cell's sums
+            if (pkey >= 0 && live) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C, pend[e]);
+            }
+            pkey = key;
+            pok = T.ok[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              pidx[e] = T.idx[j][e];
+              pend[e] = 0.f;
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pend[e] += gw * T.wgt[j][e];
+        }
+      }
+      if (gr && pkey >= 0 && live) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C, pend[e]);
+      }
+      if (gxy) {
+        const float sum = wave_sum8(gxy8);
+        const int vi = lane >> 3, j = wave * kClPPW + (vi >> 1);
+        if ((lane & 7) == 0 && j < pn) atomicAdd(gxy + (img + p0 + j) * 2 + (vi & 1), sum);
+      }
+    }
+  }
+  if (gfmap) {
+    __syncthreads();                        // f_l reused as the output tile
+#pragma unroll
+    for (int k = 0; k < kClPPW; ++k) f_l[lane][wave * kClPPW + k] = gf[k];
+    __syncthreads();
+    cl_store_tile(f_l, gfmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, a.acc_fmap != 0);
+  }
+}
+
 // ------------------------------------------------------------------ backward: geometry side
 // One thread per (b, pixel): chain gxy through the projection to the depth
 // input (summed over refs, no atomics) and to per-workgroup pose partials.
@@ -577,7 +850,7 @@ extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, c
                                      int depth_mode, float min_disp, float max_disp,
                                      const float* K, const float* ref_K, float scale,
                                      const float* pose, int pose_mode, int B, int N, int C, int h,
-                                     int w, int reduce_mean, float* cost, void* stream) {
+                                     int w, int reduce_mean, int ref_layout, float* cost, void* stream) {
   int st = check_common(fmap, fmap_ref, K, ref_K, pose, pose_mode, B, N, C, h, w);
   if (st) return st;
   if (!depth || !cost) {
@@ -588,9 +861,18 @@ extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, c
     set_error("warp_cost_forward: unknown depth_mode");
     return DRO_E_MODE;
   }
+  if (ref_layout != 0 && ref_layout != 1) {
+    set_error("warp_cost_forward: ref_layout must be 0 (NCHW) or 1 (channels-last)");
+    return DRO_E_MODE;
+  }
   WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
                          pose, pose_mode, B, N, C, h, w, reduce_mean);
   const int P = h * w;
+  if (ref_layout == 1) {
+    dim3 grid((P + kClTP - 1) / kClTP, (C + kClCH - 1) / kClCH, B);
+    hipLaunchKernelGGL(warp_cost_fwd_cl_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, cost);
+    return launch_status("warp_cost_fwd_cl_kernel launch failed");
+  }
   dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
   hipLaunchKernelGGL(warp_cost_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a, cost);
   return launch_status("warp_cost_fwd_kernel launch failed");
@@ -600,7 +882,7 @@ extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, c
 template <bool SAMPLE>
 static int warp_backward(WarpArgs a, const float* grad_out, float* grad_fmap, float* grad_fmap_ref,
                          float* grad_depth, float* grad_pose, int accumulate, void* workspace, int* cells,
-                         hipStream_t s) {
+                         int ref_layout, hipStream_t s) {
   const int B = a.B, N = a.N, C = a.C, h = a.h, w = a.w;
   const bool geo = grad_depth || grad_pose;
   if (geo && !workspace) {
@@ -624,7 +906,12 @@ static int warp_backward(WarpArgs a, const float* grad_out, float* grad_fmap, fl
       (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s)))
     return st;
   if (gxy && (st = launch_zero(gxy, (size_t)N * B * P * 2, s))) return st;
-  if (grad_fmap || grad_fmap_ref || gxy || cells) {
+  if (ref_layout == 1 && (grad_fmap || grad_fmap_ref || gxy || cells)) {
+    dim3 grid((P + kClTP - 1) / kClTP, (C + kClCH - 1) / kClCH, B);
+    hipLaunchKernelGGL(warp_cost_bwd_feat_cl_kernel, grid, dim3(256), 0, s, a, grad_out, grad_fmap,
+                       grad_fmap_ref, gxy);
+    if ((st = launch_status("warp_cost_bwd_feat_cl_kernel launch failed"))) return st;
+  } else if (grad_fmap || grad_fmap_ref || gxy || cells) {
     dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);
     hipLaunchKernelGGL(warp_cost_bwd_feat_kernel<SAMPLE>, grid, dim3(256), 0, s, a, grad_out, grad_fmap,
                        grad_fmap_ref, gxy);
@@ -645,7 +932,7 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
                                       int depth_mode, float min_disp, float max_disp,
                                       const float* K, const float* ref_K, float scale,
                                       const float* pose, int pose_mode, int B, int N, int C,
-                                      int h, int w, int reduce_mean, const float* grad_cost,
+                                      int h, int w, int reduce_mean, int ref_layout, const float* grad_cost,
                                       float* grad_fmap, float* grad_fmap_ref, float* grad_depth,
                                       float* grad_pose, int accumulate, void* workspace, int* cells,
                                       void* stream) {
@@ -655,10 +942,14 @@ extern "C" int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, 
     set_error("warp_cost_backward: NULL depth/grad_cost");
     return DRO_E_NULL;
   }
+  if (ref_layout != 0 && ref_layout != 1) {
+    set_error("warp_cost_backward: ref_layout must be 0 (NCHW) or 1 (channels-last)");
+    return DRO_E_MODE;
+  }
   WarpArgs a = make_args(fmap, fmap_ref, depth, depth_mode, min_disp, max_disp, K, ref_K, scale,
                          pose, pose_mode, B, N, C, h, w, reduce_mean);
   return warp_backward<false>(a, grad_cost, grad_fmap, grad_fmap_ref, grad_depth, grad_pose, accumulate,
-                              workspace, cells, (hipStream_t)stream);
+                              workspace, cells, ref_layout, (hipStream_t)stream);
 }
 
 extern "C" int dro_view_synthesis_forward(const float* ref_image, const float* depth, int depth_mode,
@@ -699,7 +990,7 @@ extern "C" int dro_view_synthesis_backward(const float* ref_image, const float* 
   WarpArgs a = make_args(nullptr, ref_image, depth, depth_mode, min_disp, max_disp, K, ref_K, scale, pose,
                          pose_mode, B, N, C, H, W, 0);
   return warp_backward<true>(a, grad_warped, nullptr, grad_ref_image, grad_depth, grad_pose, 0, workspace,
-                             cells, (hipStream_t)stream);
+                             cells, 0, (hipStream_t)stream);
 }
 
 extern "C" int dro_plane_sweep_forward(const float* fmap, const float* fmap_ref, const float* disp,

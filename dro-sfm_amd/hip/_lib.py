@@ -39,9 +39,9 @@ def load():
     _sig(lib.dro_abi_version)
     _sig(lib.dro_timestamp, P, I, S)
     _sig(lib.dro_wall_clock_hz, P)
-    _sig(lib.dro_warp_cost_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, P, S)
+    _sig(lib.dro_warp_cost_forward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, I, P, S)
     _sig(lib.dro_warp_cost_workspace_bytes, I, I, I, I, restype=Z)
-    _sig(lib.dro_warp_cost_backward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I,
+    _sig(lib.dro_warp_cost_backward, P, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, I, I,
          P, P, P, P, P, I, P, P, S)
     _sig(lib.dro_view_synthesis_forward, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, P, S)
     _sig(lib.dro_view_synthesis_backward, P, P, I, F, F, P, P, F, P, I, I, I, I, I, I, P, P, P, P, P, P, S)

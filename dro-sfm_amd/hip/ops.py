@@ -44,7 +44,10 @@ class GradSinkState:
     __slots__ = ("buf", "written")
 
     def __init__(self, like):
-        self.buf = torch.empty(like.shape, device=like.device, dtype=like.dtype)
+        # channels-last reference maps keep their layout (the cost kernels
+        # scatter into it); everything else gets a dense NCHW buffer
+        self.buf = (torch.empty_like(like) if _is_channels_last_refs(like)
+                    else torch.empty(like.shape, device=like.device, dtype=like.dtype))
         self.written = False
 
     def target(self):
@@ -100,7 +103,7 @@ def grad_sink(x):
     own backward reduces it once."""
     if not (_SINKS[0] and torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
         return x
-    if not x.is_contiguous() and x.dim() != 4:
+    if not x.is_contiguous() and x.dim() != 4 and not _is_channels_last_refs(x):
         # broadcast (expanded) views: only the 4-D pose maps the convs read; dense
         # tensors of any rank (the [N,B,C,h,w] reference feature maps) qualify
         return x
@@ -193,6 +196,25 @@ Tensor = torch.Tensor
 
 
 # ------------------------------------------------------------------------- warp + feature cost
+def _is_channels_last_refs(t):
+    """[N,B,C,h,w] stored as a dense [N,B,h,w,C] (channels_last_refs)."""
+    return t.dim() == 5 and not t.is_contiguous() and t.permute(0, 1, 3, 4, 2).is_contiguous()
+
+
+def _ref_layout(t):
+    """(tensor, ref_layout) for the C ABI: channels-last reference maps pass
+    as they are (1), anything else as a contiguous NCHW tensor (0)."""
+    return (t, 1) if _is_channels_last_refs(t) else (t.contiguous(), 0)
+
+
+def channels_last_refs(fmap_ref):
+    """The [N,B,C,h,w] reference feature maps re-laid channel-contiguous
+    ([N,B,h,w,C] memory, same shape): the cost kernels then gather and scatter
+    whole channel rows (dro_warp_cost_forward ref_layout 1).  One copy each
+    way per training step, shared by every cost call."""
+    return fmap_ref.permute(0, 1, 3, 4, 2).contiguous().permute(0, 1, 4, 2, 3)
+
+
 @torch.library.custom_op("dro::warp_cost", mutates_args=())
 def _warp_cost_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
                   depth_mode: int, min_disp: float, max_disp: float, scale: float, pose_mode: int,
@@ -205,11 +227,13 @@ def _warp_cost_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tensor, K
     require_device(fmap, fmap_ref, depth, pose, K, ref_K, what="warp_cost")
     B, C, h, w = fmap.shape
     N = fmap_ref.shape[0]
-    fmap, fmap_ref, depth = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous()
+    fmap, depth = fmap.contiguous(), depth.contiguous()
+    fmap_ref, layout = _ref_layout(fmap_ref)
     cost = torch.empty((B, C, h, w) if reduce_mean else (N, B, C, h, w), device=fmap.device)
     check(lib.dro_warp_cost_forward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode, min_disp, max_disp,
                                     ptr(K.contiguous()), ptr(ref_K.contiguous()), scale, ptr(pose.contiguous()),
-                                    pose_mode, B, N, C, h, w, int(reduce_mean), ptr(cost), stream_of(fmap)),
+                                    pose_mode, B, N, C, h, w, int(reduce_mean), layout, ptr(cost),
+                                    stream_of(fmap)),
           "dro_warp_cost_forward")
     return cost
 
@@ -237,8 +261,11 @@ def _warp_cost_bwd_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tenso
     B, C, h, w = fmap.shape
     N = fmap_ref.shape[0]
     dev = fmap.device
-    fmap, fmap_ref, depth, pose = fmap.contiguous(), fmap_ref.contiguous(), depth.contiguous(), pose.contiguous()
+    fmap, depth, pose = fmap.contiguous(), depth.contiguous(), pose.contiguous()
+    fmap_ref, layout = _ref_layout(fmap_ref)
     K, ref_K = K.contiguous(), ref_K.contiguous()
+    if grad_fmap_ref_out is not None and _is_channels_last_refs(grad_fmap_ref_out) != bool(layout):
+        raise RuntimeError("warp_cost backward: the fmap_ref gradient sink's layout differs from fmap_ref's")
     g_f = grad_fmap_out if grad_fmap_out is not None else (torch.empty_like(fmap) if need_fmap else None)
     g_r = grad_fmap_ref_out if grad_fmap_ref_out is not None else (
         torch.empty_like(fmap_ref) if need_fmap_ref else None)
@@ -249,7 +276,8 @@ def _warp_cost_bwd_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tenso
         ws = torch.empty(lib.dro_warp_cost_workspace_bytes(B, N, h, w) // 4 + 1, device=dev)
     check(lib.dro_warp_cost_backward(ptr(fmap), ptr(fmap_ref), ptr(depth), depth_mode, min_disp, max_disp,
                                      ptr(K), ptr(ref_K), scale, ptr(pose), pose_mode, B, N, C, h, w,
-                                     int(reduce_mean), ptr(grad_cost.contiguous()), ptr(g_f), ptr(g_r), ptr(g_d),
+                                     int(reduce_mean), layout, ptr(grad_cost.contiguous()), ptr(g_f), ptr(g_r),
+                                     ptr(g_d),
                                      ptr(g_p), accumulate, ptr(ws), ptr(cells), stream_of(fmap)),
           "dro_warp_cost_backward")
     out = lambda g, own: g if (g is not None and not own) else _none_like(dev)

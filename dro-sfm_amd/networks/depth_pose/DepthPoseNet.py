@@ -55,6 +55,9 @@ def parse_version(version):
 
 _SIDE_STREAMS = {}
 
+# the cost calls' reference maps channels-last (DRO_CL_REFS=0: NCHW, A/B)
+_CL_REFS = os.environ.get("DRO_CL_REFS", "1") != "0"
+
 
 _CONCURRENT_BLOCKS = [True]
 
@@ -233,12 +236,16 @@ class DepthPoseNet(nn.Module):
         h, w = fmaps.shape[2:]
         fmap1_raw, frefs_raw = torch.split(fmaps, [B, N * B], 0)
         frefs_raw = frefs_raw.view(N, B, C, h, w)       # free view: all refs, one tensor
+        # the cost calls read the reference maps channel-contiguous (one copy per
+        # step each way: their gathers and scatters then stay coalesced however
+        # the warp shears the reference, hip.ops.channels_last_refs)
+        frefs_cl = hip.ops.channels_last_refs(frefs_raw) if _CL_REFS else frefs_raw
         # every cost call reads the same feature maps: their gradients are summed
         # in place by the warp-cost backward (no per-call add launches)
-        fmap1, frefs = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_raw)
+        fmap1, frefs = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_cl)
 
         # initial poses of all refs in one pass: cat([fmap1, fmap_ref_j]) per ref j
-        pair = torch.cat([fmap1.unsqueeze(0).expand(N, B, C, h, w), frefs], 2).view(N * B, 2 * C, h, w)
+        pair = torch.cat([fmap1.unsqueeze(0).expand(N, B, C, h, w), frefs_raw], 2).view(N * B, 2 * C, h, w)
         poses = self.pose_head(pair).view(N, B, 6)
 
         disp = stamp_grad(self.depth_head(fmap1, act_fn=torch.sigmoid), "bwd:init_depth_head")
@@ -278,7 +285,7 @@ class DepthPoseNet(nn.Module):
                 pside.wait_stream(main)
                 with torch.cuda.stream(pside):
                     x_p = hip.grad_sink(x_p)
-                    fmap1_p, frefs_p = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_raw)
+                    fmap1_p, frefs_p = hip.grad_sink(fmap1_raw), hip.grad_sink(frefs_cl)
         for it in range(self.iters):
             disp = disp.detach()
             poses = poses.detach()

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -68,13 +68,17 @@ int dro_wall_clock_hz(long long* hz);   /* that counter's rate */
  *   fmap [B,C,h,w]; fmap_ref [N,B,C,h,w]; depth [B,1,h,w]; K, ref_K [B,3,3];
  *   pose [N,B,6|12]; cost [B,C,h,w] (reduce_mean) or [N,B,C,h,w].
  * scale == 1.0f leaves K untouched (Camera.scaled returns self, camera.py:103-104).
+ * ref_layout: 0 = fmap_ref (and grad_fmap_ref) NCHW [N,B,C,h,w]; 1 =
+ * channels-last [N,B,h,w,C] -- the tap gathers and scatter atomics are then
+ * coalesced over channels whatever the warp's geometry (the layout the
+ * training step uses; the other maps stay NCHW either way).
  * ---------------------------------------------------------------------- */
 int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, const float* depth,
                           int depth_mode, float min_disp, float max_disp,
                           const float* K, const float* ref_K, float scale,
                           const float* pose, int pose_mode,
                           int B, int N, int C, int h, int w, int reduce_mean,
-                          float* cost, void* stream);
+                          int ref_layout, float* cost, void* stream);
 
 size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w);
 
@@ -94,7 +98,7 @@ int dro_warp_cost_backward(const float* fmap, const float* fmap_ref, const float
                            const float* K, const float* ref_K, float scale,
                            const float* pose, int pose_mode,
                            int B, int N, int C, int h, int w, int reduce_mean,
-                           const float* grad_cost, float* grad_fmap, float* grad_fmap_ref,
+                           int ref_layout, const float* grad_cost, float* grad_fmap, float* grad_fmap_ref,
                            float* grad_depth, float* grad_pose, int accumulate, void* workspace,
                            int* cells, void* stream);
 

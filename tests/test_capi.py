@@ -34,13 +34,13 @@ def test_header_matches_exports(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dro_abi_version() == 6
+    assert lib.dro_abi_version() == 7
 
 
 def test_null_arguments_rejected(lib):
     NULL = None
     st = lib.dro_warp_cost_forward(NULL, NULL, NULL, 0, 0.0, 0.0, NULL, NULL, 0.125, NULL, 0,
-                                   1, 1, 1, 2, 2, 1, NULL, NULL)
+                                   1, 1, 1, 2, 2, 1, 0, NULL, NULL)
     assert st == -1
     assert b"NULL" in lib.dro_last_error()
     st = lib.dro_photometric_forward(NULL, NULL, NULL, NULL, NULL, NULL, 0, 1, 1, 1, 8, 8, 0.85,
@@ -54,10 +54,13 @@ def test_bad_sizes_and_modes_rejected(lib):
     buf = (ctypes.c_float * 64)()
     p = ctypes.cast(buf, ctypes.c_void_p)
     # h = 1 is out of range (normalisation divides by h-1)
-    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 0, 1, 1, 1, 1, 4, 1,
+    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 0, 1, 1, 1, 1, 4, 1, 0,
                                      p, None) == -2
     # unknown pose mode
-    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 7, 1, 1, 1, 2, 2, 1,
+    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 7, 1, 1, 1, 2, 2, 1, 0,
+                                     p, None) == -3
+    # unknown reference layout
+    assert lib.dro_warp_cost_forward(p, p, p, 0, 0.0, 0.0, p, p, 0.125, p, 0, 1, 1, 1, 2, 2, 1, 2,
                                      p, None) == -3
     # automask needs the min reduction
     assert lib.dro_photometric_forward(p, p, p, p, p, p, 0, 1, 1, 1, 8, 8, 0.85, 1e-4, 9e-4, 1e-3,

@@ -108,7 +108,18 @@ def test_plane_sweep_equals_per_plane_warp_cost(hip, w):
         assert torch.equal(vol[:, d], ref), d
 
 
-def test_warp_cost_kitti_size_vs_oracle(hip):
+def _ref_leaf(hip, frefs, layout):
+    """The reference maps on the device as a leaf, NCHW or channels-last
+    (hip.ops.channels_last_refs: the layout the training step hands the cost)."""
+    t = frefs.to(DEV)
+    if layout == "cl":
+        t = hip.ops.channels_last_refs(t)
+        assert hip.ops._is_channels_last_refs(t)
+    return t.detach().requires_grad_(True)
+
+
+@pytest.mark.parametrize("layout", ["nchw", "cl"])
+def test_warp_cost_kitti_size_vs_oracle(hip, layout):
     """Metric-config size: B=2, C=128, 24x80, N=2 refs, depth mean + per-ref pose cost."""
     g = torch.Generator().manual_seed(7)
     B, C, h, w, N = 2, 128, 24, 80, 2
@@ -128,7 +139,8 @@ def test_warp_cost_kitti_size_vs_oracle(hip):
     cp = torch.stack([O.get_cost_each(pc[j], fc, rc[j], depth_fixed, K, K, 1 / 8) for j in range(N)])
     ((cm * Gm).sum() + (cp * Gp).sum()).backward()
     # HIP
-    dg, fg, rg, pg = (t.to(DEV).requires_grad_(True) for t in (disp, fmap, frefs, poses))
+    dg, fg, pg = (t.to(DEV).requires_grad_(True) for t in (disp, fmap, poses))
+    rg = _ref_leaf(hip, frefs, layout)
     Kd = K.to(DEV)
     hm = hip.warp_cost(fg, rg, dg, poses.to(DEV), Kd, depth_mode=hip.DEPTH_DISP, min_depth=0.5,
                        max_depth=80.0, reduce_mean=True)
@@ -142,7 +154,8 @@ def test_warp_cost_kitti_size_vs_oracle(hip):
     assert rel(pg.grad, pc.grad) < TOL
 
 
-def test_warp_cost_backward_converging_warp(hip):
+@pytest.mark.parametrize("layout", ["nchw", "cl"])
+def test_warp_cost_backward_converging_warp(hip, layout):
     """A warp that compresses the reference ~10x (camera moved back 9 depths:
     ten consecutive target pixels sample one reference cell) next to an
     ordinary one: the fmap_ref scatter merges each run of lanes sharing a cell
@@ -164,7 +177,8 @@ def test_warp_cost_backward_converging_warp(hip):
     cp = torch.stack([O.get_cost_each(pc[j], fc, rc[j], depth.to(dt), K.to(dt), K.to(dt), 1 / 8)
                       for j in range(N)])
     ((cm * Gm.to(dt)).sum() + (cp * Gp.to(dt)).sum()).backward()
-    dg, fg, rg, pg = (t.to(DEV).requires_grad_(True) for t in (depth, fmap, frefs, poses))
+    dg, fg, pg = (t.to(DEV).requires_grad_(True) for t in (depth, fmap, poses))
+    rg = _ref_leaf(hip, frefs, layout)
     Kd = K.to(DEV)
     hm = hip.warp_cost(fg, rg, dg, poses.to(DEV), Kd, reduce_mean=True)
     hp = hip.warp_cost(fg, rg, depth.to(DEV), pg, Kd, reduce_mean=False)
@@ -175,6 +189,43 @@ def test_warp_cost_backward_converging_warp(hip):
     # the compressed ref's gradient really is concentrated: > 4 target pixels per touched cell
     touched = int((rc.grad[0].abs().sum((0, 1)) > 0).sum())
     assert touched * 4 < B * h * w, touched
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 24, 80, 2), (3, 22, 7, 13, 3), (1, 70, 5, 37, 1)])
+@pytest.mark.parametrize("reduce_mean", [True, False])
+def test_warp_cost_channels_last_matches_nchw(hip, shape, reduce_mean):
+    """Channels-last reference maps (ref_layout 1, warp_cost_*_cl_kernel) against
+    the NCHW kernels on the same inputs, including shapes no tile divides
+    (C = 22 and 70 against 64-channel blocks, 7x13 and 5x37 pixels against
+    16-pixel tiles) and a sheared warp (rotation about the optical axis:
+    neighbouring pixels sample far-apart reference pixels).  The cost and
+    d fmap are the same arithmetic per element: bit-identical.  d fmap_ref
+    (atomics in another order, runs of a cell summed first) and the depth /
+    pose gradients (channel sums in another order) within 1e-5; the bilinear
+    cells recorded by both backwards identical."""
+    B, C, h, w, N = shape
+    g = torch.Generator().manual_seed(23)
+    K = kitti_K(B, W=8 * w, H=8 * h)
+    fmap, frefs = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    disp = torch.rand(B, 1, h, w, generator=g)
+    poses = torch.cat([0.2 * torch.randn(N, B, 3, generator=g), 0.05 * torch.randn(N, B, 3, generator=g)], 2)
+    poses[0, :, 5] = 0.6                                    # ref 0 rolled: a sheared warp
+    G = torch.randn(*((B, C, h, w) if reduce_mean else (N, B, C, h, w)), generator=g).to(DEV)
+    out = {}
+    for layout in ("nchw", "cl"):
+        dg, fg, pg = (t.to(DEV).requires_grad_(True) for t in (disp, fmap, poses))
+        rg = _ref_leaf(hip, frefs, layout)
+        with hip.ops.record_bilinear_cells() as rec:
+            cost = hip.warp_cost(fg, rg, dg, pg, K.to(DEV), depth_mode=hip.DEPTH_DISP, min_depth=0.5,
+                                 max_depth=80.0, reduce_mean=reduce_mean, tag="c")
+        (cost * G).sum().backward()
+        out[layout] = (cost.detach(), fg.grad, rg.grad.contiguous(), dg.grad, pg.grad, rec.calls[0][1])
+    a, b = out["nchw"], out["cl"]
+    assert torch.equal(a[0], b[0]), "cost"
+    assert torch.equal(a[1], b[1]), "d fmap"
+    assert torch.equal(a[5], b[5]), "recorded cells"
+    for k, name in ((2, "d fmap_ref"), (3, "d depth"), (4, "d pose")):
+        assert rel(b[k], a[k]) < 1e-5, (name, rel(b[k], a[k]))
 
 
 def test_warp_cost_forward_deterministic(hip):
