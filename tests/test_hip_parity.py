@@ -635,6 +635,20 @@ def cells_from_record(rec):
     return O.cells_from_calls(rec.calls)
 
 
+# The oracle takes the product's recorded cell only within CELL_TOL of a grid
+# line, and only where it differs from the fp64 coordinate's own cell does it
+# count in PIN_STATS["cells"]: fp32 rounding moves a coordinate across a line
+# for ~1e-5 of the samples.  Far more pinned samples than that would mean
+# the product's warps had drifted from the oracle's -- fail loudly.
+PIN_CELL_FRAC = 1e-3
+
+
+def _assert_pinning_bounded(pinned, cells):
+    total = sum(int(v.numel()) for k, v in cells.items()
+                if isinstance(k, tuple) and k and k[0] in ("depth", "pose", "photo"))
+    assert pinned <= PIN_CELL_FRAC * total + 16, ("bilinear cells pinned", pinned, "of", total)
+
+
 def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=False, cells=None,
                   want_preds=False):
     """Oracle loss and parameter gradients (and, want_preds, the net's
@@ -648,8 +662,11 @@ def _oracle_grads(spec, version, mind, maxd, batch, kind, dt, forced=None, flip=
     b = {k: (v.clone().to(dt) if torch.is_tensor(v) and v.is_floating_point() else
              ([t.to(dt) for t in v] if isinstance(v, list) else v)) for k, v in batch.items()}   # (flip edits K)
     book = O.Cells(forced=cells) if cells is not None else None
+    pinned0 = O.PIN_STATS["cells"]
     out = O.train_step_loss(p, version, mind, maxd, b, kind=kind, forced_selection=forced, flip=flip, cells=book)
     out["loss"].sum().backward()
+    if cells is not None:
+        _assert_pinning_bounded(O.PIN_STATS["cells"] - pinned0, cells)
     grads = {k: v.grad for k, v in p.items() if getattr(v, "grad", None) is not None}
     if want_preds:
         return out["loss"].detach(), grads, out["preds"]
