@@ -43,6 +43,7 @@ afresh) and the split buffers are saved for the backward.
 """
 import contextlib
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -111,9 +112,12 @@ def weight_grad_scope():
         _GEN[1] -= 1
 
 
-_XCONV = [False]   # measured: not faster than the f32 engine at the step's shapes
+# measured: not faster than the f32 engine at the step's shapes;
+# DRO_SPLIT_ENGINE=all|3x3fwd turns it on for A/B runs
+_XCONV = [os.environ.get("DRO_SPLIT_ENGINE", "") in ("all", "3x3fwd")]
 _XSHAPES = {(1, 5), (5, 1), (3, 3), (1, 1)}
-_XPOLICY = ["all"]  # "all": every xconv shape, fwd + data grad; "3x3fwd": 3x3 forwards only
+# "all": every xconv shape, fwd + data grad; "3x3fwd": 3x3 forwards only
+_XPOLICY = [os.environ.get("DRO_SPLIT_ENGINE", "") or "all"]
 _SPLITS = {}       # (data_ptr, shape, device) -> [generation, fwd split, bwd split]
 
 
