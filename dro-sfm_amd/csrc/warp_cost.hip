@@ -297,7 +297,13 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_kernel(
 // The projection is computed once per (pixel, ref) by the tile's first kClTP
 // threads; tap weights of out-of-image taps are 0 with clamped indices (the
 // sum is bit-identical to the guarded one, fma(x, 0, v) == v).
-constexpr int kClTP = 16;                 // pixels per block (4 per wave)
+#ifndef DRO_WARP_CL_TP
+#define DRO_WARP_CL_TP 8
+#endif
+// pixels per block (kClTP / 4 per wave).  Measured on recorded training states
+// (tools/ab_warp_tile.sh, rocprof per launch): 4 / 8 / 16 / 32 pixels ->
+// backward 17.8 / 11.0-11.5 / 13.6 / 22.8 us, forward 12.3 / 9.3-9.4 / 10.7 / 14.6 us
+constexpr int kClTP = DRO_WARP_CL_TP;
 constexpr int kClCH = kWave;              // channels per block (one per lane)
 constexpr int kClPPW = kClTP / 4;         // pixels per wave
 constexpr int kClNC = 4;                  // refs whose taps one phase computes (kClNC * kClTP threads)
@@ -494,7 +500,7 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, 
       int pkey = -1;                        // cell of the pending scatter (wave-uniform)
       int pidx[4] = {0, 0, 0, 0}, pok = 0;
       float pend[4] = {0.f, 0.f, 0.f, 0.f};
-      float gxy8[8];
+      float gxyv[2 * kClPPW];
 #pragma unroll
       for (int k = 0; k < kClPPW; ++k) {
         const int j = wave * kClPPW + k;
@@ -510,8 +516,8 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, 
           gw = -gd;
         }
         const float ty = T.ty[j], tx = T.tx[j];
-        gxy8[2 * k] = gw * ((v[1] - v[0]) * (1.f - ty) + (v[3] - v[2]) * ty);
-        gxy8[2 * k + 1] = gw * ((v[2] - v[0]) * (1.f - tx) + (v[3] - v[1]) * tx);
+        gxyv[2 * k] = gw * ((v[1] - v[0]) * (1.f - ty) + (v[3] - v[2]) * ty);
+        gxyv[2 * k + 1] = gw * ((v[2] - v[0]) * (1.f - tx) + (v[3] - v[1]) * tx);
         if (gr && j < pn) {
           const int key = T.key[j];
           if (key != pkey) {                // flush the previous cell's sums
@@ -537,10 +543,16 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, 
         for (int e = 0; e < 4; ++e)
           if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C, pend[e]);
       }
-      if (gxy) {
-        const float sum = wave_sum8(gxy8);
-        const int vi = lane >> 3, j = wave * kClPPW + (vi >> 1);
-        if ((lane & 7) == 0 && j < pn) atomicAdd(gxy + (img + p0 + j) * 2 + (vi & 1), sum);
+      if (gxy) {   // 8 values (4 pixels x (ix, iy)) per butterfly
+#pragma unroll
+        for (int g0 = 0; g0 < 2 * kClPPW; g0 += 8) {
+          float v8[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v8[i] = g0 + i < 2 * kClPPW ? gxyv[g0 + i] : 0.f;
+          const float sum = wave_sum8(v8);
+          const int vi = g0 + (lane >> 3), j = wave * kClPPW + (vi >> 1);
+          if ((lane & 7) == 0 && vi < 2 * kClPPW && j < pn) atomicAdd(gxy + (img + p0 + j) * 2 + (vi & 1), sum);
+        }
       }
     }
   }
