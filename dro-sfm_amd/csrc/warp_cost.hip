@@ -362,17 +362,19 @@ __device__ __forceinline__ void cl_taps(const WarpArgs& a, int b, int n0, int nc
 }
 
 // tile[c][j] <- src[c * P + j] (c < cn, j < pn; 0 elsewhere), scaled
+template <int CB = kClCH>
 __device__ __forceinline__ void cl_load_tile(float (*tile)[kClTP + 1], const float* __restrict__ src, int P,
                                              int cn, int pn, float scale) {
-  for (int i = threadIdx.x; i < kClCH * kClTP; i += blockDim.x) {
+  for (int i = threadIdx.x; i < CB * kClTP; i += blockDim.x) {
     const int c = i / kClTP, j = i - c * kClTP;
     tile[c][j] = (c < cn && j < pn) ? src[(size_t)c * P + j] * scale : 0.f;
   }
 }
 
+template <int CB = kClCH>
 __device__ __forceinline__ void cl_store_tile(float (*tile)[kClTP + 1], float* __restrict__ dst, int P, int cn,
                                               int pn, bool add) {
-  for (int i = threadIdx.x; i < kClCH * kClTP; i += blockDim.x) {
+  for (int i = threadIdx.x; i < CB * kClTP; i += blockDim.x) {
     const int c = i / kClTP, j = i - c * kClTP;
     if (c < cn && j < pn) {
       float* o = dst + (size_t)c * P + j;
@@ -463,32 +465,46 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_cl_kernel(WarpArgs a, float
 
 // d/dfmap (NCHW, through the tile), d/dfmap_ref (channels-last, coalesced
 // atomics; consecutive pixels of a wave that share a bilinear cell are summed
-// in registers first) and gxy (the channel sums of a wave's 4 pixels in one
-// butterfly, one atomic per value and channel block).
+// in registers first) and the sampling-position gradient (the channel sums of
+// a wave's pixels in one butterfly).  A block covers NCH x 64 channels.
+// GEO (every channel in the block, C <= NCH * 64): the sampling-position
+// gradient of each pixel is complete in the block, so it is chained through
+// the projection right here -- d depth per pixel (summed over the refs) and
+// fp64 pose partials per (ref, image, block) -- with no gxy buffer, zero-fill,
+// atomics or geometry launch.  Otherwise gxy gets one atomic per value and
+// channel block and warp_cost_bwd_geo_kernel follows.
+template <int NCH, bool GEO>
 __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, const float* __restrict__ gcost,
                                                                     float* __restrict__ gfmap,
                                                                     float* __restrict__ gfref,
-                                                                    float* __restrict__ gxy) {
-  __shared__ float f_l[kClCH][kClTP + 1];
-  __shared__ float g_l[kClNC][kClCH][kClTP + 1];
+                                                                    float* __restrict__ gxy,
+                                                                    float* __restrict__ gdepth,
+                                                                    double* __restrict__ partial) {
+  constexpr int CB = NCH * kClCH;           // channels per block
+  __shared__ float f_l[CB][kClTP + 1];
+  __shared__ float g_l[kClNC][CB][kClTP + 1];
   __shared__ ClTaps L[kClNC];
+  __shared__ float gx_l[GEO ? kClNC : 1][kClTP][2];
+  __shared__ float gd_l[GEO ? kClNC : 1][kClTP];
   const int P = a.h * a.w;
-  const int p0 = blockIdx.x * kClTP, c0 = blockIdx.y * kClCH, b = blockIdx.z;
-  const int cn = min(kClCH, a.C - c0), pn = min(kClTP, P - p0);
+  const int p0 = blockIdx.x * kClTP, c0 = blockIdx.y * CB, b = blockIdx.z;
+  const int cn = min(CB, a.C - c0), pn = min(kClTP, P - p0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool live = lane < cn;
-  cl_load_tile(f_l, a.fmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f);
+  cl_load_tile<CB>(f_l, a.fmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f);
   if (a.reduce_mean)
-    cl_load_tile(g_l[0], gcost + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f / (float)a.N);
-  float gf[kClPPW];
+    cl_load_tile<CB>(g_l[0], gcost + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, 1.f / (float)a.N);
+  float gf[kClPPW][NCH];
 #pragma unroll
-  for (int k = 0; k < kClPPW; ++k) gf[k] = 0.f;
+  for (int k = 0; k < kClPPW; ++k)
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) gf[k][h] = 0.f;
+  float gdep = 0.f;                         // GEO: thread j < kClTP, d loss / d depth of pixel j
   for (int n0 = 0; n0 < a.N; n0 += kClNC) {
     const int nc = min(kClNC, a.N - n0);
     __syncthreads();
     if (!a.reduce_mean)
       for (int dn = 0; dn < nc; ++dn)
-        cl_load_tile(g_l[dn], gcost + (((size_t)(n0 + dn) * a.B + b) * a.C + c0) * P + p0, P, cn, pn, 1.f);
+        cl_load_tile<CB>(g_l[dn], gcost + (((size_t)(n0 + dn) * a.B + b) * a.C + c0) * P + p0, P, cn, pn, 1.f);
     cl_taps(a, b, n0, nc, p0, pn, blockIdx.y == 0, L);
     __syncthreads();
     for (int dn = 0; dn < nc; ++dn) {
@@ -499,51 +515,73 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, 
       float* gr = gfref ? gfref + img * a.C + c0 + lane : nullptr;
       int pkey = -1;                        // cell of the pending scatter (wave-uniform)
       int pidx[4] = {0, 0, 0, 0}, pok = 0;
-      float pend[4] = {0.f, 0.f, 0.f, 0.f};
+      float pend[NCH][4];
+#pragma unroll
+      for (int h = 0; h < NCH; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pend[h][e] = 0.f;
       float gxyv[2 * kClPPW];
 #pragma unroll
       for (int k = 0; k < kClPPW; ++k) {
         const int j = wave * kClPPW + k;
-        float v[4], gw = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)   // out-of-image taps read 0 (their values enter d/d(ix,iy))
-          v[e] = (live && j < pn && ((T.ok[j] >> e) & 1)) ? fr[(size_t)T.idx[j][e] * a.C] : 0.f;
-        if (live && j < pn) {
-          // one expression, as warp_cost_bwd_feat_kernel (the same contraction)
-          const float val = v[0] * T.wgt[j][0] + v[1] * T.wgt[j][1] + v[2] * T.wgt[j][2] + v[3] * T.wgt[j][3];
-          const float gd = 2.f * (f_l[lane][j] - val) * g_t[lane][j];
-          gf[k] += gd;
-          gw = -gd;
-        }
+        float gw[NCH], sx = 0.f, sy = 0.f;
         const float ty = T.ty[j], tx = T.tx[j];
-        gxyv[2 * k] = gw * ((v[1] - v[0]) * (1.f - ty) + (v[3] - v[2]) * ty);
-        gxyv[2 * k + 1] = gw * ((v[2] - v[0]) * (1.f - tx) + (v[3] - v[1]) * tx);
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+          const int cl = h * kClCH + lane;
+          const bool live = cl < cn && j < pn;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)   // out-of-image taps read 0 (their values enter d/d(ix,iy))
+            v[e] = (live && ((T.ok[j] >> e) & 1)) ? fr[(size_t)T.idx[j][e] * a.C + h * kClCH] : 0.f;
+          gw[h] = 0.f;
+          if (live) {
+            // one expression, as warp_cost_bwd_feat_kernel (the same contraction)
+            const float val = v[0] * T.wgt[j][0] + v[1] * T.wgt[j][1] + v[2] * T.wgt[j][2] + v[3] * T.wgt[j][3];
+            const float gd = 2.f * (f_l[cl][j] - val) * g_t[cl][j];
+            gf[k][h] += gd;
+            gw[h] = -gd;
+          }
+          sx += gw[h] * ((v[1] - v[0]) * (1.f - ty) + (v[3] - v[2]) * ty);
+          sy += gw[h] * ((v[2] - v[0]) * (1.f - tx) + (v[3] - v[1]) * tx);
+        }
+        gxyv[2 * k] = sx;
+        gxyv[2 * k + 1] = sy;
         if (gr && j < pn) {
           const int key = T.key[j];
           if (key != pkey) {                // flush the previous cell's sums
-            if (pkey >= 0 && live) {
+            if (pkey >= 0) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C, pend[e]);
+              for (int h = 0; h < NCH; ++h)
+                if (h * kClCH + lane < cn)
+#pragma unroll
+                  for (int e = 0; e < 4; ++e)
+                    if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C + h * kClCH, pend[h][e]);
             }
             pkey = key;
             pok = T.ok[j];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               pidx[e] = T.idx[j][e];
-              pend[e] = 0.f;
+#pragma unroll
+              for (int h = 0; h < NCH; ++h) pend[h][e] = 0.f;
             }
           }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) pend[e] += gw * T.wgt[j][e];
+          for (int h = 0; h < NCH; ++h)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pend[h][e] += gw[h] * T.wgt[j][e];
         }
       }
-      if (gr && pkey >= 0 && live) {
+      if (gr && pkey >= 0) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C, pend[e]);
+        for (int h = 0; h < NCH; ++h)
+          if (h * kClCH + lane < cn)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if ((pok >> e) & 1) atomicAdd(gr + (size_t)pidx[e] * a.C + h * kClCH, pend[h][e]);
       }
-      if (gxy) {   // 8 values (4 pixels x (ix, iy)) per butterfly
+      if (GEO || gxy) {   // 8 values (4 pixels x (ix, iy)) per butterfly
 #pragma unroll
         for (int g0 = 0; g0 < 2 * kClPPW; g0 += 8) {
           float v8[8];
@@ -551,17 +589,72 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, 
           for (int i = 0; i < 8; ++i) v8[i] = g0 + i < 2 * kClPPW ? gxyv[g0 + i] : 0.f;
           const float sum = wave_sum8(v8);
           const int vi = g0 + (lane >> 3), j = wave * kClPPW + (vi >> 1);
-          if ((lane & 7) == 0 && vi < 2 * kClPPW && j < pn) atomicAdd(gxy + (img + p0 + j) * 2 + (vi & 1), sum);
+          if ((lane & 7) == 0 && vi < 2 * kClPPW && j < pn) {
+            if (GEO)
+              gx_l[dn][j][vi & 1] = sum;
+            else
+              atomicAdd(gxy + (img + p0 + j) * 2 + (vi & 1), sum);
+          }
         }
       }
     }
+    if (GEO) {
+      __syncthreads();                      // every ref's gx_l of this chunk written
+      // thread t = dn * kClTP + j: pixel j's sampling-position gradient for ref
+      // n0 + dn chained through the projection (as warp_cost_bwd_geo_kernel)
+      const int t = threadIdx.x, dn = t / kClTP, j = t - dn * kClTP;
+      if (t < kClNC * kClTP) {              // whole 8-lane groups (wave 0) join the shuffles
+        float acc[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+        float gd = 0.f;
+        if (dn < nc && j < pn) {
+          const int p = p0 + j, n = n0 + dn;
+          float ki[9], kr[9];
+          cams(a, b, ki, kr);
+          float dd;
+          const float depth = decode_depth(a.depth[b * P + p], a.depth_mode, a.min_disp, a.span, &dd);
+          float R[9], tt[3];
+          load_pose(a.pose + (size_t)(n * a.B + b) * pose_stride(a.pose_mode), a.pose_mode, R, tt);
+          Proj q;
+          project(ki, kr, R, tt, (float)(p % a.w), (float)(p / a.w), depth, a.h, a.w, q);
+          gd = project_backward_pt(q, kr, R, tt, depth, gx_l[dn][j][0], gx_l[dn][j][1], acc, acc + 9);
+        }
+        if (dn < nc) gd_l[dn][j] = gd;
+        if (partial) {                      // the ref's 8 pixels in fixed order (lanes j of the group)
+          double d12[12];
+#pragma unroll
+          for (int k = 0; k < 12; ++k) {
+            double v = acc[k];
+#pragma unroll
+            for (int o = 1; o < kClTP; o <<= 1) v += __shfl_xor(v, o, kWave);
+            d12[k] = v;
+          }
+          if (j == 0 && dn < nc) {
+            double* dst = partial + ((size_t)((n0 + dn) * a.B + b) * gridDim.x + blockIdx.x) * 12;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) dst[k] = d12[k];
+          }
+        }
+      }
+      __syncthreads();
+      if (t < kClTP)
+        for (int d2 = 0; d2 < nc; ++d2) gdep += gd_l[d2][t];   // refs in order
+    }
+  }
+  if (GEO && gdepth && threadIdx.x < pn) {
+    float dd;
+    decode_depth(a.depth[b * P + p0 + threadIdx.x], a.depth_mode, a.min_disp, a.span, &dd);
+    gdepth[b * P + p0 + threadIdx.x] = gdep * dd;
   }
   if (gfmap) {
     __syncthreads();                        // f_l reused as the output tile
 #pragma unroll
-    for (int k = 0; k < kClPPW; ++k) f_l[lane][wave * kClPPW + k] = gf[k];
+    for (int k = 0; k < kClPPW; ++k)
+#pragma unroll
+      for (int h = 0; h < NCH; ++h) f_l[h * kClCH + lane][wave * kClPPW + k] = gf[k][h];
     __syncthreads();
-    cl_store_tile(f_l, gfmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, a.acc_fmap != 0);
+    cl_store_tile<CB>(f_l, gfmap + ((size_t)b * a.C + c0) * P + p0, P, cn, pn, a.acc_fmap != 0);
   }
 }
 
@@ -854,8 +947,11 @@ using namespace dro;
 extern "C" size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w) {
   const size_t P = (size_t)h * w;
   const size_t nblk = (P + kGeoThreads - 1) / kGeoThreads;
-  // gxy (float), then the fp64 pose partials (8-byte aligned: N*B*P*2 floats is even)
-  return (size_t)N * B * P * 2 * sizeof(float) + (size_t)N * B * nblk * 12 * sizeof(double);
+  // gxy (float), then the fp64 pose partials (8-byte aligned: N*B*P*2 floats is even);
+  // the fused channels-last backward: fp64 pose partials per pixel tile only
+  const size_t split = (size_t)N * B * P * 2 * sizeof(float) + (size_t)N * B * nblk * 12 * sizeof(double);
+  const size_t fused = (size_t)N * B * ((P + kClTP - 1) / kClTP) * 12 * sizeof(double);
+  return split > fused ? split : fused;
 }
 
 extern "C" int dro_warp_cost_forward(const float* fmap, const float* fmap_ref, const float* depth,
@@ -911,17 +1007,40 @@ static int warp_backward(WarpArgs a, const float* grad_out, float* grad_fmap, fl
   static const int nomerge = env_int("DRO_WARP_NOMERGE", 0);
   a.merge = nomerge ? 0 : 1;
   const int P = h * w;
-  float* gxy = geo ? (float*)workspace : nullptr;
-  const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
-  double* partial = (geo && grad_pose) ? (double*)(gxy + (size_t)N * B * P * 2) : nullptr;
   if (grad_fmap_ref && !(accumulate & 2) &&
       (st = launch_zero(grad_fmap_ref, (size_t)N * B * C * P, s)))
     return st;
+  // channels-last maps of <= 256 channels: one block per pixel tile holds every
+  // channel, and the depth / pose chain runs in the same launch (GEO)
+  const int nch = (C + kClCH - 1) / kClCH;
+  if (ref_layout == 1 && nch <= 4) {
+    if (!(grad_fmap || grad_fmap_ref || geo || cells)) return DRO_OK;
+    dim3 grid((P + kClTP - 1) / kClTP, 1, B);
+    double* partial = grad_pose ? (double*)workspace : nullptr;
+#define DRO_CLF(NCH_, GEO_)                                                                            \
+  hipLaunchKernelGGL((warp_cost_bwd_feat_cl_kernel<NCH_, GEO_>), grid, dim3(256), 0, s, a, grad_out, \
+                     grad_fmap, grad_fmap_ref, (float*)nullptr, grad_depth, partial)
+    if (nch == 1) {
+      if (geo) DRO_CLF(1, true); else DRO_CLF(1, false);
+    } else if (nch == 2) {
+      if (geo) DRO_CLF(2, true); else DRO_CLF(2, false);
+    } else {
+      if (geo) DRO_CLF(4, true); else DRO_CLF(4, false);
+    }
+#undef DRO_CLF
+    if ((st = launch_status("warp_cost_bwd_feat_cl_kernel launch failed"))) return st;
+    if (grad_pose)
+      return launch_pose_finalize(partial, (int)grid.x, N * B, a.pose, a.pose_mode, grad_pose, s);
+    return DRO_OK;
+  }
+  float* gxy = geo ? (float*)workspace : nullptr;
+  const int nblk = (P + kGeoThreads - 1) / kGeoThreads;
+  double* partial = (geo && grad_pose) ? (double*)(gxy + (size_t)N * B * P * 2) : nullptr;
   if (gxy && (st = launch_zero(gxy, (size_t)N * B * P * 2, s))) return st;
   if (ref_layout == 1 && (grad_fmap || grad_fmap_ref || gxy || cells)) {
-    dim3 grid((P + kClTP - 1) / kClTP, (C + kClCH - 1) / kClCH, B);
-    hipLaunchKernelGGL(warp_cost_bwd_feat_cl_kernel, grid, dim3(256), 0, s, a, grad_out, grad_fmap,
-                       grad_fmap_ref, gxy);
+    dim3 grid((P + kClTP - 1) / kClTP, nch, B);
+    hipLaunchKernelGGL((warp_cost_bwd_feat_cl_kernel<1, false>), grid, dim3(256), 0, s, a, grad_out, grad_fmap,
+                       grad_fmap_ref, gxy, (float*)nullptr, (double*)nullptr);
     if ((st = launch_status("warp_cost_bwd_feat_cl_kernel launch failed"))) return st;
   } else if (grad_fmap || grad_fmap_ref || gxy || cells) {
     dim3 grid((P + kWave - 1) / kWave, (C + kGroups * kCPT - 1) / (kGroups * kCPT), B);

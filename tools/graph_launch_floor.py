@@ -33,6 +33,8 @@ def main():
             else:
                 t.add_(1.0)
 
+    chain(x, 1)                       # library handles created outside any capture
+    torch.cuda.synchronize()
     for name, two in (("one stream", False), ("two streams", True)):
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
