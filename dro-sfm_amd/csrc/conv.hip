@@ -2224,7 +2224,13 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
   // gradients run there (dense y); otherwise form G first
   const WhPlan wh = plan_wgrad_halo(a.g.Cin, Cout, KH, KW, B, H, W);
   const bool halo_dgrad = plan_igemm(a.g.Cin, Cout, KH, KW, B, H, W).halo;
-  const bool fold = pre && wh.ok && halo_dgrad && (act == 0 || (y->total_channels == Cout && y->channel_offset == 0));
+  // the thin data gradient (7x7 over <= 8 input channels, one source) folds
+  // as well; a call without a weight gradient (the trainer queues those)
+  // needs only its data-gradient kernel to fold
+  static const bool thin_off = getenv("DRO_CONV_NO_THIN") != nullptr;
+  const bool thin_dgrad = KH == kThinK && KW == kThinK && nsrc == 1 && a.g.Cin <= 8 && B <= 65535 && !thin_off;
+  const bool fold = pre && (halo_dgrad || thin_dgrad) && (wh.ok || !grad_weight) &&
+                    (act == 0 || (y->total_channels == Cout && y->channel_offset == 0));
   a.galpha = fold ? alpha : 1.f;
   a.gy = (fold && act) ? y->data : nullptr;
   if (pre && !fold) {

@@ -256,6 +256,12 @@ _BATCH = [True]
 _PENDING = {}
 _PENDING_CB = [False]
 _MULTI_SHAPES = {(1, 1), (1, 5), (5, 1), (3, 3)}
+# shapes whose queued uses are stacked on the batch axis and reduced by ONE
+# single-use weight gradient (no multi-use kernel for them): the update blocks'
+# 7x7 state convs (convd1 / convp1, one source of 1 or 6 channels) -- 8 uses per
+# step each, 48 MFLOP per use, ~28 us + a split sum per launch when alone
+# (DRO_CAT_WGRAD=0: per use, A/B)
+_CAT_SHAPES = {(7, 7)} if os.environ.get("DRO_CAT_WGRAD", "1") != "0" else set()
 _MAX_USES = 16
 
 
@@ -265,11 +271,11 @@ def set_batched_weight_grads(enabled):
     _BATCH[0] = bool(enabled)
 
 
-def _queue_weight_grad(srcs, wshape, act, alpha, dout, y, gw, gb):
+def _queue_weight_grad(srcs, wshape, act, alpha, dout, y, gw, gb, weight=None):
     """Queue one use's weight(+bias) gradient for the end-of-backward batch;
     False when this conv shape is not batched (the caller launches it)."""
     Cout, Cin, KH, KW = wshape
-    if not _BATCH[0] or (KH, KW) not in _MULTI_SHAPES:
+    if not _BATCH[0] or not ((KH, KW) in _MULTI_SHAPES or ((KH, KW) in _CAT_SHAPES and len(srcs) == 1)):
         return False
     B, _, H, W = srcs[0].shape
     key = (gw.data_ptr(), gb.data_ptr() if gb is not None else 0, B, H, W, act, float(alpha),
@@ -277,7 +283,7 @@ def _queue_weight_grad(srcs, wshape, act, alpha, dout, y, gw, gb):
     ent = _PENDING.get(key)
     cur = torch.cuda.current_stream()
     if ent is None:
-        ent = _PENDING[key] = ((B, H, W, Cin, Cout, KH, KW, act, float(alpha), gw, gb, len(srcs)), [], [])
+        ent = _PENDING[key] = ((B, H, W, Cin, Cout, KH, KW, act, float(alpha), gw, gb, len(srcs), weight), [], [])
     ent[1].append((list(srcs), dout, y))
     if all(s != cur for s in ent[2]):
         ent[2].append(cur)
@@ -336,7 +342,15 @@ def _launch_weight_grads(items, stream):
                         x.record_stream(stream)
     with torch.cuda.stream(stream):
         for meta, uses, _ in items:
-            B, H, W, Cin, Cout, KH, KW, act, alpha, gw, gb, nsrc = meta
+            B, H, W, Cin, Cout, KH, KW, act, alpha, gw, gb, nsrc, weight = meta
+            if (KH, KW) in _CAT_SHAPES:
+                # every use on the batch axis (broadcast sources materialise),
+                # one weight-gradient launch + one split sum for all of them
+                xs = torch.cat([srcs[0].expand(B, Cin, H, W) for srcs, _, _ in uses], 0)
+                g = torch.cat([d for _, d, _ in uses], 0)
+                yy = torch.cat([t for _, _, t in uses], 0) if act else None
+                _conv_bwd([xs], weight, yy, g, act, alpha, [None], [0], gw, gb, 1)
+                continue
             for c0 in range(0, len(uses), _MAX_USES):
                 chunk = uses[c0:c0 + _MAX_USES]
                 n = len(chunk)
@@ -482,7 +496,7 @@ def _conv2d_backward(ctx, gout):
         gw, gb = ctx.direct[2], ctx.direct[3]
         if any(g is not None for g in tgt):
             _conv_bwd(srcs, weight, y, gout, act, alpha, tgt, dacc, wsplit=ctx.wsplit)
-        if not _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None):
+        if not _queue_weight_grad(srcs, weight.shape, act, alpha, gout, y, gw, gb if has_bias else None, weight):
             _conv_bwd(srcs, weight, y, gout, act, alpha, [None] * len(srcs), [0] * len(srcs), gw,
                       gb if has_bias else None, 1)
         return gsrc, None, None, None, None, none_params, None
