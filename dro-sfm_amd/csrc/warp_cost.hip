@@ -701,34 +701,35 @@ __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
   if (gdepth && live) gdepth[b * P + p] = gd_total * dd;
 }
 
-// One 64-lane block per pose: lanes 0..59 = 5 row groups x 12 components
-// stride over the pose's [nblk][12] partials (coalesced), then the 5 group
-// sums are added in a fixed order (deterministic).  The photometric loss hands
-// in 240 tile partials per pose: one serial thread per pose took 51 us there.
-__global__ __launch_bounds__(64) void pose_finalize_kernel(const double* __restrict__ partial, int nblk,
-                                                           int npose, const float* __restrict__ pose,
-                                                           int pose_mode, float* __restrict__ gpose) {
-  constexpr int G = 5;   // row groups
+// One 256-thread block per pose: threads 0..239 = 20 row groups x 12
+// components stride over the pose's [nblk][12] partials (coalesced), then the
+// 20 group sums are added in a fixed order (deterministic).  The fused cost
+// backward and the photometric loss hand in 240 partials per pose: with 5
+// groups of one wave each group walked a 48-load dependent chain.
+__global__ __launch_bounds__(256) void pose_finalize_kernel(const double* __restrict__ partial, int nblk,
+                                                            int npose, const float* __restrict__ pose,
+                                                            int pose_mode, float* __restrict__ gpose) {
+  constexpr int G = 20;   // row groups
   __shared__ double sh[G * 12];
   __shared__ double s[12];
-  const int i = blockIdx.x, lane = threadIdx.x;
+  const int i = blockIdx.x, t = threadIdx.x;
   if (i >= npose) return;
-  if (lane < G * 12) {
-    const int comp = lane % 12, g = lane / 12;
+  if (t < G * 12) {
+    const int comp = t % 12, g = t / 12;
     const double* src = partial + (size_t)i * nblk * 12 + comp;
     double v = 0.0;
     for (int j = g; j < nblk; j += G) v += src[(size_t)j * 12];
-    sh[lane] = v;
+    sh[t] = v;
   }
   __syncthreads();
-  if (lane < 12) {
+  if (t < 12) {
     double v = 0.0;
 #pragma unroll
-    for (int g = 0; g < G; ++g) v += sh[g * 12 + lane];
-    s[lane] = v;
+    for (int g = 0; g < G; ++g) v += sh[g * 12 + t];
+    s[t] = v;
   }
   __syncthreads();
-  if (lane == 0) {
+  if (t == 0) {
     double r[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) r[k] = s[k];
@@ -889,7 +890,7 @@ __global__ __launch_bounds__(1024) void plane_sweep_lds_kernel(WarpArgs a, const
 int launch_pose_finalize(const double* partial, int nblk, int npose, const float* pose,
                          int pose_mode, float* gpose, hipStream_t s) {
   if (npose <= 0) return 0;
-  hipLaunchKernelGGL(pose_finalize_kernel, dim3(npose), dim3(64), 0, s, partial, nblk,
+  hipLaunchKernelGGL(pose_finalize_kernel, dim3(npose), dim3(256), 0, s, partial, nblk,
                      npose, pose, pose_mode, gpose);
   return launch_status("pose_finalize_kernel launch failed");
 }
