@@ -1927,7 +1927,9 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     return launch_thin<MODE, ACT>(a, pl.ksplit, s);
   }
   // split-bf16 MFMA engine (xconv.hip) when the caller passed split weights
-  if (!a.flat_only && a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
+  if constexpr (EPI != 3) {   // (no stage-2 epilogue in the split-bf16 engine)
+    if (!a.flat_only && a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
+  }
   a.row_tiles = pl.row_tiles;
   a.chunks_per_split = pl.chunks_per_split;
   a.part = pl.ksplit > 1 ? reinterpret_cast<float*>(ws) : nullptr;
@@ -2170,13 +2172,20 @@ extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const 
                                (hipStream_t)stream);
 }
 
-extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H,
-                                   int W, int Cout, int KH, int KW, int act, float alpha,
-                                   const dro_slice* y, const float* dout, float* const* grad_srcs,
-                                   const int* grad_ctot, const int* grad_coff,
-                                   const int* grad_accumulate, float* grad_weight, float* grad_bias,
-                                   int grad_weight_accumulate, const void* wsplit, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
+// SepConvGRU stage 2 folded into the candidate conv's data gradient (EPI 3)
+struct GruFold {
+  const float* zr;
+  const float* h;
+  float* dzr;
+  float* dh;
+};
+
+static int conv2d_backward_impl(const dro_slice* srcs, int nsrc, const float* weight, int B, int H, int W,
+                                int Cout, int KH, int KW, int act, float alpha, const dro_slice* y,
+                                const float* dout, float* const* grad_srcs, const int* grad_ctot,
+                                const int* grad_coff, const int* grad_accumulate, float* grad_weight,
+                                float* grad_bias, int grad_weight_accumulate, const void* wsplit,
+                                void* workspace, size_t workspace_bytes, void* stream, const GruFold* gf) {
   IgArgs a = {};
   a.wsplit = static_cast<const char*>(wsplit);   // transposed layout: the data gradient
   int st = conv_setup_geom(a, srcs, nsrc, B, H, W, Cout, KH, KW);
@@ -2206,6 +2215,25 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
       set_error("conv2d_backward: gradient target too large (32-bit offsets)");
       return DRO_E_SHAPE;
     }
+  }
+  if (gf) {   // source 0 is r*h (Cout channels): its gradient feeds stage 2, not a buffer
+    if (!gf->zr || !gf->h || !gf->dzr || !gf->dh) {
+      set_error("convgru_candidate_backward: NULL zr/h/dzr/dh");
+      return DRO_E_NULL;
+    }
+    if (srcs[0].channels != Cout || act != 0 || alpha != 1.f || grad_weight || too_big(B, 2 * Cout, (long long)H * W)) {
+      set_error("convgru_candidate_backward: source 0 must be r*h with Cout channels (no activation, no weight gradient)");
+      return DRO_E_SHAPE;
+    }
+    a.z = Slice{gf->zr, Cout, 2 * Cout, Cout, 0};
+    a.h = Slice{gf->h, Cout, Cout, 0, 0};
+    a.aux = gf->dzr;
+    a.hd = Cout;
+    a.gsrc[0] = gf->dh;
+    a.gsrc_ctot[0] = Cout;
+    a.gsrc_coff[0] = 0;
+    a.gsrc_acc[0] = 1;
+    a.wsplit = nullptr;   // the split-bf16 engine has no stage-2 epilogue
   }
   a.weight = weight;
   a.gweight = grad_weight;
@@ -2252,7 +2280,10 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     a.rows = a.g.Cin;
     a.kch = Cout;
     const int gact = fold ? act : 0;
-    DRO_ACT_SWITCH(gact, st = (launch_igemm<1, A_, 0>(a, P, ws_ig, s)));
+    if (gf)
+      st = launch_igemm<1, 0, 3>(a, P, ws_ig, s);
+    else
+      DRO_ACT_SWITCH(gact, st = (launch_igemm<1, A_, 0>(a, P, ws_ig, s)));
     if (st) return st;
   }
   if (grad_weight && wh.ok && !wgrad_v1()) {
@@ -2313,6 +2344,34 @@ extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float*
     if ((st = launch_status("wgrad_finish_kernel launch failed"))) return st;
   }
   return DRO_OK;
+}
+
+extern "C" int dro_conv2d_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H,
+                                   int W, int Cout, int KH, int KW, int act, float alpha,
+                                   const dro_slice* y, const float* dout, float* const* grad_srcs,
+                                   const int* grad_ctot, const int* grad_coff,
+                                   const int* grad_accumulate, float* grad_weight, float* grad_bias,
+                                   int grad_weight_accumulate, const void* wsplit, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  return conv2d_backward_impl(srcs, nsrc, weight, B, H, W, Cout, KH, KW, act, alpha, y, dout, grad_srcs,
+                              grad_ctot, grad_coff, grad_accumulate, grad_weight, grad_bias,
+                              grad_weight_accumulate, wsplit, workspace, workspace_bytes, stream, nullptr);
+}
+
+extern "C" int dro_convgru_candidate_backward(const dro_slice* srcs, int nsrc, const float* weight, int B,
+                                              int H, int W, int hd, int KH, int KW, const float* dq,
+                                              const float* zr, const float* h, float* dzr, float* dh,
+                                              float* const* grad_srcs, const int* grad_ctot,
+                                              const int* grad_coff, const int* grad_accumulate,
+                                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (!srcs || nsrc < 1) {
+    set_error("convgru_candidate_backward: need the r*h source");
+    return DRO_E_NULL;
+  }
+  const GruFold gf = {zr, h, dzr, dh};
+  return conv2d_backward_impl(srcs, nsrc, weight, B, H, W, hd, KH, KW, 0, 1.f, nullptr, dq, grad_srcs, grad_ctot,
+                              grad_coff, grad_accumulate, nullptr, nullptr, 0, nullptr, workspace, workspace_bytes,
+                              stream, &gf);
 }
 
 // split-K partials of the parity-class data gradient, [split][class][rows][pcmax]

@@ -62,7 +62,9 @@ struct IgArgs {
   float* out;             // forward output slice base
   int out_ctot, out_coff;
   Slice z, h;             // EPI 1: out = (1-z) h + z q, q = tanh(acc + b); EPI 2: h for r*h
-  float* aux;             // EPI 1: q (saved for the backward); EPI 2: r*h  (dense, [B, hd, H, W])
+                          // MODE 1 EPI 3: z = the r gate (zr channels hd..2hd), h = the state
+  float* aux;             // EPI 1: q (saved for the backward); EPI 2: r*h  (dense, [B, hd, H, W]);
+                          // MODE 1 EPI 3: dzr (its r half is written)
   int hd;                 // EPI 2: rows >= hd are the r gate
   const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation (or w.r.t. the
                           // output when folded: then G_pre = galpha * G * act'(gy))
@@ -212,7 +214,14 @@ __device__ __forceinline__ void epi_store(const IgArgs& a, int row, int eb, size
     }
     a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
   } else {
-    if (row < a.cbase[1])
+    if (EPI == 3 && row < a.cbase[1]) {   // SepConvGRU stage 2 on d(r*h) (gru_elem_kernel)
+      const size_t zi = ((size_t)eb * a.z.ctot + a.z.coff + row) * HW + epix;
+      const size_t hi = ((size_t)eb * a.h.ctot + a.h.coff + row) * HW + epix;
+      const float r = a.z.p[zi];
+      a.aux[zi] = acc * a.h.p[hi] * r * (1.f - r);
+      float* q = a.gsrc[0] + ((size_t)eb * a.gsrc_ctot[0] + a.gsrc_coff[0] + row) * HW + epix;
+      *q += acc * r;
+    } else if (row < a.cbase[1])
       grad_put(a.gsrc[0], a.gsrc_ctot[0], a.gsrc_coff[0], a.gsrc_acc[0], row, eb, epix, HW, acc);
     else if (row < a.cbase[2])
       grad_put(a.gsrc[1], a.gsrc_ctot[1], a.gsrc_coff[1], a.gsrc_acc[1], row - a.cbase[1], eb, epix, HW, acc);
@@ -267,10 +276,23 @@ __device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int
     float* dst[16];
     bool accf[16];
     float old[16];
+    // MODE 1 EPI 3 (SepConvGRU stage 2 folded into the candidate conv's data
+    // gradient): rows of source 0 are d(r*h); they write dr~ = d h r (1-r) into
+    // dzr's r half and add d r to dh (gsrc[0]) instead of storing d(r*h)
+    float gr[EPI == 3 ? 16 : 1], gh[EPI == 3 ? 16 : 1];
+    size_t gzi[EPI == 3 ? 16 : 1];
+    bool g3[EPI == 3 ? 16 : 1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = rbase + (r & 3) + 8 * (r >> 2);
       const int si = row >= rows ? -1 : (row >= a.cbase[1]) + (row >= a.cbase[2]) + (row >= a.cbase[3]);
+      if (EPI == 3) {
+        g3[r] = si == 0;
+        const int c = si == 0 ? row : 0;
+        gzi[r] = ((size_t)eb * a.z.ctot + a.z.coff + c) * HW + epix;
+        gr[r] = si == 0 ? a.z.p[gzi[r]] : 0.f;
+        gh[r] = si == 0 ? a.h.p[((size_t)eb * a.h.ctot + a.h.coff + c) * HW + epix] : 0.f;
+      }
       float* base = nullptr;
       int ctot = 0, coff = 0, cl = 0, ac = 0;
       if (si >= 0) {
@@ -282,13 +304,19 @@ __device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int
         cl = row - cb;
       }
       dst[r] = base ? base + ((size_t)eb * ctot + coff + cl) * HW + epix : nullptr;
-      accf[r] = base && ac;
+      accf[r] = base && (ac || (EPI == 3 && si == 0));
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) old[r] = accf[r] ? *dst[r] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (dst[r]) *dst[r] = accf[r] ? old[r] + acc[r] : acc[r];
+    for (int r = 0; r < 16; ++r) {
+      if (EPI == 3 && g3[r]) {
+        a.aux[gzi[r]] = acc[r] * gh[r] * gr[r] * (1.f - gr[r]);
+        *dst[r] = old[r] + acc[r] * gr[r];
+      } else if (dst[r]) {
+        *dst[r] = accf[r] ? old[r] + acc[r] : acc[r];
+      }
+    }
   }
 }
 

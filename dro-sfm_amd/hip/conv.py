@@ -662,6 +662,35 @@ def _(stage, dhn, zr, q, h, drh, dq, dzr, dh):
     return None
 
 
+@torch.library.custom_op("dro::convgru_candidate_backward", mutates_args=("dzr", "dh", "grad_srcs"))
+def _gru_cand_bwd_op(srcs: list[Tensor], weight: Tensor, dq: Tensor, zr: Tensor, h: Tensor, dzr: Tensor,
+                     dh: Tensor, grad_srcs: list[Tensor], accumulate: list[int]) -> None:
+    """The candidate conv's data gradient with SepConvGRU stage 2 in its
+    epilogue (csrc/conv.hip dro_convgru_candidate_backward): srcs = [r*h, x...],
+    d(r*h) is not stored but turned into dzr[:, hd:] = d h r (1-r) and
+    dh += d r; grad_srcs[1:] / accumulate[1:] as in conv2d_backward
+    (grad_srcs[0] unused)."""
+    lib = _lib.load()
+    hd, Cin, KH, KW = weight.shape
+    B, _, H, W = srcs[0].shape
+    tgt = [None] + [g if g.numel() else None for g in grad_srcs[1:]]
+    ws, nws = _workspace(B, H, W, Cin, hd, KH, KW, dq.device)
+    ptrs, ctot, coff = _grad_targets(tgt) if any(t is not None for t in tgt) else (None, None, None)
+    acc = (ctypes.c_int * len(srcs))(*accumulate) if ptrs is not None else None
+    check(lib.dro_convgru_candidate_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, hd, KH, KW,
+                                             ptr(dq.contiguous()), ptr(zr), ptr(h), ptr(dzr), ptr(dh), ptrs, ctot,
+                                             coff, acc, ptr(ws), nws, stream_of(dq)),
+          "dro_convgru_candidate_backward")
+
+
+@_gru_cand_bwd_op.register_fake
+def _(srcs, weight, dq, zr, h, dzr, dh, grad_srcs, accumulate):
+    return None
+
+
+_GRU_FOLD = os.environ.get("DRO_GRU_FOLD", "1") != "0"   # A/B: 0 keeps the separate stage-2 launch
+
+
 # ------------------------------------------------------------------ dro::sepconvgru_half
 @torch.library.custom_op("dro::sepconvgru_half", mutates_args=())
 def _sepgru_op(h: Tensor, wz: Tensor, bz: Tensor, wr: Tensor, br: Tensor, wq: Tensor, bq: Tensor, xs: list[Tensor],
@@ -759,10 +788,16 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
     nones = (None,) * 6
     if ctx.direct is not None:
         (_, _), (gwzr, gbzr), (gwq, gbq) = ctx.direct
-        _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [drh, *tg], qacc0, wsplit=qb)
+        if _GRU_FOLD and qb is None:
+            # d(r*h) goes straight into stage 2 in the data gradient's epilogue
+            torch.ops.dro.convgru_candidate_backward([rh, *xs], wq, dq, zr, h, dzr, dh,
+                                                     [_placeholder(t, h.device) for t in [None, *tg]], qacc0)
+        else:
+            _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [drh, *tg], qacc0, wsplit=qb)
         if not _queue_weight_grad([rh, *xs], wq.shape, 0, 1.0, dq, None, gwq, gbq):
             _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwq, gbq, 1)
-        torch.ops.dro.gru_backward_elem(2, None, zr, None, h, drh, None, dzr, dh)
+        if not (_GRU_FOLD and qb is None):
+            torch.ops.dro.gru_backward_elem(2, None, zr, None, h, drh, None, dzr, dh)
         _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), wsplit=zb)
         if not _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
             _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwzr, gbzr, 1)

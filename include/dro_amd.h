@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 8: dro_convgru_candidate_backward (GRU stage 2 in the candidate conv's data gradient); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -525,6 +525,22 @@ int dro_conv2d_weight_grad_multi(const dro_wgrad_use* uses, int nuse, int nsrc, 
 int dro_gru_backward_elem(int stage, int B, int hd, int H, int W, const float* dhn,
                           const float* zr, const float* q, const float* h, const float* drh,
                           float* dq, float* dzr, float* dh, void* stream);
+
+/* The candidate conv's data gradient with stage 2 in its epilogue (ABI 8):
+ * dro_conv2d_backward of q~ = conv([r*h, x...]) for Cout = hd, act NONE, no
+ * weight gradient, given dq (stage 1's output), except that source 0 (r*h,
+ * hd channels) is not stored: each d(r*h) element becomes
+ *   dzr[:, hd:] = d(r*h) h r (1-r);  dh += d(r*h) r
+ * (stage 2 of dro_gru_backward_elem, one launch fewer per GRU half).
+ * grad_srcs[0] / grad_ctot[0] / grad_coff[0] / grad_accumulate[0] are ignored;
+ * sources 1.. behave as in dro_conv2d_backward.  Workspace: the
+ * dro_conv2d_workspace_bytes of the conv.  Replaces the d(r*h) path of
+ * SepConvGRU's backward (dro_sfm/networks/optim/update.py:67-70, autograd). */
+int dro_convgru_candidate_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H, int W,
+                                   int hd, int KH, int KW, const float* dq, const float* zr, const float* h,
+                                   float* dzr, float* dh, float* const* grad_srcs, const int* grad_ctot,
+                                   const int* grad_coff, const int* grad_accumulate, void* workspace,
+                                   size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused Adam over flat fp32 buffers (the data-parallel trainer's parameters,

@@ -34,7 +34,7 @@ def test_header_matches_exports(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dro_abi_version() == 7
+    assert lib.dro_abi_version() == 8
 
 
 def test_null_arguments_rejected(lib):

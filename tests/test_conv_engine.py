@@ -389,3 +389,48 @@ def test_pose_mean(hip):
     (out * G.to(DEV)).sum().backward()
     assert rel(out, ref) < TOL and rel(yd.grad, yr.grad) < TOL and rel(pd.grad, pr.grad) < TOL
     assert rel(hip.pose_mean(yd.detach(), 0.01), yr.detach().mean(dim=(2, 3)) * scale) < TOL
+
+
+@pytest.mark.parametrize("kernel,B,hd,H,W", [((1, 5), 2, 32, 24, 80), ((5, 1), 4, 32, 24, 80),
+                                              ((3, 3), 2, 64, 13, 37), ((1, 5), 1, 8, 5, 7)])
+def test_convgru_candidate_backward_matches_unfused(hip, kernel, B, hd, H, W):
+    """The candidate conv's data gradient with SepConvGRU stage 2 in its
+    epilogue (dro_convgru_candidate_backward, ABI 8) against the two-launch
+    form (conv2d_backward into d(r*h), then gru_backward_elem stage 2): dzr
+    (both halves), dh (accumulated into) and the other sources' gradients
+    (one overwritten, one accumulated) bit for bit."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    KH, KW = kernel
+    cx = (24, 10)
+    rh = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    xs = [torch.randn(B, c, H, W, device=DEV, generator=g) for c in cx]
+    wq = torch.randn(hd, hd + sum(cx), KH, KW, device=DEV, generator=g) * 0.05
+    dq = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    zr = torch.sigmoid(torch.randn(B, 2 * hd, H, W, device=DEV, generator=g))
+    h = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    dh0 = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    dzr0 = torch.randn(B, 2 * hd, H, W, device=DEV, generator=g)
+    gx0 = [torch.randn(B, c, H, W, device=DEV, generator=g) for c in cx]
+    acc = [0, 0, 1]
+    # two launches
+    drh = torch.empty_like(h)
+    dh_a, dzr_a, gx_a = dh0.clone(), dzr0.clone(), [t.clone() for t in gx0]
+    torch.ops.dro.conv2d_backward([rh, *xs], wq, None, dq, 0, 1.0, [drh, *gx_a], acc, None, None, 0, None)
+    torch.ops.dro.gru_backward_elem(2, None, zr, None, h, drh, None, dzr_a, dh_a)
+    # folded
+    dh_b, dzr_b, gx_b = dh0.clone(), dzr0.clone(), [t.clone() for t in gx0]
+    torch.ops.dro.convgru_candidate_backward([rh, *xs], wq, dq, zr, h, dzr_b, dh_b,
+                                             [torch.empty(0, device=DEV), *gx_b], acc)
+    torch.cuda.synchronize()
+    assert torch.equal(dzr_a, dzr_b)
+    assert torch.equal(dh_a, dh_b)
+    for a, b in zip(gx_a, gx_b):
+        assert torch.equal(a, b)
+    assert torch.equal(dzr_b[:, :hd], dzr0[:, :hd])     # the z half untouched
+
+
+def test_convgru_candidate_backward_rejects(hip):
+    from dro_sfm_amd.hip import _lib
+    lib = _lib.load()
+    assert lib.dro_convgru_candidate_backward(None, 0, None, 1, 1, 1, 1, 1, 5, None, None, None, None, None,
+                                              None, None, None, None, None, 0, None) != 0
