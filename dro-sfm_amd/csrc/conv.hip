@@ -1927,7 +1927,7 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
     return launch_thin<MODE, ACT>(a, pl.ksplit, s);
   }
   // split-bf16 MFMA engine (xconv.hip) when the caller passed split weights
-  if constexpr (EPI != 3) {   // (no stage-2 epilogue in the split-bf16 engine)
+  if constexpr (EPI < 3) {   // (no GRU epilogues in the split-bf16 engine)
     if (!a.flat_only && a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
   }
   a.row_tiles = pl.row_tiles;
@@ -2173,11 +2173,18 @@ extern "C" int dro_convgru_blend_forward(const dro_slice* srcs, int nsrc, const 
 }
 
 // SepConvGRU stage 2 folded into the candidate conv's data gradient (EPI 3)
+// kind 3: stage 2 of this half in the candidate conv (source 0 = r*h);
+// kind 4: stage 1 of the previous half in this half's gate conv (source 0 = h,
+// its finished gradient is the previous half's dh')
 struct GruFold {
+  int kind;
   const float* zr;
   const float* h;
   float* dzr;
   float* dh;
+  const float* q;
+  float* dq;
+  int dh_acc;
 };
 
 static int conv2d_backward_impl(const dro_slice* srcs, int nsrc, const float* weight, int B, int H, int W,
@@ -2216,7 +2223,7 @@ static int conv2d_backward_impl(const dro_slice* srcs, int nsrc, const float* we
       return DRO_E_SHAPE;
     }
   }
-  if (gf) {   // source 0 is r*h (Cout channels): its gradient feeds stage 2, not a buffer
+  if (gf && gf->kind == 3) {   // source 0 is r*h (Cout channels): its gradient feeds stage 2, not a buffer
     if (!gf->zr || !gf->h || !gf->dzr || !gf->dh) {
       set_error("convgru_candidate_backward: NULL zr/h/dzr/dh");
       return DRO_E_NULL;
@@ -2233,7 +2240,29 @@ static int conv2d_backward_impl(const dro_slice* srcs, int nsrc, const float* we
     a.gsrc_ctot[0] = Cout;
     a.gsrc_coff[0] = 0;
     a.gsrc_acc[0] = 1;
-    a.wsplit = nullptr;   // the split-bf16 engine has no stage-2 epilogue
+    a.wsplit = nullptr;   // the split-bf16 engine has no GRU epilogues
+  } else if (gf) {   // kind 4: source 0 is this half's h (hd = Cout / 2 channels), accumulated
+    const int hd = Cout / 2;
+    if (!gf->zr || !gf->h || !gf->dzr || !gf->dh || !gf->q || !gf->dq || !a.gsrc[0]) {
+      set_error("convgru_gates_backward: NULL zr/h/q/dq/dzr/dh or d h target");
+      return DRO_E_NULL;
+    }
+    if (Cout % 2 || srcs[0].channels != hd || act != 0 || alpha != 1.f || grad_weight ||
+        a.gsrc_ctot[0] != hd || a.gsrc_coff[0] != 0 || too_big(B, Cout, (long long)H * W)) {
+      set_error("convgru_gates_backward: source 0 must be h with Cout / 2 channels and a dense d h target "
+                "(no activation, no weight gradient)");
+      return DRO_E_SHAPE;
+    }
+    a.z = Slice{gf->zr, hd, Cout, 0, 0};
+    a.h = Slice{gf->h, hd, hd, 0, 0};
+    a.aux = gf->dzr;
+    a.hd = hd;
+    a.g1q = gf->q;
+    a.g1dq = gf->dq;
+    a.g1dh = gf->dh;
+    a.g1acc = gf->dh_acc ? 1 : 0;
+    a.gsrc_acc[0] = 1;
+    a.wsplit = nullptr;
   }
   a.weight = weight;
   a.gweight = grad_weight;
@@ -2280,8 +2309,10 @@ static int conv2d_backward_impl(const dro_slice* srcs, int nsrc, const float* we
     a.rows = a.g.Cin;
     a.kch = Cout;
     const int gact = fold ? act : 0;
-    if (gf)
+    if (gf && gf->kind == 3)
       st = launch_igemm<1, 0, 3>(a, P, ws_ig, s);
+    else if (gf)
+      st = launch_igemm<1, 0, 4>(a, P, ws_ig, s);
     else
       DRO_ACT_SWITCH(gact, st = (launch_igemm<1, A_, 0>(a, P, ws_ig, s)));
     if (st) return st;
@@ -2368,10 +2399,27 @@ extern "C" int dro_convgru_candidate_backward(const dro_slice* srcs, int nsrc, c
     set_error("convgru_candidate_backward: need the r*h source");
     return DRO_E_NULL;
   }
-  const GruFold gf = {zr, h, dzr, dh};
+  const GruFold gf = {3, zr, h, dzr, dh, nullptr, nullptr, 0};
   return conv2d_backward_impl(srcs, nsrc, weight, B, H, W, hd, KH, KW, 0, 1.f, nullptr, dq, grad_srcs, grad_ctot,
                               grad_coff, grad_accumulate, nullptr, nullptr, 0, nullptr, workspace, workspace_bytes,
                               stream, &gf);
+}
+
+extern "C" int dro_convgru_gates_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H,
+                                          int W, int hd, int KH, int KW, const float* dzr_in,
+                                          float* const* grad_srcs, const int* grad_ctot, const int* grad_coff,
+                                          const int* grad_accumulate, const float* prev_zr, const float* prev_q,
+                                          const float* prev_h, float* prev_dq, float* prev_dzr, float* prev_dh,
+                                          int prev_dh_accumulate, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  if (!srcs || nsrc < 1 || !grad_srcs) {
+    set_error("convgru_gates_backward: need the h source and its gradient target");
+    return DRO_E_NULL;
+  }
+  const GruFold gf = {4, prev_zr, prev_h, prev_dzr, prev_dh, prev_q, prev_dq, prev_dh_accumulate};
+  return conv2d_backward_impl(srcs, nsrc, weight, B, H, W, 2 * hd, KH, KW, 0, 1.f, nullptr, dzr_in, grad_srcs,
+                              grad_ctot, grad_coff, grad_accumulate, nullptr, nullptr, 0, nullptr, workspace,
+                              workspace_bytes, stream, &gf);
 }
 
 // split-K partials of the parity-class data gradient, [split][class][rows][pcmax]

@@ -66,6 +66,13 @@ struct IgArgs {
   float* aux;             // EPI 1: q (saved for the backward); EPI 2: r*h  (dense, [B, hd, H, W]);
                           // MODE 1 EPI 3: dzr (its r half is written)
   int hd;                 // EPI 2: rows >= hd are the r gate
+  // MODE 1 EPI 4 (the gate conv's data gradient of a SepConvGRU's second half
+  // runs the FIRST half's stage 1 on its finished d h): z = that half's zr (z
+  // channels 0..hd), h = its input state, aux = its dzr; q, dq, dh below
+  const float* g1q;
+  float* g1dq;
+  float* g1dh;
+  int g1acc;              // 1: g1dh is added into (a gradient sink already written)
   const float* G;         // [B, Cout, H, W] gradient w.r.t. the pre-activation (or w.r.t. the
                           // output when folded: then G_pre = galpha * G * act'(gy))
   const float* gy;        // folded activation: saved output y, dense [B, Cout, H, W]
@@ -214,7 +221,17 @@ __device__ __forceinline__ void epi_store(const IgArgs& a, int row, int eb, size
     }
     a.out[((size_t)eb * a.out_ctot + a.out_coff + row) * HW + epix] = v;
   } else {
-    if (EPI == 3 && row < a.cbase[1]) {   // SepConvGRU stage 2 on d(r*h) (gru_elem_kernel)
+    if (EPI == 4 && row < a.cbase[1]) {   // finished d h -> the first half's stage 1 (gru_elem_kernel)
+      float* q = a.gsrc[0] + ((size_t)eb * a.gsrc_ctot[0] + a.gsrc_coff[0] + row) * HW + epix;
+      const float gn = *q + acc;
+      *q = gn;
+      const size_t zi = ((size_t)eb * a.z.ctot + a.z.coff + row) * HW + epix;
+      const size_t i1 = ((size_t)eb * a.hd + row) * HW + epix;
+      const float z = a.z.p[zi], qv = a.g1q[i1], hv = a.h.p[((size_t)eb * a.h.ctot + a.h.coff + row) * HW + epix];
+      a.g1dq[i1] = gn * z * (1.f - qv * qv);
+      a.aux[zi] = gn * (qv - hv) * z * (1.f - z);
+      a.g1dh[i1] = a.g1acc ? a.g1dh[i1] + gn * (1.f - z) : gn * (1.f - z);
+    } else if (EPI == 3 && row < a.cbase[1]) {   // SepConvGRU stage 2 on d(r*h) (gru_elem_kernel)
       const size_t zi = ((size_t)eb * a.z.ctot + a.z.coff + row) * HW + epix;
       const size_t hi = ((size_t)eb * a.h.ctot + a.h.coff + row) * HW + epix;
       const float r = a.z.p[zi];
@@ -279,19 +296,27 @@ __device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int
     // MODE 1 EPI 3 (SepConvGRU stage 2 folded into the candidate conv's data
     // gradient): rows of source 0 are d(r*h); they write dr~ = d h r (1-r) into
     // dzr's r half and add d r to dh (gsrc[0]) instead of storing d(r*h)
-    float gr[EPI == 3 ? 16 : 1], gh[EPI == 3 ? 16 : 1];
-    size_t gzi[EPI == 3 ? 16 : 1];
-    bool g3[EPI == 3 ? 16 : 1];
+    // MODE 1 EPI 4: rows of source 0 finish d h (accumulated); that value is
+    // the first GRU half's dh' and its stage 1 is evaluated right here
+    constexpr int NG = (EPI == 3 || EPI == 4) ? 16 : 1;
+    float gr[NG], gh[NG], gq[EPI == 4 ? 16 : 1], gd[EPI == 4 ? 16 : 1];
+    size_t gzi[NG], gi1[EPI == 4 ? 16 : 1];
+    bool g3[NG];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = rbase + (r & 3) + 8 * (r >> 2);
       const int si = row >= rows ? -1 : (row >= a.cbase[1]) + (row >= a.cbase[2]) + (row >= a.cbase[3]);
-      if (EPI == 3) {
+      if (EPI == 3 || EPI == 4) {
         g3[r] = si == 0;
         const int c = si == 0 ? row : 0;
         gzi[r] = ((size_t)eb * a.z.ctot + a.z.coff + c) * HW + epix;
         gr[r] = si == 0 ? a.z.p[gzi[r]] : 0.f;
         gh[r] = si == 0 ? a.h.p[((size_t)eb * a.h.ctot + a.h.coff + c) * HW + epix] : 0.f;
+        if constexpr (EPI == 4) {
+          gi1[r] = ((size_t)eb * a.hd + c) * HW + epix;
+          gq[r] = si == 0 ? a.g1q[gi1[r]] : 0.f;
+          gd[r] = si == 0 && a.g1acc ? a.g1dh[gi1[r]] : 0.f;
+        }
       }
       float* base = nullptr;
       int ctot = 0, coff = 0, cl = 0, ac = 0;
@@ -304,7 +329,7 @@ __device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int
         cl = row - cb;
       }
       dst[r] = base ? base + ((size_t)eb * ctot + coff + cl) * HW + epix : nullptr;
-      accf[r] = base && (ac || (EPI == 3 && si == 0));
+      accf[r] = base && (ac || ((EPI == 3 || EPI == 4) && si == 0));
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) old[r] = accf[r] ? *dst[r] : 0.f;
@@ -313,6 +338,14 @@ __device__ __forceinline__ void epi_tile(const IgArgs& a, const f32x16& acc, int
       if (EPI == 3 && g3[r]) {
         a.aux[gzi[r]] = acc[r] * gh[r] * gr[r] * (1.f - gr[r]);
         *dst[r] = old[r] + acc[r] * gr[r];
+      } else if (EPI == 4 && g3[r]) {
+        if constexpr (EPI == 4) {
+          const float gn = old[r] + acc[r], z = gr[r], qv = gq[r], hv = gh[r];
+          *dst[r] = gn;
+          a.g1dq[gi1[r]] = gn * z * (1.f - qv * qv);
+          a.aux[gzi[r]] = gn * (qv - hv) * z * (1.f - z);
+          a.g1dh[gi1[r]] = a.g1acc ? gd[r] + gn * (1.f - z) : gn * (1.f - z);
+        }
       } else if (dst[r]) {
         *dst[r] = accf[r] ? old[r] + acc[r] : acc[r];
       }

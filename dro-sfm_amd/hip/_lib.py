@@ -100,6 +100,7 @@ def load():
     _sig(lib.dro_adam_step, P, P, P, P, ctypes.c_longlong, P, P, S)
     _sig(lib.dro_gru_backward_elem, I, I, I, I, I, P, P, P, P, P, P, P, P, S)
     _sig(lib.dro_convgru_candidate_backward, P, I, P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, Z, S)
+    _sig(lib.dro_convgru_gates_backward, P, I, P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, I, P, Z, S)
     _lib = lib
     return lib
 
@@ -128,7 +129,7 @@ EXPORTED = (
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv_log", "dro_conv_log_read", "dro_conv2d_forward", "dro_convgru_gates_forward",
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",
-    "dro_gru_backward_elem", "dro_convgru_candidate_backward", "dro_adam_step",
+    "dro_gru_backward_elem", "dro_convgru_candidate_backward", "dro_convgru_gates_backward", "dro_adam_step",
 )
 
 

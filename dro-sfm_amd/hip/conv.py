@@ -688,7 +688,58 @@ def _(srcs, weight, dq, zr, h, dzr, dh, grad_srcs, accumulate):
     return None
 
 
+@torch.library.custom_op("dro::convgru_gates_backward",
+                         mutates_args=("grad_srcs", "prev_dq", "prev_dzr", "prev_dh"))
+def _gru_gates_bwd_op(srcs: list[Tensor], weight: Tensor, dzr: Tensor, grad_srcs: list[Tensor],
+                      accumulate: list[int], prev_zr: Tensor, prev_q: Tensor, prev_h: Tensor, prev_dq: Tensor,
+                      prev_dzr: Tensor, prev_dh: Tensor, prev_dh_accumulate: int) -> None:
+    """The gate conv's data gradient of a SepConvGRU's second half with the
+    first half's stage 1 in its epilogue (csrc/conv.hip
+    dro_convgru_gates_backward): srcs = [h, x...] (h = the first half's
+    output), grad_srcs[0] its dense gradient (accumulated; the finished value
+    is the first half's dh'), the first half's dq, dzr[:, :hd] and dh written
+    (dh added into when prev_dh_accumulate)."""
+    lib = _lib.load()
+    C2, Cin, KH, KW = weight.shape
+    B, hd, H, W = srcs[0].shape
+    tgt = [g if g.numel() else None for g in grad_srcs]
+    ws, nws = _workspace(B, H, W, Cin, C2, KH, KW, dzr.device)
+    ptrs, ctot, coff = _grad_targets(tgt)
+    acc = (ctypes.c_int * len(srcs))(*accumulate)
+    check(lib.dro_convgru_gates_backward(_slices(srcs), len(srcs), ptr(weight), B, H, W, hd, KH, KW,
+                                         ptr(dzr.contiguous()), ptrs, ctot, coff, acc, ptr(prev_zr), ptr(prev_q),
+                                         ptr(prev_h), ptr(prev_dq), ptr(prev_dzr), ptr(prev_dh),
+                                         int(prev_dh_accumulate), ptr(ws), nws, stream_of(dzr)),
+          "dro_convgru_gates_backward")
+
+
+@_gru_gates_bwd_op.register_fake
+def _(srcs, weight, dzr, grad_srcs, accumulate, prev_zr, prev_q, prev_h, prev_dq, prev_dzr, prev_dh,
+      prev_dh_accumulate):
+    return None
+
+
 _GRU_FOLD = os.environ.get("DRO_GRU_FOLD", "1") != "0"   # A/B: 0 keeps the separate stage-2 launch
+# A/B: 0 keeps the first half's stage-1 launch (DRO_GRU_FOLD=0 implies it)
+_GRU_CHAIN = _GRU_FOLD and os.environ.get("DRO_GRU_CHAIN", "1") != "0"
+
+
+class GruChain:
+    """Links the two halves of one SepConvGRU (SepConvGRU.forward): the second
+    half's gate-conv data gradient finishes d h = the first half's dh' and runs
+    the first half's stage 1 in its epilogue.  Only built for the two halves of
+    one GRU, whose middle state nothing else reads."""
+    __slots__ = ("first", "hn_ptr", "direct", "zr", "q", "h", "hsink", "done", "dq", "dzr", "dh", "h_in_sink")
+    folded = 0   # backward passes that ran a first half's stage 1 in the epilogue (tests)
+    stats = {"first": 0, "second": 0, "linked": 0, "bwd_linked": 0}   # (tests: why a link did not form)
+
+    def __init__(self):
+        self.first = False
+        self.done = False
+        self.hn_ptr = None
+
+
+_SEPGRU_CHAIN = []   # the GruChain of the call being set up (sepconvgru_half)
 
 
 # ------------------------------------------------------------------ dro::sepconvgru_half
@@ -754,6 +805,19 @@ def _sepgru_setup(ctx, inputs, output):
     ctx.scope = current_scope()
     ctx.keys = (("zr", wz.data_ptr(), wr.data_ptr()), ("q", wq.data_ptr()))
     ctx.direct = _SEPGRU_DIRECT.pop() if _SEPGRU_DIRECT else None
+    chain = _SEPGRU_CHAIN.pop() if _SEPGRU_CHAIN else None
+    ctx.chain_first = ctx.chain_prev = None
+    if chain is not None and _GRU_CHAIN:
+        GruChain.stats["second" if chain.first else "first"] += 1
+        if not chain.first:
+            chain.first = True
+            chain.hn_ptr = hn.data_ptr()
+            chain.direct = ctx.direct is not None
+            chain.zr, chain.q, chain.h, chain.hsink = zr, q, h, ctx.hsink
+            ctx.chain_first = chain
+        elif chain.hn_ptr == h.data_ptr() and chain.direct and ctx.direct is not None and h.requires_grad:
+            ctx.chain_prev = chain
+            GruChain.stats["linked"] += 1
 
 
 _SEPGRU_DIRECT = []   # the in-place weight-gradient targets of the call being set up (sepconvgru_half)
@@ -766,15 +830,21 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
     if dhn is None:
         return (None,) * 7 + ([None] * len(xs), None, None)
     dhn = dhn.contiguous()
-    # stage 1: pre-activation grads of q and z, dh = dh' (1-z).  When h has a
-    # gradient sink that no consumer has written yet (the next GRU step runs its
-    # backward before the heads that also read this state), dh is built right in
-    # the sink and autograd gets None for h (no add launch)
-    dq = torch.empty_like(h)
-    h_in_sink = ctx.hsink is not None and not ctx.hsink.written
-    dh = ctx.hsink.target()[0] if h_in_sink else torch.empty_like(h)
-    dzr = torch.empty_like(zr)
-    torch.ops.dro.gru_backward_elem(1, dhn, zr, q, h, None, dq, dzr, dh)
+    first = ctx.chain_first
+    if first is not None and first.done:
+        # stage 1 already ran in the second half's gate-conv epilogue
+        dq, dzr, dh, h_in_sink = first.dq, first.dzr, first.dh, first.h_in_sink
+        first.dq = first.dzr = first.dh = first.zr = first.q = first.h = first.hsink = None
+    else:
+        # stage 1: pre-activation grads of q and z, dh = dh' (1-z).  When h has a
+        # gradient sink that no consumer has written yet (the next GRU step runs its
+        # backward before the heads that also read this state), dh is built right in
+        # the sink and autograd gets None for h (no add launch)
+        dq = torch.empty_like(h)
+        h_in_sink = ctx.hsink is not None and not ctx.hsink.written
+        dh = ctx.hsink.target()[0] if h_in_sink else torch.empty_like(h)
+        dzr = torch.empty_like(zr)
+        torch.ops.dro.gru_backward_elem(1, dhn, zr, q, h, None, dq, dzr, dh)
     # candidate conv over [r*h, x]: d(r*h), dx (overwrite); sources with a
     # gradient sink are accumulated in place and get None from autograd
     drh = torch.empty_like(h)
@@ -798,7 +868,25 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
             _conv_bwd([rh, *xs], wq, None, dq, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwq, gbq, 1)
         if not (_GRU_FOLD and qb is None):
             torch.ops.dro.gru_backward_elem(2, None, zr, None, h, drh, None, dzr, dh)
-        _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), wsplit=zb)
+        p = ctx.chain_prev
+        if p is not None:
+            GruChain.stats["bwd_linked"] += 1
+        if p is not None and zb is None:
+            # this half's d h, once finished, is the first half's dh': its stage 1
+            # runs in the gate conv's epilogue (dq, dzr, dh of the first half; dh
+            # straight into the first half's input sink when it has one)
+            p.dq, p.dzr = torch.empty_like(p.h), torch.empty_like(p.zr)
+            if p.hsink is not None:
+                p.dh, pacc = p.hsink.target()
+                p.h_in_sink = True
+            else:
+                p.dh, pacc, p.h_in_sink = torch.empty_like(p.h), 0, False
+            torch.ops.dro.convgru_gates_backward([h, *xs], wzr, dzr, [dh, *[_placeholder(t, h.device) for t in tg]],
+                                                 [1] * (1 + len(xs)), p.zr, p.q, p.h, p.dq, p.dzr, p.dh, pacc)
+            p.done = True
+            GruChain.folded += 1
+        else:
+            _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [dh, *tg], [1] * (1 + len(xs)), wsplit=zb)
         if not _queue_weight_grad([h, *xs], wzr.shape, 0, 1.0, dzr, None, gwzr, gbzr):
             _conv_bwd([h, *xs], wzr, None, dzr, 0, 1.0, [None] * (1 + len(xs)), [0] * (1 + len(xs)), gwzr, gbzr, 1)
         return (dh if need_h and not h_in_sink else None, *nones, dxs, None, None)
@@ -817,8 +905,10 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
 torch.library.register_autograd("dro::sepconvgru_half", _sepgru_backward, setup_context=_sepgru_setup)
 
 
-def sepconvgru_half(h, convz, convr, convq, xs):
+def sepconvgru_half(h, convz, convr, convq, xs, chain=None):
     """h' for one SepConvGRU direction; xs: the input sources (virtual concat).
+    chain: one GruChain shared by the two halves of one SepConvGRU (the
+    second half's backward then runs the first half's stage 1).
     torch.ops.dro.sepconvgru_half."""
     direct = None
     zr = _direct_targets((convz.weight, convr.weight), (convz.bias, convr.bias), mark=False)
@@ -840,8 +930,10 @@ def sepconvgru_half(h, convz, convr, convq, xs):
                 scope.cats[key] = ent
         wzr, bzr = ent
     _SEPGRU_DIRECT[:] = [direct] if direct is not None else []
+    _SEPGRU_CHAIN[:] = [chain] if chain is not None else []
     try:
         return torch.ops.dro.sepconvgru_half(h, convz.weight, convz.bias, convr.weight, convr.bias, convq.weight,
                                              convq.bias, list(xs), wzr, bzr)[0]
     finally:
         _SEPGRU_DIRECT.clear()
+        _SEPGRU_CHAIN.clear()

@@ -22,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ... import hip
+from ...hip import conv as hip_conv
 
 _BACKEND = "hip"
 _ACT_FN = {None: lambda x: x, "relu": F.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}
@@ -134,10 +135,10 @@ class SepConvGRU(nn.Module):
         for axis, k, pad in (("1", (1, 5), (0, 2)), ("2", (5, 1), (2, 0))):
             declare(self, {g + axis: (cin, hidden_dim, k, pad) for g in ("convz", "convr", "convq")})
 
-    def _gate(self, h, xs, axis):
+    def _gate(self, h, xs, axis, chain=None):
         cz, cr, cq = (getattr(self, g + axis) for g in ("convz", "convr", "convq"))
         if _BACKEND == "hip":
-            return hip.sepconvgru_half(h, cz, cr, cq, xs)
+            return hip.sepconvgru_half(h, cz, cr, cq, xs, chain=chain)
         z, r = conv_cat([h, *xs], (cz, cr), "sigmoid")
         q = conv([r * h, *xs], cq.weight, cq.bias, "tanh")
         return (1 - z) * h + z * q
@@ -149,7 +150,10 @@ class SepConvGRU(nn.Module):
     def forward(self, h, x):
         """x: the input tensor, or a list of tensors read as their channel concat."""
         xs = _as_list(x)
-        return self._gate(self._gate(h, xs, "1"), xs, "2")
+        # the two halves' backward kernels are linked (hip.conv.GruChain): the
+        # middle state is read by the second half only
+        chain = hip_conv.GruChain() if _BACKEND == "hip" else None
+        return self._gate(self._gate(h, xs, "1", chain), xs, "2", chain)
 
 
 class _Projection(nn.Module):

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 8: dro_convgru_candidate_backward (GRU stage 2 in the candidate conv's data gradient); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 8: dro_convgru_candidate_backward / dro_convgru_gates_backward (the GRU's elementwise stages in the conv data-gradient epilogues); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -541,6 +541,23 @@ int dro_convgru_candidate_backward(const dro_slice* srcs, int nsrc, const float*
                                    float* dzr, float* dh, float* const* grad_srcs, const int* grad_ctot,
                                    const int* grad_coff, const int* grad_accumulate, void* workspace,
                                    size_t workspace_bytes, void* stream);
+
+/* The gate conv's data gradient of a SepConvGRU's SECOND half with the FIRST
+ * half's stage 1 in its epilogue (ABI 8): dro_conv2d_backward of
+ * [z|r]~ = conv([h, x...]) (Cout = 2 hd, act NONE, no weight gradient) given
+ * dzr_in, source 0 = this half's h (hd channels, gradient target
+ * grad_srcs[0] dense [B,hd,H,W], always accumulated).  h is the first half's
+ * output, so its finished gradient is the first half's dh'; each element gn
+ * is stored and turned into the first half's stage 1 (dro_gru_backward_elem):
+ *   prev_dq = gn z (1-q^2); prev_dzr[:, :hd] = gn (q-h) z (1-z);
+ *   prev_dh = gn (1-z)  (added into when prev_dh_accumulate)
+ * with z, q, h the first half's saved gate, candidate and input state. */
+int dro_convgru_gates_backward(const dro_slice* srcs, int nsrc, const float* weight, int B, int H, int W,
+                               int hd, int KH, int KW, const float* dzr_in, float* const* grad_srcs,
+                               const int* grad_ctot, const int* grad_coff, const int* grad_accumulate,
+                               const float* prev_zr, const float* prev_q, const float* prev_h, float* prev_dq,
+                               float* prev_dzr, float* prev_dh, int prev_dh_accumulate, void* workspace,
+                               size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused Adam over flat fp32 buffers (the data-parallel trainer's parameters,

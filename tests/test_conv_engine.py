@@ -434,3 +434,53 @@ def test_convgru_candidate_backward_rejects(hip):
     lib = _lib.load()
     assert lib.dro_convgru_candidate_backward(None, 0, None, 1, 1, 1, 1, 1, 5, None, None, None, None, None,
                                               None, None, None, None, None, 0, None) != 0
+
+
+@pytest.mark.parametrize("kernel,B,hd,H,W,dh_acc", [((5, 1), 2, 32, 24, 80, 0), ((1, 5), 4, 32, 24, 80, 1),
+                                                     ((3, 3), 1, 16, 13, 37, 0), ((5, 1), 1, 8, 5, 7, 1)])
+def test_convgru_gates_backward_matches_unfused(hip, kernel, B, hd, H, W, dh_acc):
+    """The second GRU half's gate-conv data gradient with the first half's
+    stage 1 in its epilogue (dro_convgru_gates_backward, ABI 8) against
+    conv2d_backward (d h accumulated) followed by gru_backward_elem stage 1 on
+    the finished d h: d h, the other sources' gradients, the first half's dq
+    and dzr (z half; r half untouched) bit for bit; its dh bit for bit when
+    written, to one rounding when added into (dh_acc)."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    KH, KW = kernel
+    cx = (24, 10)
+    h2 = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    xs = [torch.randn(B, c, H, W, device=DEV, generator=g) for c in cx]
+    wzr = torch.randn(2 * hd, hd + sum(cx), KH, KW, device=DEV, generator=g) * 0.05
+    dzr2 = torch.randn(B, 2 * hd, H, W, device=DEV, generator=g)
+    dh2_0 = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    gx0 = [torch.randn(B, c, H, W, device=DEV, generator=g) for c in cx]
+    zr1 = torch.sigmoid(torch.randn(B, 2 * hd, H, W, device=DEV, generator=g))
+    q1 = torch.tanh(torch.randn(B, hd, H, W, device=DEV, generator=g))
+    h1 = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    dzr1_0 = torch.randn(B, 2 * hd, H, W, device=DEV, generator=g)
+    dh1_0 = torch.randn(B, hd, H, W, device=DEV, generator=g)
+    acc = [1, 0, 1]
+    # two launches
+    dh2_a, gx_a = dh2_0.clone(), [t.clone() for t in gx0]
+    dq1_a, dzr1_a, dh1_a = torch.empty_like(h1), dzr1_0.clone(), torch.empty_like(h1)
+    torch.ops.dro.conv2d_backward([h2, *xs], wzr, None, dzr2, 0, 1.0, [dh2_a, *gx_a], acc, None, None, 0, None)
+    torch.ops.dro.gru_backward_elem(1, dh2_a, zr1, q1, h1, None, dq1_a, dzr1_a, dh1_a)
+    if dh_acc:
+        dh1_a = dh1_0 + dh1_a
+    # folded
+    dh2_b, gx_b = dh2_0.clone(), [t.clone() for t in gx0]
+    dq1_b, dzr1_b = torch.empty_like(h1), dzr1_0.clone()
+    dh1_b = dh1_0.clone() if dh_acc else torch.empty_like(h1)
+    torch.ops.dro.convgru_gates_backward([h2, *xs], wzr, dzr2, [dh2_b, *gx_b], acc, zr1, q1, h1, dq1_b, dzr1_b,
+                                         dh1_b, dh_acc)
+    torch.cuda.synchronize()
+    assert torch.equal(dh2_a, dh2_b)
+    for a, b in zip(gx_a, gx_b):
+        assert torch.equal(a, b)
+    assert torch.equal(dq1_a, dq1_b)
+    assert torch.equal(dzr1_a, dzr1_b)
+    assert torch.equal(dzr1_b[:, hd:], dzr1_0[:, hd:])
+    if dh_acc:
+        assert rel(dh1_b, dh1_a) < 1e-6
+    else:
+        assert torch.equal(dh1_a, dh1_b)

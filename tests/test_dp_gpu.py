@@ -217,3 +217,34 @@ def test_rccl_exchange_with_captured_graph_step(in_graph):
         assert in_bwd == nb, (in_bwd, nb)
     assert loss_err < 1e-5
     assert grad_err < 1e-4
+
+
+@pytest.mark.timeout(300)
+def test_gru_chain_matches_separate_stage1():
+    """The first SepConvGRU half's stage 1 run in the second half's gate-conv
+    data-gradient epilogue (hip.conv.GruChain, dro_convgru_gates_backward) gives
+    the training step's gradient of the separate-launch form, to fp32
+    reassociation (a first half whose input-state sink is already written is
+    now added into in the epilogue instead of by the sink's add)."""
+    from dro_sfm_amd.hip import conv as C
+    from dro_sfm_amd.trainers.dp_trainer import DataParallelTrainer
+    prev, out, folded = C._GRU_CHAIN, {}, {}
+    try:
+        for chain in (False, True):
+            C._GRU_CHAIN = chain
+            with torch.backends.cudnn.flags(enabled=False):
+                m = _model(seed=0)
+                tr = DataParallelTrainer(m, lr=0.0, bucket_mb=4.0)
+                tr.step(_batch(0, 0))       # the first step sets up the in-place weight gradients
+                n0 = C.GruChain.folded
+                tr.step(_batch(0, 1))
+                torch.cuda.synchronize()
+                out[chain] = tr.grads.flat.detach().cpu().clone()
+            folded[chain] = C.GruChain.folded - n0
+    finally:
+        C._GRU_CHAIN = prev
+    assert folded[False] == 0 and folded[True] == 16, (folded, C.GruChain.stats)   # 8 iterations x (depth, pose)
+    a, b = out[True], out[False]
+    l2 = float((a - b).norm() / b.norm())
+    mx = float((a - b).abs().max() / b.abs().max())
+    assert l2 < 1e-5 and mx < 1e-4, (l2, mx)

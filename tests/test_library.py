@@ -42,7 +42,7 @@ SCHEMAS = {
 }
 BACKWARD_OPS = ["warp_cost_backward", "view_synthesis_backward", "photometric_loss_backward",
                 "supervised_loss_backward", "convex_upsample_backward", "convex_upsample_many_backward",
-                "conv2d_backward", "conv2d_strided_backward", "gru_backward_elem", "convgru_candidate_backward",
+                "conv2d_backward", "conv2d_strided_backward", "gru_backward_elem", "convgru_candidate_backward", "convgru_gates_backward",
                 "pose_mean_backward",
                 "maxpool3x3s2_backward", "bilinear_upsample2x_backward"]
 
