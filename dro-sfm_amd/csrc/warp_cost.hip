@@ -42,6 +42,7 @@ struct WarpArgs {
   int B, N, C, h, w;
   int reduce_mean;
   int acc_fmap;      // backward: add into grad_fmap
+  int acc_depth;     // backward: add into grad_depth
   int* cells;        // backward test hook: bilinear cell per (n, b, p) (pack_cell), or NULL
   int merge;         // backward: merge runs of lanes sharing a cell before the scatter (default 1;
                      // DRO_WARP_NOMERGE=1 for A/B measurements)
@@ -645,7 +646,8 @@ __global__ __launch_bounds__(256) void warp_cost_bwd_feat_cl_kernel(WarpArgs a, 
   if (GEO && gdepth && threadIdx.x < pn) {
     float dd;
     decode_depth(a.depth[b * P + p0 + threadIdx.x], a.depth_mode, a.min_disp, a.span, &dd);
-    gdepth[b * P + p0 + threadIdx.x] = gdep * dd;
+    float* gq = gdepth + b * P + p0 + threadIdx.x;
+    *gq = a.acc_depth ? *gq + gdep * dd : gdep * dd;
   }
   if (gfmap) {
     __syncthreads();                        // f_l reused as the output tile
@@ -698,7 +700,7 @@ __global__ __launch_bounds__(kGeoThreads) void warp_cost_bwd_geo_kernel(
       }
     }
   }
-  if (gdepth && live) gdepth[b * P + p] = gd_total * dd;
+  if (gdepth && live) gdepth[b * P + p] = a.acc_depth ? gdepth[b * P + p] + gd_total * dd : gd_total * dd;
 }
 
 // One 256-thread block per pose: threads 0..239 = 20 row groups x 12
@@ -919,6 +921,7 @@ static WarpArgs make_args(const float* fmap, const float* fmap_ref, const float*
                           int N, int C, int h, int w, int reduce_mean) {
   WarpArgs a;
   a.acc_fmap = 0;
+  a.acc_depth = 0;
   a.cells = nullptr;
   a.fmap = fmap;
   a.fmap_ref = fmap_ref;
@@ -998,12 +1001,13 @@ static int warp_backward(WarpArgs a, const float* grad_out, float* grad_fmap, fl
     set_error("warp backward: workspace required for depth/pose gradients");
     return DRO_E_NULL;
   }
-  if (accumulate < 0 || accumulate > 3) {
-    set_error("warp backward: accumulate must be 0..3");
+  if (accumulate < 0 || accumulate > 7) {
+    set_error("warp backward: accumulate must be 0..7");
     return DRO_E_MODE;
   }
   int st;
   a.acc_fmap = accumulate & 1;
+  a.acc_depth = (accumulate >> 2) & 1;
   a.cells = cells;
   static const int nomerge = env_int("DRO_WARP_NOMERGE", 0);
   a.merge = nomerge ? 0 : 1;

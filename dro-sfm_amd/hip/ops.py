@@ -8,6 +8,7 @@ launches on the current stream.  Differentiable ops register their backward
 kernel with the output shapes; tests/test_library.py checks the schemas.
 """
 import contextlib
+import os
 import ctypes
 from typing import Optional
 
@@ -85,6 +86,9 @@ class _GradSink(torch.autograd.Function):
 
 
 _SINKS = [True]
+# A/B: DRO_DEPTH_SINK=0 returns the cost's depth gradient to autograd instead
+# of adding it into the depth state's sink
+_DEPTH_SINK = os.environ.get("DRO_DEPTH_SINK", "1") != "0"
 
 
 def set_grad_sinks(enabled):
@@ -246,17 +250,19 @@ def _(fmap, fmap_ref, depth, pose, K, ref_K, depth_mode, min_disp, max_disp, sca
 
 
 @torch.library.custom_op("dro::warp_cost_backward",
-                         mutates_args=("grad_fmap_out", "grad_fmap_ref_out", "cells"))
+                         mutates_args=("grad_fmap_out", "grad_fmap_ref_out", "cells", "grad_depth_out"))
 def _warp_cost_bwd_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tensor, K: Tensor, ref_K: Tensor,
                       grad_cost: Tensor, depth_mode: int, min_disp: float, max_disp: float, scale: float,
                       pose_mode: int, reduce_mean: bool, need_fmap: bool, need_fmap_ref: bool, need_depth: bool,
                       need_pose: bool, grad_fmap_out: Optional[Tensor], grad_fmap_ref_out: Optional[Tensor],
-                      accumulate: int, cells: Optional[Tensor]) -> list[Tensor]:
-    """Backward of dro::warp_cost.  grad_fmap_out / grad_fmap_ref_out: buffers
-    the feature gradients are written (accumulate bit 0 / 1: added) into in
-    place -- the gradient sinks of maps every cost call of a step shares; the
-    returned gradient of such an input is empty.  Returns [g_fmap, g_fmap_ref,
-    g_depth, g_pose] (empty where not needed)."""
+                      accumulate: int, cells: Optional[Tensor],
+                      grad_depth_out: Optional[Tensor]) -> list[Tensor]:
+    """Backward of dro::warp_cost.  grad_fmap_out / grad_fmap_ref_out /
+    grad_depth_out: buffers the feature / depth gradients are written
+    (accumulate bit 0 / 1 / 2: added) into in place -- the gradient sinks of
+    maps every cost call of a step shares and of the depth state; the returned
+    gradient of such an input is empty.  Returns [g_fmap, g_fmap_ref, g_depth,
+    g_pose] (empty where not needed)."""
     lib = _lib.load()
     B, C, h, w = fmap.shape
     N = fmap_ref.shape[0]
@@ -269,7 +275,7 @@ def _warp_cost_bwd_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tenso
     g_f = grad_fmap_out if grad_fmap_out is not None else (torch.empty_like(fmap) if need_fmap else None)
     g_r = grad_fmap_ref_out if grad_fmap_ref_out is not None else (
         torch.empty_like(fmap_ref) if need_fmap_ref else None)
-    g_d = torch.empty_like(depth) if need_depth else None
+    g_d = grad_depth_out if grad_depth_out is not None else (torch.empty_like(depth) if need_depth else None)
     g_p = torch.empty_like(pose) if need_pose else None
     ws = None
     if g_d is not None or g_p is not None or cells is not None:
@@ -281,18 +287,19 @@ def _warp_cost_bwd_op(fmap: Tensor, fmap_ref: Tensor, depth: Tensor, pose: Tenso
                                      ptr(g_p), accumulate, ptr(ws), ptr(cells), stream_of(fmap)),
           "dro_warp_cost_backward")
     out = lambda g, own: g if (g is not None and not own) else _none_like(dev)
-    return [out(g_f, grad_fmap_out is not None), out(g_r, grad_fmap_ref_out is not None), out(g_d, False),
-            out(g_p, False)]
+    return [out(g_f, grad_fmap_out is not None), out(g_r, grad_fmap_ref_out is not None),
+            out(g_d, grad_depth_out is not None), out(g_p, False)]
 
 
 @_warp_cost_bwd_op.register_fake
 def _(fmap, fmap_ref, depth, pose, K, ref_K, grad_cost, depth_mode, min_disp, max_disp, scale, pose_mode,
       reduce_mean, need_fmap, need_fmap_ref, need_depth, need_pose, grad_fmap_out, grad_fmap_ref_out, accumulate,
-      cells):
+      cells, grad_depth_out):
     e = fmap.new_empty(0)
     return [fmap.new_empty(fmap.shape) if need_fmap and grad_fmap_out is None else e,
             fmap_ref.new_empty(fmap_ref.shape) if need_fmap_ref and grad_fmap_ref_out is None else e,
-            depth.new_empty(depth.shape) if need_depth else e, pose.new_empty(pose.shape) if need_pose else e]
+            depth.new_empty(depth.shape) if need_depth and grad_depth_out is None else e,
+            pose.new_empty(pose.shape) if need_pose else e]
 
 
 def _warp_cost_setup(ctx, inputs, output):
@@ -300,23 +307,28 @@ def _warp_cost_setup(ctx, inputs, output):
     ctx.save_for_backward(fmap, fmap_ref, depth, pose, K, ref_K, cells)
     ctx.cfg = (depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean)
     ctx.need = (fmap.requires_grad, fmap_ref.requires_grad, depth.requires_grad, pose.requires_grad)
-    # maps shared by every cost call of a step: gradients summed in their sinks
-    ctx.sinks = (_sink_of(fmap) if ctx.need[0] else None, _sink_of(fmap_ref) if ctx.need[1] else None)
+    # maps shared by every cost call of a step (and the depth state): gradients
+    # summed in their sinks
+    ctx.sinks = (_sink_of(fmap) if ctx.need[0] else None, _sink_of(fmap_ref) if ctx.need[1] else None,
+                 _sink_of(depth) if ctx.need[2] and _DEPTH_SINK else None)
 
 
 def _warp_cost_backward(ctx, gcost):
     fmap, fmap_ref, depth, pose, K, ref_K, cells = ctx.saved_tensors
     depth_mode, min_disp, max_disp, scale, pose_mode, reduce_mean = ctx.cfg
-    sf, sr = ctx.sinks
-    acc, bf, br = 0, None, None
+    sf, sr, sd = ctx.sinks
+    acc, bf, br, bd = 0, None, None, None
     if sf is not None:
         bf, a = sf.target()
         acc |= a
     if sr is not None:
         br, a = sr.target()
         acc |= 2 * a
+    if sd is not None:
+        bd, a = sd.target()
+        acc |= 4 * a
     g = torch.ops.dro.warp_cost_backward(fmap, fmap_ref, depth, pose, K, ref_K, gcost, depth_mode, min_disp,
-                                         max_disp, scale, pose_mode, reduce_mean, *ctx.need, bf, br, acc, cells)
+                                         max_disp, scale, pose_mode, reduce_mean, *ctx.need, bf, br, acc, cells, bd)
     return (*[_opt(t) for t in g], None, None, None, None, None, None, None, None, None)
 
 

@@ -86,9 +86,10 @@ size_t dro_warp_cost_workspace_bytes(int B, int N, int h, int w);
  * grad_depth is w.r.t. the depth input in its depth_mode encoding; grad_pose
  * is w.r.t. the pose input in its pose_mode encoding.  `workspace` must hold
  * dro_warp_cost_workspace_bytes() bytes when grad_depth or grad_pose is set.
- * accumulate: bit 0 adds into grad_fmap, bit 1 into grad_fmap_ref (otherwise
- * they are overwritten) -- the feature maps are shared by every cost call of a
- * step, so their gradients can be summed in place (hip.grad_sink).
+ * accumulate: bit 0 adds into grad_fmap, bit 1 into grad_fmap_ref, bit 2 into
+ * grad_depth (otherwise they are overwritten) -- the feature maps are shared by
+ * every cost call of a step and the depth state by the cost, the depth encoder
+ * and the update, so their gradients can be summed in place (hip.grad_sink).
  * cells (test hook, NULL in production): int32 [N,B,h,w] receives the bilinear
  * cell each pixel's sampling position fell in, packed ((y0 + 32768) << 16) |
  * (x0 + 32768) -- the branch of grid_sample's piecewise-linear derivative this

@@ -923,3 +923,43 @@ def test_train_step_kitti_metric_config(hip):
     """Metric config (KITTI 192x640, it8-seq4-inter-out, B=2, N=2, self-sup;
     _full_size_step)."""
     _full_size_step("kitti")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["nchw", "cl"])
+def test_warp_cost_depth_gradient_into_sink(hip, layout):
+    """The cost backward adds its depth gradient into the depth state's
+    gradient sink (accumulate bit 2) when the state has one
+    (BasicUpdateBlockDepth): the depth gradient equals the one autograd sums
+    from the returned gradient, with the sink written first by the cost (bit 2
+    clear) and after another consumer (bit 2 set)."""
+    from dro_sfm_amd.hip import ops
+    B, C, h, w, N = 2, 64, 12, 20, 2
+    g = torch.Generator().manual_seed(29)
+    K = kitti_K(B, W=8 * w, H=8 * h).to(DEV)
+    fmap, frefs = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    disp = torch.rand(B, 1, h, w, generator=g)
+    poses = torch.cat([0.2 * torch.randn(N, B, 3, generator=g), 0.05 * torch.randn(N, B, 3, generator=g)], 2)
+    G = torch.randn(B, C, h, w, generator=g).to(DEV)
+    Wd = torch.randn(B, 1, h, w, generator=g).to(DEV)
+    W2 = torch.randn(B, 1, h, w, generator=g).to(DEV)
+    prev = ops._DEPTH_SINK
+    res = {}
+    try:
+        for use in (False, True):
+            ops._DEPTH_SINK = use
+            for cost_first in (True, False):
+                dg = disp.to(DEV).requires_grad_(True)
+                ds = hip.grad_sink(dg)
+                rg = _ref_leaf(hip, frefs, layout)
+                cost = hip.warp_cost(fmap.to(DEV), rg, ds, poses.to(DEV), K, depth_mode=hip.DEPTH_DISP,
+                                     min_depth=0.5, max_depth=80.0)
+                # another consumer of the depth state, before or after the cost in the backward
+                other = hip.conv2d([ds], W2.new_ones(1, 1, 3, 3), None) if not cost_first else ds * Wd
+                ((cost * G).sum() + (other * Wd).sum()).backward()
+                res[(use, cost_first)] = dg.grad.detach().clone()
+    finally:
+        ops._DEPTH_SINK = prev
+    for cf in (True, False):
+        a, b = res[(False, cf)], res[(True, cf)]
+        assert float((a - b).abs().max() / b.abs().max()) < 1e-6, cf
