@@ -304,6 +304,12 @@ __device__ __forceinline__ float ssim_value(const SsimStats& s, float C1, float 
   return num / den;
 }
 
+// torch.clamp(v, max=thr) with its NaN handling: a NaN value or a NaN bound
+// gives NaN (fminf would return the other operand)
+__device__ __forceinline__ float clamp_max(float v, float thr) {
+  return (v > thr || thr != thr) ? thr : v;
+}
+
 __device__ __forceinline__ float clamp_ssim_loss(float ssim) {
   return fminf(fmaxf((1.f - ssim) / 2.f, 0.f), 1.f);
 }
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
       const size_t gp = (size_t)(y0 + ly) * W + x0 + lx;
       float vw;
       if (MODE == kPhotoSelect) {
-        vw = fminf(pmj[gp], a.thr[j * a.n + i]);          // torch.clamp(max=...)
+        vw = clamp_max(pmj[gp], a.thr[j * a.n + i]);      // torch.clamp(max=...)
       } else {
         vw = photo_value(a, est, tgt, o, W1, PL);
         if (MODE == kPhotoStore) {
@@ -461,7 +467,7 @@ __global__ __launch_bounds__(kThreads) void photo_fwd_kernel(PhotoArgs a) {
       }
       if (a.automask) {
         float vu = a.am[((size_t)j * a.B + b) * HW + gp];
-        if (MODE == kPhotoSelect) vu = fminf(vu, a.thr[a.N * a.n + j]);
+        if (MODE == kPhotoSelect) vu = clamp_max(vu, a.thr[a.N * a.n + j]);
         if (a.reduce_min) {
           if (vu < best[r]) {
             best[r] = vu;

@@ -440,7 +440,8 @@ __global__ __launch_bounds__(256) void warp_cost_fwd_cl_kernel(WarpArgs a, float
         if (j < pn && lane < cn) {
           float val = 0.f;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) val += fr[(size_t)T.idx[j][e] * a.C] * T.wgt[j][e];
+          for (int e = 0; e < 4; ++e)   // in-image taps only (zeros padding: an Inf / NaN elsewhere stays out)
+            if ((T.ok[j] >> e) & 1) val += fr[(size_t)T.idx[j][e] * a.C] * T.wgt[j][e];
           const float d = f_l[lane][j] - val;
           if (a.reduce_mean)
             acc[k] += d * d;

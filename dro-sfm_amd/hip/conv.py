@@ -702,6 +702,11 @@ def _gru_gates_bwd_op(srcs: list[Tensor], weight: Tensor, dzr: Tensor, grad_srcs
     lib = _lib.load()
     C2, Cin, KH, KW = weight.shape
     B, hd, H, W = srcs[0].shape
+    # the first half's tensors are read as dense [B, hd|2hd, H, W] arrays
+    for name, t in (("prev_zr", prev_zr), ("prev_q", prev_q), ("prev_h", prev_h), ("prev_dq", prev_dq),
+                    ("prev_dzr", prev_dzr), ("prev_dh", prev_dh)):
+        if not t.is_contiguous():
+            raise RuntimeError(f"convgru_gates_backward: {name} must be contiguous")
     tgt = [g if g.numel() else None for g in grad_srcs]
     ws, nws = _workspace(B, H, W, Cin, C2, KH, KW, dzr.device)
     ptrs, ctot, coff = _grad_targets(tgt)
@@ -795,7 +800,8 @@ def _sepgru_setup(ctx, inputs, output):
     # passes one; a direct op call without it gets the same concatenation)
     wzr = wzr_in if wzr_in is not None else torch.cat([wz, wr], 0).detach().contiguous()
     ctx.wsplit = (_wsplit_bwd(wzr), _wsplit_bwd(wq.contiguous()))
-    ctx.save_for_backward(h.contiguous(), rh, wzr, wq.contiguous(), zr, q, *xs)
+    hc = h.contiguous()    # the dense state both this half's and a linked second half's backward read
+    ctx.save_for_backward(hc, rh, wzr, wq.contiguous(), zr, q, *xs)
     ctx.mark_non_differentiable(zr, rh, q)
     ctx.set_materialize_grads(False)     # no zero-filled gradients for the three saved outputs
     ctx.sinks = [_sink_of(x) if x.requires_grad else None for x in xs]
@@ -813,7 +819,7 @@ def _sepgru_setup(ctx, inputs, output):
             chain.first = True
             chain.hn_ptr = hn.data_ptr()
             chain.direct = ctx.direct is not None
-            chain.zr, chain.q, chain.h, chain.hsink = zr, q, h, ctx.hsink
+            chain.zr, chain.q, chain.h, chain.hsink = zr, q, hc, ctx.hsink
             ctx.chain_first = chain
         elif chain.hn_ptr == h.data_ptr() and chain.direct and ctx.direct is not None and h.requires_grad:
             ctx.chain_prev = chain
@@ -832,9 +838,12 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
     dhn = dhn.contiguous()
     first = ctx.chain_first
     if first is not None and first.done:
-        # stage 1 already ran in the second half's gate-conv epilogue
+        # stage 1 already ran in the second half's gate-conv epilogue; the link is
+        # one-shot: a second backward through the graph (retain_graph) finds the
+        # chain's tensors released and runs both halves unlinked
         dq, dzr, dh, h_in_sink = first.dq, first.dzr, first.dh, first.h_in_sink
         first.dq = first.dzr = first.dh = first.zr = first.q = first.h = first.hsink = None
+        first.done = False
     else:
         # stage 1: pre-activation grads of q and z, dh = dh' (1-z).  When h has a
         # gradient sink that no consumer has written yet (the next GRU step runs its
@@ -871,6 +880,8 @@ def _sepgru_backward(ctx, dhn, _gzr, _grh, _gq):
         p = ctx.chain_prev
         if p is not None:
             GruChain.stats["bwd_linked"] += 1
+        if p is not None and p.h is None:
+            p = None           # the chain was consumed by an earlier backward pass
         if p is not None and zb is None:
             # this half's d h, once finished, is the first half's dh': its stage 1
             # runs in the gate conv's epilogue (dq, dzr, dh of the first half; dh

@@ -37,6 +37,7 @@ backward -> (all-reduce) -> Adam step.
 """
 import os
 import sys
+import time
 
 import torch
 import torch.distributed as dist
@@ -44,21 +45,39 @@ import torch.distributed as dist
 
 def graph_safe_nccl_env():
     """Environment for RCCL collectives captured in hipGraphs, set before the
-    process group is created (explicit settings win).  The ProcessGroupNCCL
-    watchdog thread polls the events of the collectives it tracks; while a
-    step is being captured it has been seen to query an event last recorded
-    inside the capture and, with the default settings, to abort the process
-    from the watchdog thread ('operation not permitted on an event last
-    recorded in a capturing stream'; round 5, the world-1 RCCL capture test,
-    about 1 run in 7).  The flight recorder and the event cache (event
-    objects recycled between eager and captured collectives) are off, and a
-    HIP error seen by the watchdog's event queries is logged instead of
-    rethrown (TORCH_NCCL_RETHROW_CUDA_ERRORS=0): the collective itself is
-    unaffected, and a real device error still surfaces at the step's next
-    synchronisation."""
+    process group is created (explicit settings win): no flight recorder and
+    no event cache (event objects recycled between eager and captured
+    collectives).  Neither hides an error: a HIP error the watchdog sees still
+    aborts the process, as by default.  The capture abort of round 5 was the
+    watchdog polling the warm-up steps' eager collectives inside the capture
+    (drain_watchdog)."""
     os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "0")
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
+
+
+# ProcessGroupNCCL's watchdog retires completed works once per poll (every
+# 100 ms in this torch); waiting three polls covers a late one
+_WATCHDOG_DRAIN_S = float(os.environ.get("DRO_WATCHDOG_DRAIN_S", "0.3"))
+
+
+def drain_watchdog():
+    """Block until the RCCL watchdog can no longer hold an eager collective.
+
+    Cause of the round-5 abort (hipErrorCapturedEvent thrown by the watchdog
+    thread, `WorkNCCL::finishedGPUExecutionInternal`, while GraphedTrainStep
+    captured with collectives inside): the watchdog tracks every EAGER
+    collective until a poll finds it complete -- up to one poll interval after
+    it finished.  The warm-up steps' last all-reduces were still tracked when
+    the capture began; their end events were recorded on RCCL's internal
+    stream, which the first captured collective pulls into the capture; a
+    poll landing after that queried an event whose stream was capturing and
+    got hipErrorCapturedEvent (timing-dependent: "1 run in 7";
+    tools/rccl_watchdog_probe.py makes the window deterministic).  Captured
+    collectives are never tracked, so after this wait the capture has nothing
+    for the watchdog to query."""
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    time.sleep(_WATCHDOG_DRAIN_S)
 
 
 def init_distributed(backend=None):
@@ -126,6 +145,14 @@ class GradBuckets:
         self.buckets, self._pending, self._seen = [], [], set()
         self.issued = []              # bucket indices in issue order (last step; tests)
         self.issued_in_backward = 0   # of those, issued from backward hooks (tests)
+        # GraphedTrainStep sets this to the capture's origin stream while it
+        # captures with collectives inside; each collective's issuing stream
+        # must then be part of the capture (issue_capturing, one flag per
+        # collective of the last step): a collective issued from a stream
+        # outside the capture is tracked by RCCL's watchdog as eager while its
+        # kernel and end event land in the capture through RCCL's own stream
+        self.capture_origin = None
+        self.issue_capturing = []
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         # the stream every bucket's collective is issued from: created here, never
         # during a graph capture (a stream first created inside a capture was
@@ -239,6 +266,8 @@ class GradBuckets:
                 for st in self._bside[b]:
                     comm.wait_stream(st)
                 with torch.cuda.stream(comm):
+                    if self.capture_origin is not None:
+                        self.issue_capturing.append(torch.cuda.is_current_stream_capturing())
                     self._pending.append(dist.all_reduce(self._slice(self.buckets[b]), op=dist.ReduceOp.SUM,
                                                          group=self.group, async_op=True))
 
@@ -268,6 +297,7 @@ class GradBuckets:
         self.flat.zero_()
         self._pending = []
         self.issued = []
+        self.issue_capturing = []
         if self.active is not None:
             self._left = list(self._need)
             self._ready = [False] * len(self.buckets)
@@ -700,6 +730,10 @@ class GraphedTrainStep:
                 self._body(flips[i % len(flips)])
         cur.wait_stream(side)
         torch.cuda.synchronize()
+        if self.in_graph:
+            # the warm-up's eager collectives must be retired by the RCCL watchdog
+            # before any collective is captured (drain_watchdog)
+            drain_watchdog()
         self.pool = torch.cuda.graph_pool_handle() if share_pool else None
         group, dev = trainer.grads.group, trainer.grads.flat.device
         if not self.in_graph:
@@ -726,15 +760,26 @@ class GraphedTrainStep:
         check_same_across_ranks(next(iter(seqs)), group, dev, "captured collective sequence")
 
     def _capture_all(self, flips):
-        self.graphs, self.issue_seq = {}, {}
+        self.graphs, self.issue_seq, self.issue_capturing = {}, {}, {}
         for f in flips:
             g = torch.cuda.CUDAGraph()
             # thread_local: the RCCL watchdog thread queries the events of the
             # warm-up steps' collectives; under the default (global) mode that
             # query from another thread invalidated the capture (measured:
             # hipErrorStreamCaptureUnsupported in the watchdog, then an abort)
+            grads = self.tr.grads
             with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
-                out = self._captured(f)
+                grads.capture_origin = torch.cuda.current_stream() if self.in_graph else None
+                try:
+                    out = self._captured(f)
+                finally:
+                    grads.capture_origin = None
+            if self.in_graph and not all(grads.issue_capturing):
+                # such a collective would run in the graph AND be polled by the
+                # watchdog as an eager one (its end event inside the capture)
+                raise RuntimeError(f"GraphedTrainStep: {grads.issue_capturing.count(False)} collective(s) "
+                                   "issued from a stream outside the capture")
+            self.issue_capturing[f] = list(grads.issue_capturing)
             self.graphs[f] = (g, out)
             # in-graph: the buckets the hooks issued inside this capture; after
             # replay: reduce_now's fixed runs (the same for every graph)

@@ -133,6 +133,7 @@ class Cells:
     def __init__(self, forced=None, record=False):
         self.forced = forced or {}
         self.recorded = {} if record else None
+        self.thresholds = {}      # clip index -> this evaluation's own clip threshold (photometric_map)
 
     def sample(self, img, grid, key):
         return grid_sample_cells(img, grid, self.forced.get(key), self, key)
@@ -172,8 +173,10 @@ def cells_from_calls(calls):
             for j in range(c.shape[0]):
                 for i in range(c.shape[1]):
                     out[("photo", j, i)] = c[j, i]
-        elif tag == "photo_clip":             # float [N*n + N] clip thresholds (photometric_map)
-            out[("clip", "thr")] = cells.cpu()
+        elif tag == "photo_clip":
+            # the product's float [N*n + N] clip thresholds: compared by the tests
+            # with the oracle's own (Cells.thresholds), never used by the oracle
+            continue
         elif tag == "photo_clipmask":         # uint8 [N,n,B,H,W]: value <= threshold (not clamped)
             for j in range(c.shape[0]):
                 for i in range(c.shape[1]):
@@ -334,10 +337,12 @@ def photometric_map(est, tgt, ssim_w, C1, C2, clip_loss=0.0, cells=None, key=Non
     """calc_photometric_loss (multiview_photometric_loss_mf.py:194-229) of one
     [B,3,H,W] pair.  clip_loss > 0 (:223-227): the map is clamped from above
     at float(mean + clip_loss * std) of itself (unbiased std, a detached
-    constant computed in the map's dtype); with a Cells book holding
-    ("clip", "thr") -- another evaluation's thresholds -- entry clip_index is
-    used instead (a pixel within rounding of its map's threshold is clamped or
-    not by rounding: the oracle then takes the other evaluation's side)."""
+    constant computed in the map's dtype, always by this evaluation itself:
+    a Cells book gets it as thresholds[clip_index], for the tests to compare
+    with the product's).  With a Cells book holding ("clipkeep", key) --
+    another evaluation's clamp decisions -- a pixel within CLIP_TOL of the
+    threshold (clamped or not by rounding) takes the other evaluation's side;
+    the clamp itself is continuous, so only the derivative's branch is pinned."""
     l1 = l1_pinned(est - tgt, cells, key)
     if ssim_w <= 0.0:
         out = l1
@@ -345,12 +350,10 @@ def photometric_map(est, tgt, ssim_w, C1, C2, clip_loss=0.0, cells=None, key=Non
         s = torch.clamp((1.0 - ssim(est, tgt, C1, C2)) / 2.0, 0.0, 1.0)
         out = ssim_w * s.mean(1, True) + (1 - ssim_w) * l1.mean(1, True)
     if clip_loss > 0.0:
-        forced = cells.forced.get(("clip", "thr")) if cells is not None else None
-        if forced is not None and clip_index is not None:
-            thr = float(forced[clip_index])
-        else:
-            mean, std = out.mean(), out.std()
-            thr = float(mean + clip_loss * std)
+        mean, std = out.mean(), out.std()
+        thr = float(mean + clip_loss * std)
+        if cells is not None and clip_index is not None:
+            cells.thresholds[clip_index] = thr
         keep = cells.forced.get(("clipkeep", key)) if cells is not None and key is not None else None
         if keep is not None:
             # the other evaluation's clamp decision where the value is within

@@ -484,3 +484,53 @@ def test_convgru_gates_backward_matches_unfused(hip, kernel, B, hd, H, W, dh_acc
         assert rel(dh1_b, dh1_a) < 1e-6
     else:
         assert torch.equal(dh1_a, dh1_b)
+
+
+def test_convgru_gates_backward_rejects_strided_state(hip):
+    """the first half's tensors are read as dense arrays; a strided
+    one is refused instead of being read at the wrong elements."""
+    B, hd, H, W = 2, 8, 5, 7
+    h2 = torch.randn(B, hd, H, W, device=DEV)
+    wzr = torch.randn(2 * hd, hd, 1, 5, device=DEV)
+    dzr2 = torch.randn(B, 2 * hd, H, W, device=DEV)
+    zr1 = torch.rand(B, 2 * hd, H, W, device=DEV)
+    q1 = torch.rand(B, hd, H, W, device=DEV)
+    h1 = torch.randn(B, 2 * hd, H, W, device=DEV)[:, :hd]          # a channel slice
+    with pytest.raises(RuntimeError, match="contiguous"):
+        torch.ops.dro.convgru_gates_backward([h2], wzr, dzr2, [torch.zeros_like(h2)], [1], zr1, q1, h1,
+                                             torch.empty_like(q1), torch.empty_like(zr1), torch.empty_like(q1), 0)
+
+
+def test_gru_chain_second_backward(hip):
+    """the GruChain link is one-shot.  A second backward through the
+    same graph (retain_graph) runs both halves unlinked and adds the same
+    gradients again (2x the first pass, to fp32 reassociation)."""
+    from dro_sfm_amd.hip import conv as C
+    from dro_sfm_amd.networks.optim.update import SepConvGRU
+    from dro_sfm_amd.trainers.dp_trainer import GradBuckets, flatten_parameters
+    if not C._GRU_CHAIN:
+        pytest.skip("GRU chain disabled (DRO_GRU_CHAIN=0)")
+    torch.manual_seed(3)
+    B, hd, cx, H, W = 2, 32, 48, 12, 20
+    gru = SepConvGRU(hidden_dim=hd, input_dim=cx).to(DEV)
+    with torch.no_grad():
+        for p in gru.parameters():
+            p.mul_(0.5)
+    buckets = GradBuckets(list(gru.parameters()), groups=gru.dro_param_groups())
+    # the trainer's layout: fused weights are views of one flat parameter buffer
+    flatten_parameters(buckets.params, buckets.offsets, buckets.flat.numel(), buckets.flat.device)
+    h = torch.randn(B, hd, H, W, device=DEV).tanh().requires_grad_()
+    x = torch.randn(B, cx, H, W, device=DEV).requires_grad_()
+    gout = torch.randn(B, hd, H, W, device=DEV)
+    with C.weight_grad_scope():
+        out = gru(h, x)
+    n0 = C.GruChain.folded
+    (out * gout).sum().backward(retain_graph=True)
+    torch.cuda.synchronize()
+    assert C.GruChain.folded == n0 + 1               # the first pass ran linked
+    g1 = [buckets.flat.clone(), h.grad.clone(), x.grad.clone()]
+    (out * gout).sum().backward()
+    torch.cuda.synchronize()
+    assert C.GruChain.folded == n0 + 1               # the second pass ran unlinked
+    for a, b in zip([buckets.flat, h.grad, x.grad], g1):
+        assert rel(a, 2 * b) < 1e-5

@@ -161,6 +161,7 @@ def _rccl_graph_worker(rank, port, out, in_graph):
         gs = GraphedTrainStep(tr, batch, warmup=2, flips=(False, True), reduce_in_graph=in_graph)
         stage("captured")
         seqs = dict(gs.issue_seq)
+        capflags = {f: list(v) for f, v in gs.issue_capturing.items()}
         assert gs.in_graph == in_graph and gs.outside == (not in_graph)
         nb, issued = len(tr.grads.buckets), list(tr.grads.issued)
         in_bwd = tr.grads.issued_in_backward
@@ -186,7 +187,7 @@ def _rccl_graph_worker(rank, port, out, in_graph):
         ge = tr.grads.flat.clone()
         torch.cuda.synchronize()
         out["res"] = (nb, issued, in_bwd, O.rel_err(lg.cpu(), le.cpu()), float((gg - ge).norm() / ge.norm()),
-                      seqs)
+                      seqs, capflags)
     stage("results recorded; teardown")
     # the graphs hold RCCL kernels of this communicator: release them first
     del gs
@@ -207,7 +208,7 @@ def test_rccl_exchange_with_captured_graph_step(in_graph):
     with mp.Manager() as mgr:
         out = mgr.dict()
         mp.spawn(_rccl_graph_worker, args=(_free_port(), out, in_graph), nprocs=1, join=True)
-        nb, issued, in_bwd, loss_err, grad_err, seqs = out["res"]
+        nb, issued, in_bwd, loss_err, grad_err, seqs, capflags = out["res"]
     assert nb > 2 and issued == list(range(nb))
     # both flip graphs captured, with the same collective sequence
     assert set(seqs) == {False, True} and seqs[False] == seqs[True], seqs
@@ -215,6 +216,9 @@ def test_rccl_exchange_with_captured_graph_step(in_graph):
         assert [b for b, _, _ in seqs[False]] == list(range(nb))
     if in_graph:
         assert in_bwd == nb, (in_bwd, nb)
+        # every captured collective was issued from a stream inside the capture
+        # (else RCCL's watchdog tracks it as eager: the round-5 abort)
+        assert all(len(v) == nb and all(v) for v in capflags.values()), capflags
     assert loss_err < 1e-5
     assert grad_err < 1e-4
 

@@ -228,6 +228,31 @@ def test_warp_cost_channels_last_matches_nchw(hip, shape, reduce_mean):
         assert rel(b[k], a[k]) < 1e-5, (name, rel(b[k], a[k]))
 
 
+@pytest.mark.parametrize("reduce_mean", [False, True])
+def test_warp_cost_channels_last_inf_outside_taps(hip, reduce_mean):
+    """an out-of-image tap must not read its (clamped) reference
+    pixel at all -- grid_sample's zeros padding.  Pixel (0, 0) of every
+    reference map is +Inf: the channels-last forward gives the NCHW cost
+    element for element (Inf / NaN exactly where a tap really samples (0, 0),
+    finite everywhere else)."""
+    B, C, h, w, N = 2, 70, 7, 13, 2
+    g = torch.Generator().manual_seed(29)
+    K = kitti_K(B, W=8 * w, H=8 * h)
+    fmap, frefs = torch.randn(B, C, h, w, generator=g), torch.randn(N, B, C, h, w, generator=g)
+    frefs[:, :, :, 0, 0] = float("inf")
+    disp = torch.rand(B, 1, h, w, generator=g)
+    poses = torch.cat([0.3 * torch.randn(N, B, 3, generator=g), 0.05 * torch.randn(N, B, 3, generator=g)], 2)
+    out = {}
+    for layout in ("nchw", "cl"):
+        rg = _ref_leaf(hip, frefs, layout).detach()
+        out[layout] = hip.warp_cost(fmap.to(DEV), rg, disp.to(DEV), poses.to(DEV), K.to(DEV),
+                                    depth_mode=hip.DEPTH_DISP, min_depth=0.5, max_depth=80.0,
+                                    reduce_mean=reduce_mean).cpu()
+    a, b = out["nchw"], out["cl"]
+    assert torch.isfinite(a).float().mean() > 0.5            # most pixels never touch (0, 0)
+    torch.testing.assert_close(b, a, rtol=0, atol=0, equal_nan=True)
+
+
 def test_warp_cost_forward_deterministic(hip):
     d = fx("cost_each_small")
     a = hip.warp_cost(d["fmap"], d["fmap_ref"], d["depth"], d["pose"], d["K"], reduce_mean=False)
@@ -315,12 +340,14 @@ def test_view_synthesis_kitti_size_vs_oracle(hip):
 
 
 # ------------------------------------------------------------------ photometric loss
-def _oracle_photometric(d, dt, forced_selection=None, cells=None):
+def _oracle_photometric(d, dt, forced_selection=None, cells=None, book=None):
     """Oracle loss and gradients on the fixture inputs in dtype dt; with
     forced_selection the min reduction takes the given candidates, with cells
-    (cells_from_record) the warps take the given bilinear cells."""
+    (cells_from_record) the warps take the given bilinear cells.  book: a dict
+    that receives the oracle's Cells book (its own clip thresholds)."""
     invs = [i.cpu().to(dt).requires_grad_(True) for i in d["inv_depths"]]
     vecs = d["poses"].cpu().to(dt).requires_grad_(True)
+    bk = O.Cells(forced=cells) if cells is not None else O.Cells()
     N, n = vecs.shape[1], vecs.shape[2]
     poses = [[vecs[:, j, i] for i in range(n)] for j in range(N)]
     out = O.photometric_decay_loss(d["image"].cpu().to(dt), [c.cpu().to(dt) for c in d["context"]], invs,
@@ -328,8 +355,9 @@ def _oracle_photometric(d, dt, forced_selection=None, cells=None):
                                    automask=bool(int(d["automask"])),
                                    reduce="min" if int(d["reduce_min"]) else "mean",
                                    forced_selection=forced_selection,
-                                   cells=O.Cells(forced=cells) if cells is not None else None,
-                                   clip_loss=_clip(d))
+                                   cells=bk, clip_loss=_clip(d))
+    if book is not None:
+        book["cells"] = bk
     out["loss"].sum().backward()
     return torch.stack([i.grad for i in invs]).double(), vecs.grad.double(), out["loss"].detach().double()
 
@@ -381,8 +409,18 @@ def test_photometric_loss_golden(hip, name):
         _, _, l64_free = _oracle_photometric(d, torch.float64)
         _, _, l64_forced = _oracle_photometric(d, torch.float64, forced)
         assert float(l64_forced - l64_free) <= 1e-9 * float(l64_free), "selection differs beyond near-ties"
-    gi64, gp64, _ = _oracle_photometric(d, torch.float64, forced, cells)
+    book = {}
+    gi64, gp64, _ = _oracle_photometric(d, torch.float64, forced, cells, book)
     gi32, _, _ = _oracle_photometric(d, torch.float32, forced, cells)
+    if _clip(d) > 0:
+        # the clip thresholds (mean + clip * std of each map) are continuous
+        # quantities: the product's own, not pinned, within 1e-5 of fp64's
+        thr_hip = next(t for tag, t in rec.calls if tag == "photo_clip").cpu().double()
+        thr64 = book["cells"].thresholds
+        Nn = d["poses"].shape[1] * d["poses"].shape[2]        # every warped map (+ N unwarped with automask)
+        assert set(range(Nn)) <= set(thr64) <= set(range(thr_hip.numel())), (sorted(thr64), thr_hip.numel())
+        for k, t64 in thr64.items():
+            assert abs(float(thr_hip[k]) - t64) <= 1e-5 * abs(t64), ("clip threshold", k, float(thr_hip[k]), t64)
     ref_i, ref_p = d["g_inv_depths"].double().cpu(), d["g_poses"].double().cpu()
     got_i, got_p = invs.grad.double().cpu(), vec.grad.double().cpu()
     bound_p = TOL * ref_p.abs().max() + (ref_p - gp64).abs()
@@ -825,7 +863,14 @@ def full_size_case(case):
     configs[1] (KITTI 192x640, it8-seq4-inter-out, B=2, N=2, self-sup);
     "sup_view3" -- configs[2] (ScanNet 240x320, it12-h-out, N=2, supervised,
     B=1); "selfsup_view5" -- configs[4]'s model (240x320, it12-h-out, N=4,
-    self-sup, B=1).  Returns (tag, version, kind, min_depth, max_depth, batch)."""
+    self-sup, B=1).  A "_b<B>" suffix sets the batch: "sup_view3_b8" is
+    configs[2] at its own batch of 8, "selfsup_view5_b4" configs[4] at its
+    per-rank batch of 4 (the batch-dependent BN and split-K plans).
+    Returns (tag, version, kind, min_depth, max_depth, batch)."""
+    B = 1
+    if "_b" in case:
+        case, B = case.rsplit("_b", 1)
+        B = int(B)
     if case == "kitti":
         B, N, H, W = 2, 2, 192, 640
         img = smooth_images(B, H, W, 51, detail=0.3)
@@ -834,7 +879,7 @@ def full_size_case(case):
         batch = {"rgb": img, "rgb_context": refs, "rgb_original": img, "rgb_context_original": refs,
                  "intrinsics": kitti_K(B)}
         return "it8", "it8-seq4-inter-out", "selfsup", 0.5, 80.0, batch
-    B, H, W = 1, 240, 320
+    H, W = 240, 320
     N = 4 if case == "selfsup_view5" else 2
     img = smooth_images(B, H, W, 81, detail=0.3)
     refs = [torch.roll(img, 2 * (j + 1), 3) * (1 - REF_MIX) + REF_MIX * smooth_images(B, H, W, 82 + j, detail=0.3)
@@ -911,11 +956,14 @@ def _full_size_step(case):
     assert not bad, (bad[:5], l2)
 
 
-@pytest.mark.parametrize("case", ["selfsup_view5", "sup_view3"])
+@pytest.mark.parametrize("case", ["selfsup_view5", "sup_view3", "selfsup_view5_b4", "sup_view3_b8"])
 def test_train_step_scannet_size_vs_oracle(hip, case):
     """BASELINE configs[4] (SelfSupModelMF it12-h-out, N=4) and configs[2]
     (SupModelMF it12-h-out, N=2, dense GT) at the ScanNet training shape
-    240x320, B=1 (_full_size_step)."""
+    240x320 (_full_size_step): B=1, and each config's own batch -- configs[2]
+    B=8, configs[4] B=4 per rank -- where BatchNorm sites exceed the one-launch
+    limit (layer1 holds 38 400 elements per channel at B=8) and the split-K
+    plans change with the batch."""
     _full_size_step(case)
 
 
