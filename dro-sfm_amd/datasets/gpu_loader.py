@@ -19,13 +19,35 @@ the context poses untouched), and:
     370x1226, 374x1238, ...): samples of one size are resized in one launch,
     per size group, and the batch is reassembled in sample order.
 
-Decoding stays on the host (PNG/JPEG entropy decoding is serial per image;
-there is no ROCm image decoder in this image).
+With gpu_decode=True (round 6) PNG frames are decoded on the GPU as well
+(datasets/png.py, csrc/png.hip: inflate + row filters, bit-identical to
+Pillow): the workers only open the files (PIL's Image.open is lazy), read their
+bytes and walk the PNG chunks; GPUTrainPipeline decodes every frame of the
+batch in one launch pair per geometry before the transforms.  JPEG frames (no
+GPU decoder here) are decoded by the workers as before.
 """
 import numpy as np
 import torch
 
 from .gpu_transforms import train_transforms
+
+
+def _png_source(img):
+    """The PNG file behind a lazily opened PIL image (load_image), or None."""
+    fn = getattr(img, "filename", None)
+    return fn if getattr(img, "format", None) == "PNG" and fn else None
+
+
+def _frame(img, gpu_decode):
+    """A worker-side frame: PngInfo (the compressed stream; decoded on the GPU)
+    when gpu_decode and the image is a PNG file, else uint8 HWC pixels."""
+    if gpu_decode:
+        fn = _png_source(img)
+        if fn is not None:
+            from .png import parse_png
+            with open(fn, "rb") as f:
+                return parse_png(f.read())
+    return _as_uint8(img)
 
 
 def _as_uint8(img):
@@ -62,7 +84,13 @@ def resize_depth_nearest(depth, shape):
     return depth.index_select(-2, iy).index_select(-1, ix).unsqueeze(1)
 
 
-def collate_decoded(samples):
+def collate_encoded(samples):
+    """collate_decoded with PNG frames left encoded (datasets/png.PngInfo):
+    GPUTrainPipeline decodes them on the GPU."""
+    return collate_decoded(samples, gpu_decode=True)
+
+
+def collate_decoded(samples, gpu_decode=False):
     """Collate reference samples built WITHOUT data_transform: 'rgb' and
     'rgb_context' (PIL images or uint8 HWC arrays) become lists of uint8
     [H0, W0, 3] tensors (pinned when a GPU is present; per sample, raw sizes
@@ -72,12 +100,15 @@ def collate_decoded(samples):
     other keys as lists."""
     pin = torch.cuda.is_available()
     out = {}
-    rgb = [_as_uint8(s["rgb"]) for s in samples]
-    out["rgb"] = [t.pin_memory() if pin else t for t in rgb]
+
+    def host(img):
+        t = _frame(img, gpu_decode)
+        return t.pin_memory() if pin and torch.is_tensor(t) else t
+
+    out["rgb"] = [host(s["rgb"]) for s in samples]
     if "rgb_context" in samples[0]:
         n = len(samples[0]["rgb_context"])
-        out["rgb_context"] = [[(lambda t: t.pin_memory() if pin else t)(_as_uint8(s["rgb_context"][j]))
-                               for s in samples] for j in range(n)]
+        out["rgb_context"] = [[host(s["rgb_context"][j]) for s in samples] for j in range(n)]
     if "intrinsics" in samples[0]:
         out["intrinsics"] = torch.stack([torch.as_tensor(np.asarray(s["intrinsics"]), dtype=torch.float32)
                                          for s in samples])
@@ -113,8 +144,7 @@ class GPUTrainPipeline:
         dev = self.device
         B = len(host["rgb"])
         N = len(host.get("rgb_context", []))
-        frames = [[t.to(dev, non_blocking=True) for t in host["rgb"]]]
-        frames += [[t.to(dev, non_blocking=True) for t in host["rgb_context"][j]] for j in range(N)]
+        frames = self._frames([host["rgb"]] + [host["rgb_context"][j] for j in range(N)])
         K = host["intrinsics"].to(dev, non_blocking=True) if "intrinsics" in host else None
         sizes = [tuple(f.shape[:2]) for f in frames[0]]
         # jitter draws must follow sample order: group only consecutive equal sizes
@@ -146,6 +176,29 @@ class GPUTrainPipeline:
             out["depth_context"] = [self._depths(d) for d in host["depth_context"]]
         return out
 
+    def _frames(self, lists):
+        """Host frames (uint8 tensors, or PngInfo streams from collate_encoded)
+        -> uint8 [H0, W0, 3] device tensors; every encoded frame of the batch is
+        decoded on the GPU in one launch pair per geometry."""
+        dev = self.device
+        flat = [f for lst in lists for f in lst]
+        enc = [i for i, f in enumerate(flat) if not torch.is_tensor(f)]
+        dec = {}
+        if enc:
+            from .png import decode_pngs
+            for i, t in zip(enc, decode_pngs([flat[i] for i in enc], dev)):
+                if t.dim() != 3:
+                    raise RuntimeError("GPUTrainPipeline: a 16-bit PNG among the RGB frames")
+                dec[i] = t
+        out, k = [], 0
+        for lst in lists:
+            row = []
+            for f in lst:
+                row.append(dec[k] if k in dec else f.to(dev, non_blocking=True))
+                k += 1
+            out.append(row)
+        return out
+
     def _depths(self, maps):
         """Per-sample raw depth maps -> [B, 1, H, W] on the device (nearest
         neighbour, resize_sample's depth branch, augmentations.py:135-143),
@@ -161,12 +214,13 @@ class GPUTrainPipeline:
 
 
 def gpu_data_loader(dataset, batch_size, image_shape, jittering=(0.2, 0.2, 0.2, 0.05), num_workers=4,
-                    shuffle=True, generator=None, device=None, **loader_kw):
+                    shuffle=True, generator=None, device=None, gpu_decode=False, **loader_kw):
     """Iterate a reference dataset built with data_transform=None through the
     GPU pipeline: a DataLoader over collate_decoded (workers decode and stack
-    uint8 frames) whose batches GPUTrainPipeline transforms on the GPU."""
+    uint8 frames; with gpu_decode, collate_encoded: PNG frames stay encoded and
+    are decoded on the GPU) whose batches GPUTrainPipeline transforms on the GPU."""
     loader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
-                                         collate_fn=collate_decoded, **loader_kw)
+                                         collate_fn=collate_encoded if gpu_decode else collate_decoded, **loader_kw)
     pipe = GPUTrainPipeline(image_shape, jittering, device=device, generator=generator)
     for host in loader:
         yield pipe(host)

@@ -81,6 +81,8 @@ def load():
     _sig(lib.dro_color_jitter_rgb8, P, I, I, I, P, P, S)
     _sig(lib.dro_resize_rgb8, P, I, I, I, I, I, P, P, I, P, P, I, P, P, S)
     _sig(lib.dro_rgb8_to_tensor, P, I, I, I, P, S)
+    _sig(lib.dro_png_filtered_bytes, I, I, I, restype=Z)
+    _sig(lib.dro_png_decode, P, P, I, I, I, I, P, P, P, S)
     _sig(lib.dro_batchnorm_workspace_bytes, I, I, I, restype=Z)
     _sig(lib.dro_batchnorm_relu_forward, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P, P, P, Z, S)
     _sig(lib.dro_batchnorm_relu_backward, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, Z, S)
@@ -124,6 +126,7 @@ EXPORTED = (
     "dro_conv2d_strided_workspace_bytes", "dro_conv2d_strided_forward", "dro_conv2d_strided_backward",
     "dro_pose_mean_forward", "dro_pose_mean_backward",
     "dro_resize_rgb8_to_tensor", "dro_color_jitter_rgb8", "dro_resize_rgb8", "dro_rgb8_to_tensor",
+    "dro_png_filtered_bytes", "dro_png_decode",
     "dro_batchnorm_workspace_bytes", "dro_batchnorm_relu_forward", "dro_batchnorm_relu_backward",
     "dro_weight_split_bytes", "dro_weight_split",
     "dro_conv2d_workspace_bytes", "dro_conv2d_plan", "dro_debug_conv_stamps", "dro_conv_log", "dro_conv_log_read", "dro_conv2d_forward", "dro_convgru_gates_forward",

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 8: dro_convgru_candidate_backward / dro_convgru_gates_backward (the GRU's elementwise stages in the conv data-gradient epilogues); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 9: dro_png_decode (GPU PNG inflate + unfilter); 8: dro_convgru_candidate_backward / dro_convgru_gates_backward (the GRU's elementwise stages in the conv data-gradient epilogues); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -323,6 +323,21 @@ int dro_resize_rgb8(const unsigned char* src, int N, int H0, int W0, int H, int 
                     const int* xbounds, const int* xcoef, int KX, const int* ybounds,
                     const int* ycoef, int KY, unsigned char* tmp, unsigned char* dst, void* stream);
 int dro_rgb8_to_tensor(const unsigned char* src, int N, int H, int W, float* dst, void* stream);
+
+/* PNG decode of N images of one geometry (the reference's load_image =
+ * PIL.Image.open of KITTI frames, utils/image.py:13-27 via
+ * datasets/kitti_dataset.py:354, :387, and read_png_depth,
+ * kitti_dataset.py:38-44), bit-identical to Pillow.  zdata: the concatenated
+ * IDAT payloads (zlib streams), image i at byte zoff[i] (4-byte aligned) to
+ * zoff[i+1] (N+1 int64 offsets).  kind: 0 grey8, 2 RGB8, 6 RGBA8 -> out uint8
+ * [N, H, W, 3] (PIL convert("RGB")); 16 grey16 -> out float32 [N, H, W] =
+ * value / 256, -1 where 0.  filtered: workspace of N x
+ * dro_png_filtered_bytes(H, W, bytes per pixel) bytes.  status[i] (int32,
+ * device): 0 decoded, > 0 a malformed stream (the output is then undefined).
+ * Non-interlaced images only; rows of at most 16384 bytes. */
+size_t dro_png_filtered_bytes(int H, int W, int bpp);
+int dro_png_decode(const unsigned char* zdata, const long long* zoff, int N, int H, int W, int kind,
+                   unsigned char* filtered, void* out, int* status, void* stream);
 int dro_color_jitter_rgb8(unsigned char* frames, int N, int H, int W, const int* params,
                           unsigned long long* workspace, void* stream);
 

@@ -117,3 +117,53 @@ def test_gpu_pipeline_depth_two_raw_sizes():
         for j in range(2):
             want = O.resize_depth_cv2_nearest(s[n]["depth_context"][j], (H, W))[..., 0]
             assert np.array_equal(out["depth_context"][j][n, 0].cpu().numpy(), want), (n, j)
+
+
+def _png_samples(tmp_path, sizes, seed=21, n_ctx=2):
+    """Samples whose frames are lazily opened PNG files (load_image =
+    Image.open, utils/image.py:13-27), textured so the encoder uses every
+    filter and real Huffman blocks."""
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    out = []
+    for i, (h0, w0) in enumerate(sizes):
+        def img(tag):
+            y, x = np.mgrid[0:h0, 0:w0]
+            a = np.stack([(x * (2 + c) + y * 3 + rng.integers(0, 9)) % 256 for c in range(3)], -1)
+            a = (a + rng.integers(0, 24, a.shape)).clip(0, 255).astype(np.uint8)
+            fn = str(tmp_path / f"s{i}_{tag}.png")
+            Image.fromarray(a).save(fn)
+            return Image.open(fn)
+        K = np.array([[721.5, 0.0, w0 / 2], [0.0, 721.5, h0 / 2], [0.0, 0.0, 1.0]], np.float32)
+        out.append({"idx": i, "rgb": img("t"), "rgb_context": [img(f"c{j}") for j in range(n_ctx)],
+                    "intrinsics": K, "pose_context": [np.eye(4, dtype=np.float32)] * n_ctx})
+    return out
+
+
+def test_collate_encoded_keeps_png_streams(tmp_path):
+    """With GPU decoding the workers do not decode PNG frames: they pass the
+    parsed streams (PngInfo); in-memory (non-file) frames are decoded as before."""
+    from dro_sfm_amd.datasets.gpu_loader import collate_encoded
+    from dro_sfm_amd.datasets.png import PngInfo
+    s = _png_samples(tmp_path, [(12, 20), (10, 18)])
+    s[1]["rgb"] = s[1]["rgb"].copy()                      # an in-memory image: no file behind it
+    b = collate_encoded(s)
+    assert isinstance(b["rgb"][0], PngInfo) and b["rgb"][0].key == (12, 20, 2)
+    assert torch.is_tensor(b["rgb"][1]) and b["rgb"][1].shape == (10, 18, 3)
+    assert isinstance(b["rgb_context"][1][1], PngInfo) and b["rgb_context"][1][1].key == (10, 18, 2)
+
+
+@pytest.mark.gpu
+def test_gpu_pipeline_with_gpu_decode_equals_host_decode(tmp_path):
+    """The whole GPU pipeline fed encoded PNG frames (decoded on the GPU, two
+    raw sizes in one batch) == the same pipeline fed Pillow-decoded frames:
+    every output tensor bit-identical."""
+    from dro_sfm_amd.datasets.gpu_loader import GPUTrainPipeline, collate_decoded, collate_encoded
+    s = _png_samples(tmp_path, [(375, 1242), (370, 1226), (370, 1226)])
+    a = GPUTrainPipeline((192, 640), JIT, generator=torch.Generator().manual_seed(7))(collate_encoded(s))
+    b = GPUTrainPipeline((192, 640), JIT, generator=torch.Generator().manual_seed(7))(collate_decoded(s))
+    for key in ("rgb", "rgb_original", "intrinsics"):
+        assert torch.equal(a[key], b[key]), key
+    for key in ("rgb_context", "rgb_context_original"):
+        for x, y in zip(a[key], b[key]):
+            assert torch.equal(x, y), key
