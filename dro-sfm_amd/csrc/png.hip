@@ -146,7 +146,6 @@ __device__ __forceinline__ void uniform(Inflater& s) {
 }
 
 __device__ __forceinline__ void refill(Inflater& s) {
-  uniform(s);
   if (s.bc > 32) return;
   stage(s);
   const long long r = s.ip - s.lo;      // byte offset in the window, < 4096 - 8
@@ -407,9 +406,27 @@ __global__ __launch_bounds__(kPngThreads) void png_inflate_kernel(const unsigned
     }
     // the block's symbols
     for (;;) {
+      uniform(s);
       pos = rfl64(pos);
       flushed = rfl64(flushed);
       if (pos - flushed >= kWin / 2) flush();          // unflushed bytes stay < 32 KB
+      // Literal runs first: a tight loop over direct-table literal hits (the
+      // measured cost of the general path was ~75 instructions per literal,
+      // SQ counters of a literal-only stream, tools/png_pmc_probe.py)
+      {
+        const long long lim = flushed + kWin / 2 < flen ? flushed + kWin / 2 : flen;
+        while (pos < lim) {
+          if (s.bc < 16) refill(s);
+          const unsigned e = __builtin_amdgcn_readfirstlane(hl.fast[s.bb & ((1u << kFastBits) - 1)]);
+          const int l = (int)(e & 15);
+          if (e == 0 || (e >> 4) > 255 || l > s.bc) break;
+          s.bb >>= l;
+          s.bc -= l;
+          if (lane == 0) win[pos & (kWin - 1)] = (unsigned char)(e >> 4);
+          ++pos;
+        }
+        if (pos - flushed >= kWin / 2) continue;       // flush before the next symbol
+      }
       const int sym = decode(s, hl);
       if (sym < 0) {
         fail(s.err);
