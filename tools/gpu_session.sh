@@ -27,6 +27,7 @@ for step in "$@"; do
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
     testsall) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
+    testsm) rm -f "$OUT/parity_margins.jsonl"; run pytest_gpu 1100 env DRO_PARITY_LOG="$OUT/parity_margins.jsonl" python -u -m pytest tests -m gpu -v --durations=15 --timeout=300 --timeout-method=thread -p no:cacheprovider ;;
     bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchab) run bench_a 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline ;;
