@@ -261,11 +261,126 @@ struct HaloShape {
   static_assert(NJ <= 4 && WPER <= 16 && CK % 4 == 0 && TH * TW == 64, "halo shape");
 };
 
+// ---- BatchNorm statistics in the conv epilogue (EPI 5 / 6, BnFuse)
+// One arrival at a self-resetting counter: true in the block that arrives
+// last (the counter is back at 0 for the next launch / graph replay).
+// The partial sums go through agent-coherent accesses (bn_put / bn_get:
+// written through to, and read from, the coherence point past the XCDs'
+// L2s), so before the arrival every wave only waits for its own stores to be
+// acknowledged (s_waitcnt 0) -- no agent-scope release fence, which writes
+// back the whole L2 of the block's XCD in every block.
+__device__ __forceinline__ bool last_arrival(unsigned* c, unsigned n, unsigned* flag) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = old == n - 1u;
+    if (old == n - 1u) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return *flag != 0u;
+}
+
+__device__ __forceinline__ void bn_put(double2* p, double a, double b) {
+  double* q = reinterpret_cast<double*>(p);
+  __hip_atomic_store(q, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double2 bn_get(const double2* p) {
+  double* q = const_cast<double*>(reinterpret_cast<const double*>(p));
+  return make_double2(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// After a block wrote its tile's partials (part[pt][row]): the last block of
+// each level-1 group of g1 pixel tiles folds the group (fixed order) into
+// part2, and the last group of the row tile finalises its channels --
+// batchnorm.hip's formulas (EPI 5: mean, biased variance, invstd, running
+// statistics with the unbiased variance; EPI 6: mean(g), mean(g xhat),
+// dgamma, dbeta).
+// Sum of items p < n (item p of row r at base[p * rows + r]) by the T
+// consecutive threads of row r: thread j loads items j, j + T, ... eight at a
+// time (the agent-coherent loads in flight together), then the T lanes
+// combine by a fixed butterfly -- a fixed order, every lane gets the sum.
+__device__ __forceinline__ double2 bn_fold(const double2* base, int n, int rows, int r, int j, int T) {
+  double s1 = 0.0, s2 = 0.0;
+  for (int p0 = j; p0 < n; p0 += 8 * T) {
+    double2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + u * T;
+      v[u] = p < n ? bn_get(base + (size_t)p * rows + r) : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s1 += v[u].x;
+      s2 += v[u].y;
+    }
+  }
+  for (int o = 1; o < T; o <<= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  return make_double2(s1, s2);
+}
+
+template <int EPI>
+__device__ void bn_finish(const IgArgs& a, int pt, int rt, int row0, int bm) {
+  __shared__ unsigned flag;
+  const BnFuse& f = a.bn;
+  if (f.dbg & 1) return;
+  const int rows = a.rows, ptiles = a.g.B * a.tiles_img;
+  const int grp = pt / f.g1, lo = grp * f.g1, n1 = min(f.g1, ptiles - lo);
+  if (!last_arrival(f.cnt + (size_t)rt * f.ngroups + grp, (unsigned)n1, &flag)) return;
+  // T threads per row (blockDim / bm: 4 .. 32, inside one wave)
+  const int T = (int)blockDim.x / bm, rl = (int)threadIdx.x / T, j = (int)threadIdx.x - rl * T;
+  const int r = row0 + rl;
+  const bool live = r < rows;
+  {
+    const double2 v = bn_fold(f.part + (size_t)lo * rows, live ? n1 : 0, rows, live ? r : 0, j, T);
+    if (live && j == 0) bn_put(f.part2 + (size_t)grp * rows + r, v.x, v.y);
+  }
+  if (!last_arrival(f.cnt + (size_t)a.row_tiles * f.ngroups + rt, (unsigned)f.ngroups, &flag)) return;
+  const double2 v = bn_fold(f.part2, live ? f.ngroups : 0, rows, live ? r : 0, j, T);
+  if (!live || j != 0) return;
+  const double s1 = v.x, s2 = v.y;
+  const long long L = (long long)a.g.B * a.g.H * a.g.W;
+  if (EPI == 5) {
+    const double mean = s1 / (double)L;
+    double var = s2 / (double)L - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+    const float mu = (float)mean;
+    f.coef[r] = (f.gamma ? f.gamma[r] : 1.f) * invstd;
+    f.coef[rows + r] = mu;
+    f.coef[2 * rows + r] = f.beta ? f.beta[r] : 0.f;
+    f.save_mean[r] = mu;
+    f.save_invstd[r] = invstd;
+    if (f.rmean) {
+      const double unb = L > 1 ? var * (double)L / (double)(L - 1) : var;
+      f.rmean[r] = (1.f - f.momentum) * f.rmean[r] + f.momentum * mu;
+      f.rvar[r] = (1.f - f.momentum) * f.rvar[r] + f.momentum * (float)unb;
+    }
+    if (r == 0 && f.nbt) *f.nbt += 1;
+  } else {   // the data-gradient staging coefficients of the producer (XF 3)
+    const float invstd = f.invstd[r];
+    f.coef[r] = (f.gamma ? f.gamma[r] : 1.f) * invstd;
+    f.coef[rows + r] = (float)(s1 / (double)L);
+    f.coef[2 * rows + r] = (float)(s2 / (double)L);
+    f.coef[3 * rows + r] = f.mean[r];
+    f.coef[4 * rows + r] = invstd;
+    if (f.dgamma) f.dgamma[r] = (float)s2;
+    if (f.dbeta) f.dbeta[r] = (float)s1;
+  }
+}
+
 // KS > 1: intra-block K split.  The block is KS groups of 4 waves; group g
 // stages and multiplies chunks g, g+KS, ... in its own LDS region, and the
 // groups' accumulators are summed in group order at the end (more waves per
 // tile to hide the staging latency, no split-K partials or finish launch).
-template <int BM, int KH, int KW, int MODE, int ACT, int EPI, int KS>
+template <int BM, int KH, int KW, int MODE, int ACT, int EPI, int KS, int XF = 0>
 __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   using S = HaloShape<BM, KH, KW>;
   {   // diagnostics: kernel entry of wave 0 (slot 10) and of the block's last wave (slot 11)
@@ -310,7 +425,8 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   // lanes run over the halo in NJ passes whose byte offsets are chunk
   // independent (lanes outside the image read pixel 0 and are zeroed when staged)
   unsigned xpb[NJ];
-  bool xok[NJ];
+  bool xok[NJ], own[NJ];
+  static_assert(XF == 0 || ((MODE == 0) == (XF != 3) && ACT == 0), "BN staging transforms: XF 1/2 forward, 3 data gradient");
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int e = lane + 64 * j;
@@ -318,6 +434,10 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
     const int yy = ty0 - PH + hy, xx = tx0 - PW + hx;
     xok[j] = e < HALO && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
     xpb[j] = xok[j] ? 4u * (unsigned)(yy * W + xx) : 0u;
+    // XF: the transformed source is stored at the pixels of the block's own
+    // tile, for the chunks whose index is its row tile modulo the row tiles
+    // (prep: Stage::ownc) -- every element exactly once, spread over the blocks
+    own[j] = XF != 0 && xok[j] && hy >= PH && hy < PH + TH && hx >= PW && hx < PW + TW;
   }
   const unsigned wlast = (unsigned)Cout * CinT - 1;
 
@@ -343,10 +463,16 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   const unsigned long long dQ1 = sQ[1] - sQ[0], dQ2 = sQ[2] - sQ[1], dQ3 = sQ[3] - sQ[2];
   const unsigned dR1 = sR[1] - sR[0], dR2 = sR[2] - sR[1], dR3 = sR[3] - sR[2];
   const unsigned dM1 = sM[1] - sM[0], dM2 = sM[2] - sM[1], dM3 = sM[3] - sM[2];
-  const long long yshift = reinterpret_cast<long long>(a.gy) - reinterpret_cast<long long>(Gp);
+  // second staged stream at the same offsets: the folded activation's y
+  // (FOLD), the skip (XF 2) or the BN input z (XF 3); XF owner stores go to yout
+  const long long sbase = MODE == 0 ? reinterpret_cast<long long>(a.src[0].p) : reinterpret_cast<long long>(Gp);
+  const long long yshift = reinterpret_cast<long long>(XF == 2 ? a.bn.skip : XF == 3 ? a.bn.z : a.gy) - sbase;
+  const long long oshift = reinterpret_cast<long long>(a.bn.yout) - sbase;
 
   // MODE 1 with ACT != 0: the activation derivative is folded into G staging
   constexpr bool FOLD = MODE == 1 && ACT != 0;
+  constexpr bool Y2 = FOLD || XF == 2 || XF == 3;
+  constexpr int NXC = XF == 3 ? 5 : 3;   // BN coefficients per staged channel
   const float galpha = a.galpha;
   // weights are staged as float4 runs (a run never crosses a weight row: RUN %
   // 4 == 0); starts need only dword alignment; per-thread offsets are chunk
@@ -365,9 +491,13 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   }
   // one chunk's staging registers; with PF == 2 two sets alternate so the
   // loads of chunk c+2 are in flight while chunk c is multiplied
+  typedef __attribute__((address_space(1))) char* GWPtr;
   struct Stage {
-    float xr[XPER * NJ], yr[FOLD ? XPER * NJ : 1], wv[WREG];
+    float xr[XPER * NJ], yr[Y2 ? XPER * NJ : 1], wv[WREG];
     unsigned cmask;   // scalar: bit i = channel i of this wave exists
+    unsigned ownc;    // XF, scalar: this block stores this chunk's transformed values
+    float xc[XF ? NXC * XPER : 1];   // XF: the staged channels' BN coefficients (scalar)
+    GWPtr yo[XF ? XPER : 1];         // XF: owner-store rows
   };
   // a chunk's loads: scalar set-up (weight base, one row address per channel),
   // then NVM independent load items that the MFMA loop can interleave
@@ -399,8 +529,14 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       const unsigned long long rq = Q + (unsigned long long)(unsigned)cc * R;
       r.rowp[i] = reinterpret_cast<GPtr>(rq);
       r.yrow[i] = reinterpret_cast<GPtr>(rq + (unsigned long long)yshift);
+      if (XF) {
+        st.yo[i] = reinterpret_cast<GWPtr>(rq + (unsigned long long)oshift);
+#pragma unroll
+        for (int k = 0; k < NXC; ++k) st.xc[k * XPER + i] = a.bn.xcoef[k * kch + cc];
+      }
     }
     st.cmask = cm;
+    if (XF) st.ownc = (unsigned)(chunk % a.row_tiles) == (unsigned)rt ? ~0u : 0u;
   };
   auto item = [&](Stage& st, const Rows& r, int k) {
     if (k < WPER4) {
@@ -414,7 +550,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       const int q = k - WPER4, i = q / NJ, j = q - i * NJ;
       const unsigned o = xpb[j] & r.M[i];
       st.xr[q] = *reinterpret_cast<GFPtr>(r.rowp[i] + o);
-      if (FOLD) st.yr[q] = *reinterpret_cast<GFPtr>(r.yrow[i] + o);
+      if (Y2) st.yr[q] = *reinterpret_cast<GFPtr>(r.yrow[i] + o);
     }
   };
   auto load = [&](Stage& st, int chunk) {
@@ -425,12 +561,22 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   };
   auto store = [&](const Stage& st, int buf) {
     const float(&xr)[XPER * NJ] = st.xr;
-    const float(&yr)[FOLD ? XPER * NJ : 1] = st.yr;
+    const float(&yr)[Y2 ? XPER * NJ : 1] = st.yr;
     const float(&wv)[WREG] = st.wv;
     float* Ws = smem + buf * STAGE;
     float* Xs = Ws + WSZ + wave * XPER * HPAD + lane;
     auto xval = [&](int i, int j) {
-      float v = (((st.cmask >> i) & 1u) && xok[j]) ? xr[i * NJ + j] : 0.f;
+      const bool ok = ((st.cmask >> i) & 1u) && xok[j];
+      float v = ok ? xr[i * NJ + j] : 0.f;
+      if (XF == 1 || XF == 2) {   // BN (+ skip) + ReLU of the producer (batchnorm.hip bn_fused_fwd_kernel)
+        const float r = fmaf(v - st.xc[XPER + i], st.xc[i], st.xc[2 * XPER + i]) + (XF == 2 ? yr[i * NJ + j] : 0.f);
+        v = ok ? fmaxf(r, 0.f) : 0.f;
+      } else if (XF == 3) {       // BN backward (bn_fused_bwd_kernel): dz from g and z
+        const float xh = (yr[i * NJ + j] - st.xc[3 * XPER + i]) * st.xc[4 * XPER + i];
+        const float r = st.xc[i] * (v - st.xc[XPER + i] - xh * st.xc[2 * XPER + i]);
+        v = ok ? r : 0.f;
+      }
+      if (XF && own[j] && ((st.cmask & st.ownc) >> i & 1u)) *reinterpret_cast<__attribute__((address_space(1))) float*>(st.yo[i] + xpb[j]) = v;
       if (MODE == 1) v *= galpha;
       if (FOLD) v *= act_bwd(yr[i * NJ + j], ACT);
       return v;
@@ -441,7 +587,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
 #pragma unroll
       for (int j = 0; j < JF; ++j) Xs[i * HPAD + 64 * j] = xval(i, j);
     }
-    if (JF < NJ && lane + 64 * (NJ - 1) < HPAD) {
+    if (JF < NJ && lane + 64 * (NJ - 1) < HPAD) {   // (XF owners: e < HALO <= HPAD, all inside)
 #pragma unroll
       for (int i = 0; i < XPER; ++i) Xs[i * HPAD + 64 * (NJ - 1)] = xval(i, NJ - 1);
     }
@@ -587,6 +733,73 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
   __syncthreads();
   stamp(13);
   const long long P = (long long)a.g.B * HW;
+  if constexpr (EPI >= 5) {
+    // BN statistics of the tile: each thread finishes its elements (output /
+    // g stored) and parks the value the statistics need in LDS at the
+    // element's set-0 slot (only this thread reads that element's sets);
+    // then one thread per row sums the row's 64 pixels in order (fp64) --
+    // EPI 6 in two passes (g, then g * xhat, kept in registers meanwhile)
+    constexpr int NIT = BM * 64 / (256 * KS);
+    float second[EPI == 6 ? NIT : 1];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = (int)threadIdx.x + it * 256 * KS;
+      const int rl = e >> 6, pl = e & 63;
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < KS; ++g) {
+        if (WM == 1)
+          v += smem_all[((size_t)(2 * g) * BM + rl) * 64 + pl] + smem_all[((size_t)(2 * g + 1) * BM + rl) * 64 + pl];
+        else
+          v += smem_all[((size_t)g * BM + rl) * 64 + pl];
+      }
+      const int row = row0 + rl;
+      const int py = pl / TW, px = pl - py * TW;
+      const int oy = ty0 + py, ox = tx0 + px;
+      float first = 0.f;
+      if (EPI == 6) second[it] = 0.f;
+      if (row < rows && oy < H && ox < W) {
+        const size_t epix = (size_t)oy * W + ox;
+        if (EPI == 5) {
+          first = v + (a.bias ? a.bias[row] : 0.f);
+          a.out[((size_t)b * a.out_ctot + a.out_coff + row) * HW + epix] = first;
+        } else {
+          const size_t idx = ((size_t)b * rows + row) * HW + epix;
+          first = a.bn.y[idx] > 0.f ? v : 0.f;
+          const float xh = (a.bn.z[idx] - a.bn.mean[row]) * a.bn.invstd[row];
+          a.gsrc[0][idx] = first;
+          second[it] = first * xh;
+        }
+      }
+      smem_all[e] = first;
+    }
+    __syncthreads();
+    const int rl = threadIdx.x, row = row0 + rl;
+    const bool rowt = rl < BM && row < rows && !(a.bn.dbg & 4);
+    double s1 = 0.0, s2 = 0.0;
+    if (rowt) {
+#pragma unroll 16
+      for (int p = 0; p < 64; ++p) {
+        const double v = smem_all[rl * 64 + p];
+        s1 += v;
+        if (EPI == 5) s2 += v * v;
+      }
+    }
+    if (EPI == 6) {
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) smem_all[(int)threadIdx.x + it * 256 * KS] = second[EPI == 6 ? it : 0];
+      __syncthreads();
+      if (rowt) {
+#pragma unroll 16
+        for (int p = 0; p < 64; ++p) s2 += (double)smem_all[rl * 64 + p];
+      }
+    }
+    if (rowt && !(a.bn.dbg & 2)) bn_put(a.bn.part + (size_t)pt * rows + row, s1, s2);
+    bn_finish<EPI>(a, pt, rt, row0, BM);
+    stamp(14);
+    return;
+  }
   for (int e = threadIdx.x; e < BM * 64; e += 256 * KS) {
     const int rl = e >> 6, pl = e & 63;
     float v = 0.f;
@@ -1910,10 +2123,23 @@ int launch_thin(IgArgs& a, int max_splits, hipStream_t s) {
 unsigned long long* g_conv_stamps = nullptr;   // dro_debug_conv_stamps
 
 // rows / kch set by the caller; `ws` must hold plan.part_bytes
-template <int MODE, int ACT, int EPI>
+template <int MODE, int ACT, int EPI, int XF = 0>
 int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
-  const IgPlan pl = a.flat_only ? plan_igemm_flat(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W)
-                                 : plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
+  IgPlan pl = a.flat_only ? plan_igemm_flat(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W)
+                          : plan_igemm(a.rows, a.kch, a.g.KH, a.g.KW, a.g.B, a.g.H, a.g.W);
+  // BN fused into the conv (BnFuse): 3x3 halo kernel only, and no split-K for
+  // the statistics epilogues (the blocks' own tiles are the partials)
+  constexpr bool BNF = EPI >= 5 || XF != 0;
+  if (BNF) {
+    if (!pl.halo || a.g.KH != 3 || a.g.KW != 3 || a.flat_only) {
+      set_error("conv2d: BatchNorm fusion needs a 3x3 stride-1 halo convolution");
+      return DRO_E_SHAPE;
+    }
+    if (EPI >= 5) {
+      pl.chunks_per_split = (a.kch + pl.CK - 1) / pl.CK;
+      pl.ksplit = 1;
+    }
+  }
   a.stamps = g_conv_stamps;
   a.dbg = 0;
   if (g_conv_stamps) {
@@ -1922,12 +2148,12 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   }
   a.K = a.kch * a.g.KH * a.g.KW;
   static const bool thin_off = getenv("DRO_CONV_NO_THIN") != nullptr;   // A/B switch
-  if (!a.flat_only && !thin_off && thin_ok<MODE, EPI>(a)) {
+  if (!BNF && !a.flat_only && !thin_off && thin_ok<MODE, EPI>(a)) {
     a.part = reinterpret_cast<float*>(ws);
     return launch_thin<MODE, ACT>(a, pl.ksplit, s);
   }
   // split-bf16 MFMA engine (xconv.hip) when the caller passed split weights
-  if constexpr (EPI < 3) {   // (no GRU epilogues in the split-bf16 engine)
+  if constexpr (EPI < 3 && !BNF) {   // (no GRU / BN epilogues in the split-bf16 engine)
     if (!a.flat_only && a.wsplit && xconv_supported(a.g.KH, a.g.KW)) return launch_xconv<MODE, ACT, EPI>(a, ws, s);
   }
   a.row_tiles = pl.row_tiles;
@@ -1968,13 +2194,16 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
 #define DRO_DCONV(BM_, KH_, KW_)                                                                    \
     do {                                                                                            \
       if (pl.kin == 4)                                                                              \
-        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 4>), grid, dim3(1024), 0, s, a); \
+        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 4, XF>), grid, dim3(1024), 0, s, a); \
       else if (pl.kin == 2)                                                                         \
-        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 2>), grid, dim3(512), 0, s, a);  \
+        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 2, XF>), grid, dim3(512), 0, s, a);  \
       else                                                                                          \
-        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 1>), grid, dim3(256), 0, s, a);  \
+        hipLaunchKernelGGL((dconv_kernel<BM_, KH_, KW_, MODE, ACT, EPI, 1, XF>), grid, dim3(256), 0, s, a);  \
     } while (0)
-    if (pl.bm == 32) {
+    if constexpr (BNF) {
+      if (pl.bm == 32) DRO_DCONV(32, 3, 3);
+      else DRO_DCONV(64, 3, 3);
+    } else if (pl.bm == 32) {
       if (KH == 1 && KW == 1) DRO_DCONV(32, 1, 1);
       else if (KH == 1) DRO_DCONV(32, 1, 5);
       else if (KW == 1) DRO_DCONV(32, 5, 1);
@@ -1986,7 +2215,7 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
       else DRO_DCONV(64, 3, 3);
     }
 #undef DRO_DCONV
-  } else {
+  } else if constexpr (!BNF) {
     a.kdiv = make_fdiv(a.kch);
     if (pl.bm == 64)
       hipLaunchKernelGGL((igemm_kernel<64, MODE, ACT, EPI>), grid, dim3(256), 0, s, a);
@@ -1995,12 +2224,16 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
   }
   int st = launch_status("conv kernel launch failed");
   if (st || pl.ksplit == 1) return st;
-  const long long total = (long long)a.rows * P;
-  long long blocks = (total + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL((igemm_finish_kernel<MODE, ACT, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, a,
-                     pl.ksplit);
-  return launch_status("igemm_finish_kernel launch failed");
+  if constexpr (EPI >= 5) {   // (never split; XF with split-K takes the finish below)
+    return st;
+  } else {
+    const long long total = (long long)a.rows * P;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL((igemm_finish_kernel<MODE, ACT, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, a,
+                       pl.ksplit);
+    return launch_status("igemm_finish_kernel launch failed");
+  }
 }
 
 int check_ws(const void* ws, size_t have, size_t need, const char* what) {
@@ -2106,6 +2339,285 @@ extern "C" int dro_conv2d_forward(const dro_slice* srcs, int nsrc, const float* 
   char* ws = static_cast<char*>(workspace);
   DRO_ACT_SWITCH(act, st = (launch_igemm<0, A_, 0>(a, P, ws, s)));
   return st;
+}
+
+// ---- BatchNorm fused into the 3x3 convs (ABI 10): per-site state layout
+// [counters | part: ptiles x C double2 | part2: groups x C double2 | coef: 5 x C]
+namespace {
+struct BnLayout {
+  int ptiles, g1, ngroups;
+  size_t cnt, part, part2, coef, bytes;
+};
+
+BnLayout bn_layout(int B, int H, int W, int C) {
+  BnLayout l;
+  l.ptiles = B * ((H + 7) / 8) * ((W + 7) / 8);   // the 3x3 halo kernel's 8 x 8 pixel tiles
+  l.g1 = 32;
+  l.ngroups = (l.ptiles + l.g1 - 1) / l.g1;
+  const int rtmax = (C + 31) / 32;                  // row tiles (BM >= 32)
+  l.cnt = 0;
+  l.part = align256((size_t)rtmax * (l.ngroups + 1) * sizeof(unsigned));
+  l.part2 = l.part + align256((size_t)l.ptiles * C * sizeof(double2));
+  l.coef = l.part2 + align256((size_t)l.ngroups * C * sizeof(double2));
+  l.bytes = l.coef + align256((size_t)5 * C * sizeof(float));
+  return l;
+}
+
+void bn_bind(BnFuse& f, void* state, const BnLayout& l) {
+  char* b = static_cast<char*>(state);
+  f.cnt = reinterpret_cast<unsigned*>(b + l.cnt);
+  f.part = reinterpret_cast<double2*>(b + l.part);
+  f.part2 = reinterpret_cast<double2*>(b + l.part2);
+  f.coef = reinterpret_cast<float*>(b + l.coef);
+  f.g1 = l.g1;
+  f.ngroups = l.ngroups;
+  static const int dbg = [] {
+    const char* e = getenv("DRO_BN_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  f.dbg = dbg;
+}
+
+const float* bn_coef(const void* state, const BnLayout& l) {
+  return reinterpret_cast<const float*>(static_cast<const char*>(state) + l.coef);
+}
+
+bool bn_dims_ok(int B, int H, int W, int Cin, int Cout) {
+  return B >= 1 && H >= 1 && W >= 1 && Cin >= 1 && Cout >= 1 && Cin < 4096 && Cout < 4096 &&
+         !too_big(B, Cin > Cout ? Cin : Cout, (long long)H * W);
+}
+}  // namespace
+
+extern "C" size_t dro_bn_state_bytes(int B, int H, int W, int C) {
+  if (!bn_dims_ok(B, H, W, C, C)) return 0;
+  return bn_layout(B, H, W, C).bytes;
+}
+
+// y = relu(fmaf(x - mean, k, beta) [+ skip]) from the coefficients a producing
+// conv's statistics epilogue left in a BN state (bn_fused_fwd_kernel's
+// arithmetic): the BN output of a site whose consumer is not a 3x3 halo conv
+namespace {
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_coef_apply_kernel(const float* __restrict__ x, const float* __restrict__ skip,
+                                                            const float* __restrict__ coef, int relu, int C, int HW,
+                                                            float* __restrict__ y) {
+  const int plane = blockIdx.y, c = plane % C;
+  const float k = coef[c], mu = coef[C + c], o = coef[2 * C + c];
+  const long long base = (long long)plane * HW;
+  auto f = [&](float v, float s) {
+    const float r = fmaf(v - mu, k, o) + s;
+    return relu ? fmaxf(r, 0.f) : r;
+  };
+  const int hw4 = VEC ? (HW & ~3) : 0;
+  for (int i = 4 * (blockIdx.x * 256 + threadIdx.x); i < hw4; i += 4 * 256 * gridDim.x) {
+    const float4 v = *reinterpret_cast<const float4*>(x + base + i);
+    const float4 s = skip ? *reinterpret_cast<const float4*>(skip + base + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(y + base + i) = make_float4(f(v.x, s.x), f(v.y, s.y), f(v.z, s.z), f(v.w, s.w));
+  }
+  for (int i = hw4 + blockIdx.x * 256 + threadIdx.x; i < HW; i += 256 * gridDim.x)
+    y[base + i] = f(x[base + i], skip ? skip[base + i] : 0.f);
+}
+
+// dz = k (g - mean(g) - xhat mean(g xhat)), xhat = (z - mean) invstd, from
+// the coefficients a consumer's data gradient (EPI 6) left in the backward
+// state: the BN backward's apply where the producer's data gradient does not
+// stage it (XF 3 re-reads z once per row tile: dearer than this pass beyond
+// one row tile)
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_bwd_coef_apply_kernel(const float* __restrict__ g, const float* __restrict__ z,
+                                                                const float* __restrict__ coef, int C, int HW,
+                                                                float* __restrict__ dz) {
+  const int plane = blockIdx.y, c = plane % C;
+  const float k = coef[c], mg = coef[C + c], mgx = coef[2 * C + c], mu = coef[3 * C + c], is = coef[4 * C + c];
+  const long long base = (long long)plane * HW;
+  auto f = [&](float gv, float zv) {
+    const float xh = (zv - mu) * is;
+    return k * (gv - mg - xh * mgx);
+  };
+  const int hw4 = VEC ? (HW & ~3) : 0;
+  for (int i = 4 * (blockIdx.x * 256 + threadIdx.x); i < hw4; i += 4 * 256 * gridDim.x) {
+    const float4 a = *reinterpret_cast<const float4*>(g + base + i);
+    const float4 b = *reinterpret_cast<const float4*>(z + base + i);
+    *reinterpret_cast<float4*>(dz + base + i) = make_float4(f(a.x, b.x), f(a.y, b.y), f(a.z, b.z), f(a.w, b.w));
+  }
+  for (int i = hw4 + blockIdx.x * 256 + threadIdx.x; i < HW; i += 256 * gridDim.x) dz[base + i] = f(g[base + i], z[base + i]);
+}
+}  // namespace
+
+extern "C" int dro_bn_backward_apply(const float* g, const float* z, int B, int C, int H, int W,
+                                     const void* state, float* dz, void* stream) {
+  if (!bn_dims_ok(B, H, W, C, C) || (long long)B * C > 65535) {
+    set_error("bn_backward_apply: sizes out of range");
+    return DRO_E_SHAPE;
+  }
+  if (!g || !z || !dz || !state) {
+    set_error("bn_backward_apply: NULL g/z/dz/state");
+    return DRO_E_NULL;
+  }
+  const int HW = H * W;
+  const float* coef = bn_coef(state, bn_layout(B, H, W, C));
+  long long per = (2048 + (long long)B * C - 1) / ((long long)B * C);
+  const long long need = (HW + 1023) / 1024;
+  if (per > need) per = need;
+  if (per < 1) per = 1;
+  const dim3 grid((unsigned)per, (unsigned)(B * C));
+  auto al = [](const void* p) { return (reinterpret_cast<size_t>(p) & 15) == 0; };
+  hipStream_t s = (hipStream_t)stream;
+  if ((HW & 3) == 0 && al(g) && al(z) && al(dz))
+    hipLaunchKernelGGL(bn_bwd_coef_apply_kernel<true>, grid, dim3(256), 0, s, g, z, coef, C, HW, dz);
+  else
+    hipLaunchKernelGGL(bn_bwd_coef_apply_kernel<false>, grid, dim3(256), 0, s, g, z, coef, C, HW, dz);
+  return launch_status("bn_bwd_coef_apply_kernel launch failed");
+}
+
+extern "C" int dro_bn_apply(const float* x, const float* skip, int relu, int B, int C, int H, int W,
+                            const void* state, float* y, void* stream) {
+  if (!bn_dims_ok(B, H, W, C, C) || (long long)B * C > 65535) {
+    set_error("bn_apply: sizes out of range");
+    return DRO_E_SHAPE;
+  }
+  if (!x || !y || !state) {
+    set_error("bn_apply: NULL x/y/state");
+    return DRO_E_NULL;
+  }
+  if (relu != 0 && relu != 1) {
+    set_error("bn_apply: relu must be 0 or 1");
+    return DRO_E_MODE;
+  }
+  const int HW = H * W;
+  const float* coef = bn_coef(state, bn_layout(B, H, W, C));
+  long long per = (2048 + (long long)B * C - 1) / ((long long)B * C);
+  const long long need = (HW + 1023) / 1024;
+  if (per > need) per = need;
+  if (per < 1) per = 1;
+  const dim3 grid((unsigned)per, (unsigned)(B * C));
+  auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<size_t>(p) & 15) == 0; };
+  hipStream_t s = (hipStream_t)stream;
+  if ((HW & 3) == 0 && al(x) && al(skip) && al(y))
+    hipLaunchKernelGGL(bn_coef_apply_kernel<true>, grid, dim3(256), 0, s, x, skip, coef, relu, C, HW, y);
+  else
+    hipLaunchKernelGGL(bn_coef_apply_kernel<false>, grid, dim3(256), 0, s, x, skip, coef, relu, C, HW, y);
+  return launch_status("bn_coef_apply_kernel launch failed");
+}
+
+extern "C" int dro_conv2d_bn_forward(const float* x, int B, int H, int W, int Cin, const float* weight, int Cout,
+                                     const void* in_state, const float* in_skip, float* in_y,
+                                     const dro_bn_params* bn, void* out_state, float* out, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (!bn_dims_ok(B, H, W, Cin, Cout)) {
+    set_error("conv2d_bn_forward: sizes out of range");
+    return DRO_E_SHAPE;
+  }
+  if (!x || !weight || !out || (!in_state) != (!in_y) || (in_skip && !in_state) || (!bn) != (!out_state) ||
+      (bn && (!bn->save_mean || !bn->save_invstd || (!bn->running_mean) != (!bn->running_var)))) {
+    set_error("conv2d_bn_forward: NULL pointer (x/weight/out; in_y with in_state; out_state and "
+              "save_mean/save_invstd with bn)");
+    return DRO_E_NULL;
+  }
+  const dro_slice sl{x, Cin, Cin, 0, 0};
+  IgArgs a = {};
+  int st = conv_setup_geom(a, &sl, 1, B, H, W, Cout, 3, 3);
+  if (st) return st;
+  if ((st = check_ws(workspace, workspace_bytes, fwd_workspace(B, H, W, Cin, Cout, 3, 3), "conv2d_bn_forward")))
+    return st;
+  a.weight = weight;
+  a.alpha = 1.f;
+  a.out = out;
+  a.out_ctot = Cout;
+  a.out_coff = 0;
+  a.rows = Cout;
+  a.kch = Cin;
+  if (in_state) {
+    a.bn.xcoef = bn_coef(in_state, bn_layout(B, H, W, Cin));
+    a.bn.skip = in_skip;
+    a.bn.yout = in_y;
+  }
+  if (bn) {
+    bn_bind(a.bn, out_state, bn_layout(B, H, W, Cout));
+    a.bn.gamma = bn->gamma;
+    a.bn.beta = bn->beta;
+    a.bn.rmean = bn->running_mean;
+    a.bn.rvar = bn->running_var;
+    a.bn.nbt = bn->num_batches_tracked;
+    a.bn.eps = bn->eps;
+    a.bn.momentum = bn->momentum;
+    a.bn.save_mean = bn->save_mean;
+    a.bn.save_invstd = bn->save_invstd;
+  }
+  const long long P = (long long)B * H * W;
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = static_cast<char*>(workspace);
+  const int xf = in_state ? (in_skip ? 2 : 1) : 0;
+  if (bn) {
+    if (xf == 2) return launch_igemm<0, 0, 5, 2>(a, P, ws, s);
+    if (xf == 1) return launch_igemm<0, 0, 5, 1>(a, P, ws, s);
+    return launch_igemm<0, 0, 5, 0>(a, P, ws, s);
+  }
+  if (xf == 2) return launch_igemm<0, 0, 0, 2>(a, P, ws, s);
+  if (xf == 1) return launch_igemm<0, 0, 0, 1>(a, P, ws, s);
+  return launch_igemm<0, 0, 0, 0>(a, P, ws, s);
+}
+
+extern "C" int dro_conv2d_bn_backward_data(const float* weight, int B, int H, int W, int Cin, int Cout,
+                                           const float* dout, const void* gin_state, const float* gin_z,
+                                           float* gin_dz, const dro_bn_grad_params* src_bn, void* src_state,
+                                           float* grad_x, int grad_x_accumulate, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  if (!bn_dims_ok(B, H, W, Cin, Cout)) {
+    set_error("conv2d_bn_backward_data: sizes out of range");
+    return DRO_E_SHAPE;
+  }
+  if (!weight || !dout || !grad_x || (gin_state && (!gin_z || !gin_dz)) || (!src_bn) != (!src_state) ||
+      (src_bn && (!src_bn->y || !src_bn->z || !src_bn->save_mean || !src_bn->save_invstd))) {
+    set_error("conv2d_bn_backward_data: NULL pointer (weight/dout/grad_x; gin_z/gin_dz with gin_state; "
+              "src_state and y/z/save_mean/save_invstd with src_bn)");
+    return DRO_E_NULL;
+  }
+  if (src_bn && grad_x_accumulate) {
+    set_error("conv2d_bn_backward_data: grad_x receives g with src_bn (no accumulation)");
+    return DRO_E_MODE;
+  }
+  if (gin_state && src_bn) {
+    set_error("conv2d_bn_backward_data: gin_state and src_bn in one call are not supported");
+    return DRO_E_MODE;
+  }
+  const dro_slice sl{grad_x, Cin, Cin, 0, 0};   // geometry only (the data gradient stages dout)
+  IgArgs a = {};
+  int st = conv_setup_geom(a, &sl, 1, B, H, W, Cout, 3, 3);
+  if (st) return st;
+  if ((st = check_ws(workspace, workspace_bytes, plan_igemm(Cin, Cout, 3, 3, B, H, W).part_bytes,
+                     "conv2d_bn_backward_data")))
+    return st;
+  a.weight = weight;
+  a.G = dout;
+  a.galpha = 1.f;
+  a.gsrc[0] = grad_x;
+  a.gsrc_ctot[0] = Cin;
+  a.gsrc_coff[0] = 0;
+  a.gsrc_acc[0] = grad_x_accumulate ? 1 : 0;
+  a.rows = Cin;
+  a.kch = Cout;
+  if (gin_state) {
+    a.bn.xcoef = bn_coef(gin_state, bn_layout(B, H, W, Cout));
+    a.bn.z = gin_z;
+    a.bn.yout = gin_dz;
+  }
+  if (src_bn) {
+    bn_bind(a.bn, src_state, bn_layout(B, H, W, Cin));
+    a.bn.y = src_bn->y;
+    a.bn.z = src_bn->z;
+    a.bn.gamma = src_bn->gamma;
+    a.bn.mean = src_bn->save_mean;
+    a.bn.invstd = src_bn->save_invstd;
+    a.bn.dgamma = src_bn->grad_gamma;
+    a.bn.dbeta = src_bn->grad_beta;
+  }
+  const long long P = (long long)B * H * W;
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = static_cast<char*>(workspace);
+  if (src_bn) return launch_igemm<1, 0, 6, 0>(a, P, ws, s);
+  if (gin_state) return launch_igemm<1, 0, 0, 3>(a, P, ws, s);
+  return launch_igemm<1, 0, 0, 0>(a, P, ws, s);
 }
 
 extern "C" int dro_convgru_gates_forward(const dro_slice* srcs, int nsrc, const float* weight,

@@ -52,6 +52,54 @@ struct ConvGeom {
   int B, H, W, Cin, Cout, KH, KW, PH, PW;
 };
 
+// Training-mode BatchNorm fused into the halo conv (3x3, stride 1) of the
+// ResNet-18 encoders: conv -> BN [+ skip] -> ReLU -> conv (batchnorm.hip's
+// arithmetic, fixed-order fp64 statistics).
+//   EPI 5 (forward): the conv's output z is the BN input; the epilogue writes
+//     per-(pixel tile, channel) partial sums of z and z^2, and the last block
+//     to finish folds them (two fixed-order levels, self-resetting counters)
+//     into mean / invstd, the running statistics and xcoef-style coefficients
+//     `coef` = [k = gamma * invstd | mean | beta] per channel.
+//   EPI 6 (data gradient): the conv's data gradient dy is the gradient of the
+//     BN's ReLU output y; the epilogue writes g = dy [y > 0] and the partial
+//     sums of g and g * xhat (xhat from z, mean, invstd), folded as above into
+//     `coef` = [mean(g) | mean(g xhat)] and dgamma / dbeta.
+//   XF 1 / 2 (forward staging): the source read is z, staged as
+//     relu(fmaf(z - mean, k, beta) [+ skip]) from `xcoef`; the block that owns
+//     a pixel (row tile 0, the pixel inside its tile) stores that value to
+//     `yout` -- the BN output is materialised by its consumer, not by a launch.
+//   XF 3 (data-gradient staging): the gradient read is g, staged as
+//     dz = k (g - mean(g) - xhat mean(g xhat)) from `xcoef` = [k | mean(g) |
+//     mean(g xhat) | mean | invstd] and z; owners store dz to `yout` (the
+//     weight gradient's input).
+// Sources / gradients / skip / yout / z / y are dense [B, C, H, W] tensors.
+struct BnFuse {
+  double2* part;          // [ptiles][C]
+  double2* part2;         // [ngroups][C]
+  unsigned* cnt;          // [row_tiles][ngroups] level-1 counters, then [row_tiles] level-2
+  int g1, ngroups;        // pixel tiles per level-1 group, groups
+  const float* gamma;     // nullable (1)
+  const float* beta;      // nullable (0)
+  float* rmean;           // nullable (no running statistics)
+  float* rvar;
+  long long* nbt;         // nullable
+  float eps, momentum;
+  float* save_mean;       // EPI 5 outputs
+  float* save_invstd;
+  float* coef;            // EPI 5: [3][C]; EPI 6: [2][C]
+  const float* y;         // EPI 6: the BN's ReLU output (mask)
+  const float* z;         // EPI 6 / XF 3: the BN input
+  const float* mean;      // EPI 6: saved mean / invstd
+  const float* invstd;
+  float* dgamma;          // EPI 6 outputs (nullable)
+  float* dbeta;
+  const float* xcoef;     // XF: coefficients of the staged source's BN
+  const float* skip;      // XF 2
+  float* yout;            // XF: owner stores of the transformed source
+  int dbg;                // timing ablations (env DRO_BN_ABLATE, results invalid): 1 no arrival /
+                          // fold, 2 no partial stores, 4 no row sums
+};
+
 struct IgArgs {
   ConvGeom g;
   Slice src[kMaxSrc];     // forward inputs (virtual concat); read by index from the kernarg segment
@@ -116,6 +164,7 @@ struct IgArgs {
   unsigned long long* stamps;   // diagnostics (dro_debug_conv_stamps): [block][16] s_memtime
   int dbg;                      // diagnostics with stamps on (env DRO_CONV_DBG): 1 skip the K
                                 // loop's loads, 2 its MFMAs, 4 its LDS stores (results invalid)
+  BnFuse bn;                    // EPI 5 / 6 and the XF staging transforms (halo kernel only)
 };
 
 // The K-loop ablations exist only in a diagnostic build (-DDRO_CONV_ABLATE=1,

@@ -87,4 +87,4 @@ extern "C" int dro_wall_clock_hz(long long* hz) {
 
 extern "C" const char* dro_last_error(void) { return dro::g_last_error; }
 
-extern "C" int dro_abi_version(void) { return 9; }
+extern "C" int dro_abi_version(void) { return 10; }

@@ -103,6 +103,11 @@ def load():
     _sig(lib.dro_gru_backward_elem, I, I, I, I, I, P, P, P, P, P, P, P, P, S)
     _sig(lib.dro_convgru_candidate_backward, P, I, P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, Z, S)
     _sig(lib.dro_convgru_gates_backward, P, I, P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, I, P, Z, S)
+    _sig(lib.dro_bn_state_bytes, I, I, I, I, restype=Z)
+    _sig(lib.dro_bn_apply, P, P, I, I, I, I, I, P, P, S)
+    _sig(lib.dro_bn_backward_apply, P, P, I, I, I, I, P, P, S)
+    _sig(lib.dro_conv2d_bn_forward, P, I, I, I, I, P, I, P, P, P, P, P, P, P, Z, S)
+    _sig(lib.dro_conv2d_bn_backward_data, P, I, I, I, I, I, P, P, P, P, P, P, P, I, P, Z, S)
     _lib = lib
     return lib
 
@@ -133,6 +138,7 @@ EXPORTED = (
     "dro_convgru_blend_forward", "dro_conv2d_backward",
     "dro_conv2d_weight_grad_multi_workspace_bytes", "dro_conv2d_weight_grad_multi",
     "dro_gru_backward_elem", "dro_convgru_candidate_backward", "dro_convgru_gates_backward", "dro_adam_step",
+    "dro_bn_state_bytes", "dro_bn_apply", "dro_bn_backward_apply", "dro_conv2d_bn_forward", "dro_conv2d_bn_backward_data",
 )
 
 

@@ -35,6 +35,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ... import hip
+from ...hip import bnconv
 
 
 _FUSED_BN = [True]
@@ -93,6 +94,12 @@ def set_fused_batchnorm(enabled):
     _FUSED_BN[0] = bool(enabled)
 
 
+def _fused_bn_ok(bn, conv, x):
+    """BN inside the conv launches (hip.bnconv) for this site: the native conv
+    engine and the fused BN are on and the conv is 3x3 stride 1 (round 6)."""
+    return _FUSED_BN[0] and _NATIVE_CONV[0] and bnconv.supported(bn, conv, x)
+
+
 class BatchNorm2d(nn.BatchNorm2d):
     """nn.BatchNorm2d (same state_dict) computed by the native kernels."""
 
@@ -131,6 +138,18 @@ class BasicBlock(nn.Module):
         # conv1, the skip (or the downsample) all read x: their input gradients
         # meet in place in a sink (the skip's BN backward writes it first)
         x = hip.grad_sink(x)
+        if _fused_bn_ok(self.bn2, self.conv2, x):
+            # BN inside the 3x3 stride-1 convs (hip.bnconv): conv2 takes bn2's
+            # statistics in its epilogue; in a stride-1 block conv1 takes bn1's
+            # and conv2 stages relu(bn1(.)) itself
+            if self.downsample is None and bnconv.supported(self.bn1, self.conv1, x):
+                z1 = bnconv.conv_bn_stats(x, self.conv1, self.bn1)
+                z2 = bnconv.bn_relu_conv_stats(z1, self.bn1, self.conv2, self.bn2)
+                return bnconv.bn_apply(z2, self.bn2, skip=x)
+            y = self.bn1.act(conv3x3(self.conv1, x))
+            skip = x if self.downsample is None else \
+                self.downsample[1].act(conv3x3(self.downsample[0], x), relu=False)
+            return bnconv.bn_apply(bnconv.conv_bn_stats(y, self.conv2, self.bn2), self.bn2, skip=skip)
         y = self.bn1.act(conv3x3(self.conv1, x))
         if self.downsample is None:
             skip = x

@@ -50,7 +50,7 @@ extern "C" {
 #define DRO_E_MODE (-3)     /* unknown pose/depth mode or option     */
 
 const char* dro_last_error(void);
-int dro_abi_version(void);   /* 9: dro_png_decode (GPU PNG inflate + unfilter); 8: dro_convgru_candidate_backward / dro_convgru_gates_backward (the GRU's elementwise stages in the conv data-gradient epilogues); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
+int dro_abi_version(void);   /* 10: BatchNorm fused into the 3x3 convs (dro_conv2d_bn_forward / dro_conv2d_bn_backward_data, dro_bn_state_bytes); 9: dro_png_decode (GPU PNG inflate + unfilter); 8: dro_convgru_candidate_backward / dro_convgru_gates_backward (the GRU's elementwise stages in the conv data-gradient epilogues); 7: warp-cost forward/backward take ref_layout (channels-last reference maps); 6: photometric calls take clip_loss (and the backward the l1_signs test hook); 5: warp-cost / photometric backward take the `cells` test hook, view synthesis entry points; 4: convex upsample takes the fused add/mul; 3: conv calls take split-bf16 weights (dro_weight_split); 2: dro_adam_step reads its hyper-parameters from device memory */
 
 /* In-graph step timeline (diagnostics, tools/step_timeline.py): record the
  * device's constant-rate real-time counter into buf[slot] when `stream`
@@ -574,6 +574,84 @@ int dro_convgru_gates_backward(const dro_slice* srcs, int nsrc, const float* wei
                                const float* prev_zr, const float* prev_q, const float* prev_h, float* prev_dq,
                                float* prev_dzr, float* prev_dh, int prev_dh_accumulate, void* workspace,
                                size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * BatchNorm fused into the encoders' 3x3 stride-1 convolutions (ABI 10).
+ * Replaces the separate BN launches of the ResNet-18 BasicBlocks
+ * (dro_sfm/networks/optim/extractor.py:67-107 via torchvision's BasicBlock:
+ * conv1 -> bn1 -> relu -> conv2 -> bn2 (+ skip) -> relu) with work inside the
+ * convolutions, batchnorm.hip's arithmetic (fixed-order fp64 statistics,
+ * torch.nn.functional.batch_norm training semantics):
+ *   - the PRODUCING conv's epilogue takes the batch statistics of its output
+ *     (per pixel tile, folded by the last block to finish: no statistics
+ *     launch), writes save_mean / save_invstd / the running statistics and
+ *     the coefficients its consumer needs into `out_state`;
+ *   - the CONSUMING conv stages relu(bn(x) [+ skip]) from those coefficients
+ *     and stores it once per pixel into `in_y` (the BN output the weight
+ *     gradient and the ReLU mask need): no apply launch;
+ *   - backward, the consumer's data gradient takes g = dy [y > 0] and the BN
+ *     backward's statistics in its epilogue (grad_x receives g), and the
+ *     producer's data gradient stages dz = k (g - mean(g) - xhat mean(g xhat))
+ *     and stores it to `gin_dz` for the producer's weight gradient.
+ * A BN state is per site and direction: dro_bn_state_bytes of the BN's
+ * activation geometry, ZERO-FILLED once before its first use (its counters
+ * reset themselves; one call at a time per state). */
+typedef struct dro_bn_params {   /* forward statistics of a training-mode BatchNorm2d */
+  const float* gamma;            /* nullable (1) */
+  const float* beta;             /* nullable (0) */
+  float* running_mean;           /* nullable together with running_var */
+  float* running_var;
+  long long* num_batches_tracked;/* nullable */
+  float eps, momentum;
+  float* save_mean;              /* [C] out */
+  float* save_invstd;            /* [C] out */
+} dro_bn_params;
+
+typedef struct dro_bn_grad_params {   /* backward statistics of BN + ReLU */
+  const float* y;                /* the ReLU output (mask y > 0), dense [B, C, H, W] */
+  const float* z;                /* the BN input, dense [B, C, H, W] */
+  const float* gamma;            /* nullable (1) */
+  const float* save_mean;
+  const float* save_invstd;
+  float* grad_gamma;             /* [C] out, nullable */
+  float* grad_beta;              /* [C] out, nullable */
+} dro_bn_grad_params;
+
+size_t dro_bn_state_bytes(int B, int H, int W, int C);
+
+/* y = relu(bn(x) [+ skip]) (relu 0/1) from a BN state a producing
+ * dro_conv2d_bn_forward filled: the BN output of a site whose consumer is not
+ * a 3x3 stride-1 conv (one launch instead of statistics + apply). */
+int dro_bn_apply(const float* x, const float* skip, int relu, int B, int C, int H, int W, const void* state,
+                 float* y, void* stream);
+
+/* dz = k (g - mean(g) - xhat mean(g xhat)) from the backward BN state a
+ * consumer's dro_conv2d_bn_backward_data (src_bn) filled, g its grad_x and z
+ * the BN input: the BN backward's apply for a producer whose data gradient
+ * does not stage it (gin_state). */
+int dro_bn_backward_apply(const float* g, const float* z, int B, int C, int H, int W, const void* state,
+                          float* dz, void* stream);
+
+/* out [B, Cout, H, W] = conv3x3(s) (stride 1, pad 1, no bias), s = x or, with
+ * in_state (the producer's out_state), s = relu(bn(x) [+ in_skip]) stored to
+ * in_y; with bn / out_state the BN statistics of out.  Workspace:
+ * dro_conv2d_workspace_bytes(B, H, W, Cin, Cout, 3, 3). */
+int dro_conv2d_bn_forward(const float* x, int B, int H, int W, int Cin, const float* weight, int Cout,
+                          const void* in_state, const float* in_skip, float* in_y,
+                          const dro_bn_params* bn, void* out_state, float* out, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/* Data gradient of out = conv3x3(s) into grad_x [B, Cin, H, W] (added when
+ * grad_x_accumulate) from dout [B, Cout, H, W]; with gin_state (the output
+ * BN's state after its consumer's backward) dout is that BN's g and the
+ * conv's output gradient dz is formed in staging (z = gin_z) and stored to
+ * gin_dz; with src_bn / src_state the source is relu(bn(z)) and grad_x
+ * receives g = dy [y > 0] (dense, not accumulated) plus the BN backward's
+ * statistics (src_state, grad_gamma / grad_beta). */
+int dro_conv2d_bn_backward_data(const float* weight, int B, int H, int W, int Cin, int Cout, const float* dout,
+                                const void* gin_state, const float* gin_z, float* gin_dz,
+                                const dro_bn_grad_params* src_bn, void* src_state, float* grad_x,
+                                int grad_x_accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused Adam over flat fp32 buffers (the data-parallel trainer's parameters,

@@ -34,7 +34,7 @@ def test_header_matches_exports(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dro_abi_version() == 9
+    assert lib.dro_abi_version() == 10
 
 
 def test_null_arguments_rejected(lib):
