@@ -326,27 +326,11 @@ __device__ __forceinline__ double2 bn_fold(const double2* base, int n, int rows,
   return make_double2(s1, s2);
 }
 
+// Channel r's statistics from its sums over the batch: batchnorm.hip's
+// formulas (EPI 5: mean, biased variance, invstd, running statistics with the
+// unbiased variance; EPI 6: mean(g), mean(g xhat), dgamma, dbeta)
 template <int EPI>
-__device__ void bn_finish(const IgArgs& a, int pt, int rt, int row0, int bm) {
-  __shared__ unsigned flag;
-  const BnFuse& f = a.bn;
-  if (f.dbg & 1) return;
-  const int rows = a.rows, ptiles = a.g.B * a.tiles_img;
-  const int grp = pt / f.g1, lo = grp * f.g1, n1 = min(f.g1, ptiles - lo);
-  if (!last_arrival(f.cnt + (size_t)rt * f.ngroups + grp, (unsigned)n1, &flag)) return;
-  // T threads per row (blockDim / bm: 4 .. 32, inside one wave)
-  const int T = (int)blockDim.x / bm, rl = (int)threadIdx.x / T, j = (int)threadIdx.x - rl * T;
-  const int r = row0 + rl;
-  const bool live = r < rows;
-  {
-    const double2 v = bn_fold(f.part + (size_t)lo * rows, live ? n1 : 0, rows, live ? r : 0, j, T);
-    if (live && j == 0) bn_put(f.part2 + (size_t)grp * rows + r, v.x, v.y);
-  }
-  if (!last_arrival(f.cnt + (size_t)a.row_tiles * f.ngroups + rt, (unsigned)f.ngroups, &flag)) return;
-  const double2 v = bn_fold(f.part2, live ? f.ngroups : 0, rows, live ? r : 0, j, T);
-  if (!live || j != 0) return;
-  const double s1 = v.x, s2 = v.y;
-  const long long L = (long long)a.g.B * a.g.H * a.g.W;
+__device__ __forceinline__ void bn_finalize_row(const BnFuse& f, int r, int rows, long long L, double s1, double s2) {
   if (EPI == 5) {
     const double mean = s1 / (double)L;
     double var = s2 / (double)L - mean * mean;
@@ -374,6 +358,64 @@ __device__ void bn_finish(const IgArgs& a, int pt, int rt, int row0, int bm) {
     if (f.dgamma) f.dgamma[r] = (float)s2;
     if (f.dbeta) f.dbeta[r] = (float)s1;
   }
+}
+
+// In-kernel fold (BnFuse::inkernel, env DRO_BN_FOLD=kernel): after a block
+// wrote its tile's partials (part[pt][row]), the last block of each level-1
+// group of g1 pixel tiles folds the group (fixed order) into part2, and the
+// last group of the row tile finalises its channels.  Measured slower in the
+// training step than bn_finalize_kernel (the per-block store drain before
+// each arrival and the serial tail under the other stream's load).
+template <int EPI>
+__device__ void bn_finish(const IgArgs& a, int pt, int rt, int row0, int bm) {
+  __shared__ unsigned flag;
+  const BnFuse& f = a.bn;
+  if (f.dbg & 1) return;
+  const int rows = a.rows, ptiles = a.g.B * a.tiles_img;
+  const int grp = pt / f.g1, lo = grp * f.g1, n1 = min(f.g1, ptiles - lo);
+  if (!last_arrival(f.cnt + (size_t)rt * f.ngroups + grp, (unsigned)n1, &flag)) return;
+  // T threads per row (blockDim / bm: 4 .. 32, inside one wave)
+  const int T = (int)blockDim.x / bm, rl = (int)threadIdx.x / T, j = (int)threadIdx.x - rl * T;
+  const int r = row0 + rl;
+  const bool live = r < rows;
+  {
+    const double2 v = bn_fold(f.part + (size_t)lo * rows, live ? n1 : 0, rows, live ? r : 0, j, T);
+    if (live && j == 0) bn_put(f.part2 + (size_t)grp * rows + r, v.x, v.y);
+  }
+  if (!last_arrival(f.cnt + (size_t)a.row_tiles * f.ngroups + rt, (unsigned)f.ngroups, &flag)) return;
+  const double2 v = bn_fold(f.part2, live ? f.ngroups : 0, rows, live ? r : 0, j, T);
+  if (!live || j != 0) return;
+  bn_finalize_row<EPI>(f, r, rows, (long long)a.g.B * a.g.H * a.g.W, v.x, v.y);
+}
+
+// The default: one small launch after the conv (kernel boundary: the
+// partials are visible, no atomics or store drains in the conv's blocks).
+// Block r folds channel r's ptiles partials: thread t sums tiles t, t + 256,
+// ... in order, then a fixed tree over the block.
+template <int EPI>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFuse f, int rows, int ptiles, long long L) {
+  __shared__ double red[2][4];
+  const int r = blockIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int p = threadIdx.x; p < ptiles; p += 256) {
+    const double2 v = f.part[(size_t)p * rows + r];
+    s1 += v.x;
+    s2 += v.y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s1;
+    red[1][w] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    bn_finalize_row<EPI>(f, r, rows, L, (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]),
+                         (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
 }
 
 // KS > 1: intra-block K split.  The block is KS groups of 4 waves; group g
@@ -796,7 +838,7 @@ __global__ __launch_bounds__(256 * KS) void dconv_kernel(IgArgs a) {
       }
     }
     if (rowt && !(a.bn.dbg & 2)) bn_put(a.bn.part + (size_t)pt * rows + row, s1, s2);
-    bn_finish<EPI>(a, pt, rt, row0, BM);
+    if (a.bn.inkernel) bn_finish<EPI>(a, pt, rt, row0, BM);
     stamp(14);
     return;
   }
@@ -2223,9 +2265,12 @@ int launch_igemm(IgArgs& a, long long P, char* ws, hipStream_t s) {
       hipLaunchKernelGGL((igemm_kernel<32, MODE, ACT, EPI>), grid, dim3(256), 0, s, a);
   }
   int st = launch_status("conv kernel launch failed");
-  if (st || pl.ksplit == 1) return st;
+  if (st || (EPI < 5 && pl.ksplit == 1)) return st;
   if constexpr (EPI >= 5) {   // (never split; XF with split-K takes the finish below)
-    return st;
+    if (st || a.bn.inkernel) return st;
+    hipLaunchKernelGGL((bn_finalize_kernel<EPI>), dim3((unsigned)a.rows), dim3(256), 0, s, a.bn, a.rows,
+                       pl.ptiles, P);
+    return launch_status("bn_finalize_kernel launch failed");
   } else {
     const long long total = (long long)a.rows * P;
     long long blocks = (total + 255) / 256;
@@ -2375,7 +2420,12 @@ void bn_bind(BnFuse& f, void* state, const BnLayout& l) {
     const char* e = getenv("DRO_BN_ABLATE");
     return e ? atoi(e) : 0;
   }();
+  static const int inkernel = [] {   // DRO_BN_FOLD=kernel: the last block folds (A/B)
+    const char* e = getenv("DRO_BN_FOLD");
+    return e && strcmp(e, "kernel") == 0 ? 1 : 0;
+  }();
   f.dbg = dbg;
+  f.inkernel = inkernel;
 }
 
 const float* bn_coef(const void* state, const BnLayout& l) {

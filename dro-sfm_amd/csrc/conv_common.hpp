@@ -96,6 +96,7 @@ struct BnFuse {
   const float* xcoef;     // XF: coefficients of the staged source's BN
   const float* skip;      // XF 2
   float* yout;            // XF: owner stores of the transformed source
+  int inkernel;           // 1: the last block folds the partials (bn_finish), else bn_finalize_kernel
   int dbg;                // timing ablations (env DRO_BN_ABLATE, results invalid): 1 no arrival /
                           // fold, 2 no partial stores, 4 no row sums
 };

@@ -41,17 +41,23 @@ from ._lib import check, ptr, require_device, stream_of
 from .ops import _sink_of, record_branch
 from .conv import _workspace, _direct_targets, _queue_weight_grad, _conv_bwd, _grad_buffers, current_scope
 
-_ENABLED = [os.environ.get("DRO_BN_FUSION", "1") != "0"]
+# "large" (default): fused where a channel holds more than 16 K elements
+# (B*H*W > 16384: there hip.batchnorm_act takes two launches each way; below
+# it one, and the fused path's finalize launch and epilogue cost as much --
+# measured); "all": every 3x3 stride-1 site; "0": never
+_MODE = [{"0": "0", "1": "large", "large": "large", "all": "all"}.get(os.environ.get("DRO_BN_FUSION", "large"),
+                                                                      "large")]
+_LARGE = 16384
 
 
-def set_bn_fusion(enabled):
-    """BN fused into the 3x3 stride-1 convs (True, default) or hip.batchnorm_act
-    after each conv (False, A/B runs; DRO_BN_FUSION=0 at start-up)."""
-    _ENABLED[0] = bool(enabled)
+def set_bn_fusion(mode):
+    """True / "large" (default), "all" or False: which BN sites run inside the
+    3x3 stride-1 convs (A/B runs; DRO_BN_FUSION=0|large|all at start-up)."""
+    _MODE[0] = "large" if mode is True else ("0" if mode is False else str(mode))
 
 
 def bn_fusion_enabled():
-    return _ENABLED[0]
+    return _MODE[0] != "0"
 
 
 class DroBnParams(ctypes.Structure):
@@ -107,10 +113,14 @@ def site_of(bn, shape, device):
     return s
 
 
-def supported(bn, conv, x):
+def supported(bn, conv, x, elems=None):
     """The fused path applies: a training-mode BN with momentum after a 3x3
-    stride-1 'same' conv without bias on a float32 CUDA tensor."""
-    return (_ENABLED[0] and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and bn.training
+    stride-1 'same' conv without bias on a float32 CUDA tensor, with `elems`
+    (the BN's elements per channel, B*H*W) above the size policy's bound."""
+    if _MODE[0] == "0" or (_MODE[0] == "large" and (elems if elems is not None else
+                                                    x.shape[0] * x.shape[2] * x.shape[3]) <= _LARGE):
+        return False
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and bn.training
             and bn.momentum is not None and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
             and conv.padding_mode == "zeros")
@@ -272,6 +282,99 @@ class _BnReluConvStats(torch.autograd.Function):
         return g1, dg, db, gw, None, None, None, None, None
 
 
+def _bn_relu_backward(dy, z, y, gamma, smean, sinv, need_gamma, need_beta, gs):
+    """hip.batchnorm_act's backward (relu, skip gradient into gs when given):
+    (dz, dgamma, dbeta)."""
+    lib = _lib.load()
+    N, C, H, W = z.shape
+    gx = torch.empty_like(z)
+    gw = torch.empty(C, device=z.device) if need_gamma else None
+    gb = torch.empty(C, device=z.device) if need_beta else None
+    nws = lib.dro_batchnorm_workspace_bytes(N, C, H * W)
+    ws = torch.empty(max(nws, 16), device=z.device, dtype=torch.uint8)
+    check(lib.dro_batchnorm_relu_backward(
+        ptr(dy), ptr(z), ptr(y), ptr(gamma), ptr(smean), ptr(sinv), 1, N, C, H * W,
+        ptr(gx), ptr(gw), ptr(gb), ptr(gs), ptr(ws), nws, stream_of(dy)), "dro_batchnorm_relu_backward")
+    return gx, gw, gb
+
+
+class _BnAddReluConvStats(torch.autograd.Function):
+    """(y, z1) = (relu(bn2(z2) + skip), conv1(y)): a BasicBlock's output
+    staged by the NEXT block's conv1 from bn2's statistics (XF 2; y stored
+    once per pixel by the conv: it is that block's skip), with bn1's
+    statistics of z1 in conv1's epilogue.  Backward: conv1's data gradient
+    adds into dy (the skip's gradient the next bn2 returned), then bn2's
+    backward (dro_batchnorm_relu_backward)."""
+
+    @staticmethod
+    def forward(ctx, z2, gamma2, beta2, skip, w1, bn2, site2, bn1, site1, direct):
+        lib = _lib.load()
+        B, C, H, W = z2.shape
+        C1 = w1.shape[0]
+        skip = skip.contiguous()
+        y = torch.empty_like(z2)
+        z1 = torch.empty(B, C1, H, W, device=z2.device, dtype=torch.float32)
+        smean1 = torch.empty(C1, device=z2.device, dtype=torch.float32)
+        sinv1 = torch.empty(C1, device=z2.device, dtype=torch.float32)
+        prm = site1.params(bn1, smean1, sinv1)
+        ws, nws = _workspace(B, H, W, C, C1, 3, 3, z2.device)
+        check(lib.dro_conv2d_bn_forward(ptr(z2), B, H, W, C, ptr(w1), C1, ptr(site2.fwd), ptr(skip), ptr(y),
+                                        ctypes.byref(prm), ptr(site1.fwd), ptr(z1), ptr(ws), nws, stream_of(z2)),
+              "dro_conv2d_bn_forward")
+        site1.saved = (smean1, sinv1)
+        smean2, sinv2 = site2.saved
+        ctx.save_for_backward(z2, y, gamma2, smean2, sinv2, w1, z1)
+        ctx.site1, ctx.direct, ctx.scope = site1, direct, current_scope()
+        ctx.need_w = w1.requires_grad
+        ctx.skipsink = _sink_of(skip) if skip.requires_grad else None
+        ctx.y = y        # the parity tests' ReLU branch record
+        return y, z1
+
+    @staticmethod
+    def backward(ctx, gy, gz1):
+        z2, y, gamma2, smean2, sinv2, w1, z1 = ctx.saved_tensors
+        B, C, H, W = z2.shape
+        C1 = w1.shape[0]
+        site1 = ctx.site1
+        # the block output's gradient: what its other reader (the next bn2's
+        # skip) returned, plus conv1's data gradient added in place
+        if gy is not None:
+            dy, acc = gy.contiguous(), 1
+        else:
+            dy, acc = torch.empty_like(y), 0
+        gw1 = None
+        if gz1 is not None:
+            gz1 = gz1.contiguous()
+            if site1.g_ready and _stage_dz(B, H, W, C, C1):
+                site1.g_ready = False
+                dz1 = torch.empty_like(z1)
+                ws, nws = _workspace(B, H, W, C, C1, 3, 3, z2.device)
+                check(_lib.load().dro_conv2d_bn_backward_data(ptr(w1), B, H, W, C, C1, ptr(gz1), ptr(site1.bwd),
+                                                              ptr(z1), ptr(dz1), None, None, ptr(dy), acc, ptr(ws),
+                                                              nws, stream_of(gz1)), "dro_conv2d_bn_backward_data")
+            else:
+                if site1.g_ready:
+                    site1.g_ready = False
+                    dz1 = torch.empty_like(z1)
+                    check(_lib.load().dro_bn_backward_apply(ptr(gz1), ptr(z1), B, C1, H, W, ptr(site1.bwd),
+                                                            ptr(dz1), stream_of(gz1)), "dro_bn_backward_apply")
+                else:
+                    dz1 = gz1
+                _conv_bwd([y], w1, None, dz1, 0, 1.0, [dy], [acc])
+            gw1 = _weight_grad(ctx, [y], w1, dz1)
+        elif gy is None:
+            return (None,) * 10
+        gs, in_sink = None, False
+        if ctx.needs_input_grad[3]:
+            if ctx.skipsink is not None and not ctx.skipsink.written:
+                gs, in_sink = ctx.skipsink.target()[0], True
+            else:
+                gs = torch.empty_like(z2)
+        gx, gg, gb = _bn_relu_backward(dy, z2, y, gamma2, smean2, sinv2, ctx.needs_input_grad[1],
+                                       ctx.needs_input_grad[2], gs)
+        return gx, gg, gb, (None if in_sink else gs), gw1, None, None, None, None, None
+
+
 class _BnApply(torch.autograd.Function):
     """relu(bn(z) [+ skip]) from the statistics the producing conv left; the
     backward is hip.batchnorm_act's (dro_batchnorm_relu_backward)."""
@@ -310,6 +413,20 @@ class _BnApply(torch.autograd.Function):
             ptr(gy), ptr(x), ptr(y), ptr(weight), ptr(smean), ptr(sinv), ctx.relu, N, C, H * W,
             ptr(gx), ptr(gw), ptr(gb), ptr(gs), ptr(ws), nws, stream_of(gy)), "dro_batchnorm_relu_backward")
         return gx, gw, gb, (None if in_sink else gs), None, None, None
+
+
+def bn_add_relu_conv_stats(z2, bn2, skip, conv1, bn1):
+    """(relu(bn2(z2) + skip), conv1 of it) with z2 from a conv that took
+    bn2's statistics: the block output is staged (and stored) by the next
+    block's conv1, whose epilogue takes bn1's statistics."""
+    site2 = site_of(bn2, z2.shape, z2.device)
+    if site2.saved is None:
+        raise RuntimeError("bn_add_relu_conv_stats: z2 must come from a conv that took bn2's statistics")
+    site1 = site_of(bn1, (z2.shape[0], conv1.weight.shape[0], z2.shape[2], z2.shape[3]), z2.device)
+    y, z1 = _BnAddReluConvStats.apply(z2, bn2.weight, bn2.bias, skip, conv1.weight, bn2, site2, bn1, site1,
+                                      _direct(conv1.weight))
+    record_branch(("relu", getattr(bn2, "_dro_tag", None)), lambda: (y > 0).to(torch.uint8), z2)
+    return y, z1
 
 
 def _direct(w):

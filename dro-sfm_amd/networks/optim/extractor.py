@@ -6,10 +6,18 @@ BasicBlocks (conv1/bn1/conv2/bn2[/downsample.0,1]), upconv1.0,
 upconv1_fusion.0, out_conv (+ upconv2*, stride 4).  Pretrained ImageNet
 weights are never downloaded -- load a checkpoint instead.
 
-Training-mode batch normalisation runs fused with the ReLU / residual add that
-follows it (hip.batchnorm_act, csrc/batchnorm.hip: one launch each way where a
-channel fits one block, two otherwise, with fixed-order fp64 statistics,
-against 6-9 PyTorch launches per site).  Not MIOpen's BN: measured on MI355X
+Training-mode batch normalisation (round 6) runs INSIDE the 3x3 stride-1
+convolutions at the sites whose channels hold more than 16 K elements (the
+layer1 blocks of fnet and cnet_pose at KITTI size; hip.bnconv's size policy,
+"all" for every stride-1 site) (hip.bnconv, csrc/conv.hip BnFuse): the
+producing conv's epilogue takes the batch statistics, the consuming conv
+stages relu(bn(.) [+ skip]) and stores it once, the consumer's data gradient
+takes the BN backward's statistics; a stage's first block output is staged by
+the second block's conv1 (run_stage).  After the stride-2 convs (stage
+entries, downsamples, stems) BN runs as hip.batchnorm_act (csrc/batchnorm.hip:
+one launch each way where a channel fits one block, two otherwise) -- both
+with fixed-order fp64 statistics, against 6-9 PyTorch launches per site
+(DRO_BN_FUSION=0|large|all / hip.bnconv.set_bn_fusion: A/B runs).  Not MIOpen's BN: measured on MI355X
 in round 2, its one-pass variance put 1e-2 relative error on encoder gradients
 against the fp64 oracle.  Eval mode and CPU tensors use PyTorch's native
 kernels.
@@ -94,10 +102,14 @@ def set_fused_batchnorm(enabled):
     _FUSED_BN[0] = bool(enabled)
 
 
-def _fused_bn_ok(bn, conv, x):
+def _fused_bn_ok(bn, conv, x, stride=1):
     """BN inside the conv launches (hip.bnconv) for this site: the native conv
-    engine and the fused BN are on and the conv is 3x3 stride 1 (round 6)."""
-    return _FUSED_BN[0] and _NATIVE_CONV[0] and bnconv.supported(bn, conv, x)
+    engine and the fused BN are on, the conv is 3x3 stride 1 and the site is
+    inside hip.bnconv's size policy (x: the block input, `stride` the block's)."""
+    if x.dim() != 4:
+        return False
+    elems = x.shape[0] * ((x.shape[2] - 1) // stride + 1) * ((x.shape[3] - 1) // stride + 1)
+    return _FUSED_BN[0] and _NATIVE_CONV[0] and bnconv.supported(bn, conv, x, elems)
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -134,22 +146,39 @@ class BasicBlock(nn.Module):
             self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
                                             BatchNorm2d(cout))
 
+    def fused_ok(self, x):
+        """BN inside the 3x3 stride-1 convs (hip.bnconv) for this block."""
+        return _fused_bn_ok(self.bn2, self.conv2, x, self.conv1.stride[0])
+
+    def forward_z2(self, x):
+        """(z2, skip): conv2's output with bn2's statistics taken (hip.bnconv)
+        and the skip -- relu(bn2(z2) + skip) is the block's output.  In a
+        stride-1 block conv1 takes bn1's statistics and conv2 stages
+        relu(bn1(.)) itself; a stride-2 block keeps bn1 / the downsample's BN
+        after the strided convs (hip.batchnorm_act)."""
+        x = hip.grad_sink(x)
+        if self.downsample is None and bnconv.supported(self.bn1, self.conv1, x):
+            z1 = bnconv.conv_bn_stats(x, self.conv1, self.bn1)
+            return bnconv.bn_relu_conv_stats(z1, self.bn1, self.conv2, self.bn2), x
+        y = self.bn1.act(conv3x3(self.conv1, x))
+        skip = x if self.downsample is None else self.downsample[1].act(conv3x3(self.downsample[0], x), relu=False)
+        return bnconv.conv_bn_stats(y, self.conv2, self.bn2), skip
+
+    def forward_after(self, z2p, skipp, bn2p):
+        """This (stride-1) block on the previous block's (z2, skip, bn2): its
+        conv1 stages the previous output relu(bn2p(z2p) + skipp) and stores it
+        (it is this block's skip) -- no apply launch for the previous block."""
+        x, z1 = bnconv.bn_add_relu_conv_stats(z2p, bn2p, skipp, self.conv1, self.bn1)
+        z2 = bnconv.bn_relu_conv_stats(z1, self.bn1, self.conv2, self.bn2)
+        return bnconv.bn_apply(z2, self.bn2, skip=x)
+
     def forward(self, x):
         # conv1, the skip (or the downsample) all read x: their input gradients
         # meet in place in a sink (the skip's BN backward writes it first)
+        if self.fused_ok(x):
+            z2, skip = self.forward_z2(x)
+            return bnconv.bn_apply(z2, self.bn2, skip=skip)
         x = hip.grad_sink(x)
-        if _fused_bn_ok(self.bn2, self.conv2, x):
-            # BN inside the 3x3 stride-1 convs (hip.bnconv): conv2 takes bn2's
-            # statistics in its epilogue; in a stride-1 block conv1 takes bn1's
-            # and conv2 stages relu(bn1(.)) itself
-            if self.downsample is None and bnconv.supported(self.bn1, self.conv1, x):
-                z1 = bnconv.conv_bn_stats(x, self.conv1, self.bn1)
-                z2 = bnconv.bn_relu_conv_stats(z1, self.bn1, self.conv2, self.bn2)
-                return bnconv.bn_apply(z2, self.bn2, skip=x)
-            y = self.bn1.act(conv3x3(self.conv1, x))
-            skip = x if self.downsample is None else \
-                self.downsample[1].act(conv3x3(self.downsample[0], x), relu=False)
-            return bnconv.bn_apply(bnconv.conv_bn_stats(y, self.conv2, self.bn2), self.bn2, skip=skip)
         y = self.bn1.act(conv3x3(self.conv1, x))
         if self.downsample is None:
             skip = x
@@ -160,6 +189,18 @@ class BasicBlock(nn.Module):
 
 def _stage(cin, cout, stride):
     return nn.Sequential(BasicBlock(cin, cout, stride), BasicBlock(cout, cout, 1))
+
+
+def run_stage(stage, x):
+    """stage(x) for a ResNet stage of two BasicBlocks; with the fused BN path
+    the first block's output is staged by the second block's conv1
+    (BasicBlock.forward_after) instead of being applied by its own launch."""
+    b0, b1 = stage[0], stage[1]
+    if (len(stage) == 2 and b0.fused_ok(x) and b1.downsample is None
+            and bnconv.supported(b1.bn1, b1.conv1, x) and b1.fused_ok(x)):
+        z2, skip = b0.forward_z2(x)
+        return b1.forward_after(z2, skip, b0.bn2)
+    return stage(x)
 
 
 class ResNetEncoder(nn.Module):
@@ -201,9 +242,9 @@ class ResNetEncoder(nn.Module):
         x = self.bn1.act(conv3x3(self.conv1, x))
         x = (hip.maxpool3x3s2(x, getattr(self, "_dro_tag", None)) if (x.is_cuda and _NATIVE_POOL[0])
              else F.max_pool2d(x, 3, 2, 1))
-        s4 = self.layer1(x)
-        s8 = self.layer2(s4)
-        x = self.layer3(s8)
+        s4 = run_stage(self.layer1, x)
+        s8 = run_stage(self.layer2, s4)
+        x = run_stage(self.layer3, s8)
         rec = hip.ops.record_relu         # parity tests: the ReLU branch of each decoder conv
         x = rec(conv3x3(self.upconv1[0], hip.bilinear_upsample2x(x), "relu"), self.upconv1[0])
         x = rec(conv3x3(self.upconv1_fusion[0], [x, s8], "relu"), self.upconv1_fusion[0])   # concat read in place

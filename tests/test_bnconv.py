@@ -66,7 +66,7 @@ def _run(blk, x, gout, fused, masks=None):
     mask y > 0 (the product's branch record, hip.ops.record_branch)."""
     for name in ("bn1", "bn2"):
         object.__setattr__(getattr(blk, name), "_dro_tag", name)
-    bnconv.set_bn_fusion(fused)
+    bnconv.set_bn_fusion("all" if fused else False)
     try:
         xd = x.clone().requires_grad_()
         with record_bilinear_cells() as rec:
@@ -78,6 +78,13 @@ def _run(blk, x, gout, fused, masks=None):
         return out.detach(), xd.grad, {n: t.grad.clone() for n, t in blk.named_parameters()}
     finally:
         bnconv.set_bn_fusion(True)
+
+
+@pytest.fixture
+def all_sites():
+    bnconv.set_bn_fusion("all")
+    yield
+    bnconv.set_bn_fusion(True)
 
 
 CASES = [  # (cin, cout, stride, B, H, W): KITTI layer1 / layer2 / layer3, ragged, batch 1
@@ -121,6 +128,74 @@ def test_fused_block_matches_fp64(case):
             assert int(t) == 1, n
 
 
+def _stage_reference(stage, x, gout, masks):
+    """fp64 CPU forward + backward of a two-block stage, ReLUs pinned to the
+    product's masks (tags b<i>.bn<j>)."""
+    p = {n: t.detach().double().cpu().requires_grad_() for n, t in stage.named_parameters()}
+    bufs = {n: t.detach().double().cpu() for n, t in stage.named_buffers() if "running" in n}
+    xr = x.detach().double().cpu().requires_grad_()
+
+    def bn(z, name):
+        return F.batch_norm(z, bufs[name + ".running_mean"], bufs[name + ".running_var"], p[name + ".weight"],
+                            p[name + ".bias"], training=True, momentum=0.1, eps=1e-5)
+
+    h = xr
+    for i in range(2):
+        blk = stage[i]
+        s = blk.conv1.stride[0]
+        y = bn(F.conv2d(h, p[f"{i}.conv1.weight"], stride=s, padding=1), f"{i}.bn1") * masks[f"b{i}.bn1"].double()
+        z2 = bn(F.conv2d(y, p[f"{i}.conv2.weight"], padding=1), f"{i}.bn2")
+        skip = h if blk.downsample is None else bn(F.conv2d(h, p[f"{i}.downsample.0.weight"], stride=s),
+                                                    f"{i}.downsample.1")
+        h = (z2 + skip) * masks[f"b{i}.bn2"].double()
+    h.backward(gout.double().cpu())
+    return h.detach(), xr.grad, {n: t.grad for n, t in p.items()}, bufs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(64, 64, 1, 6, 48, 160), (64, 128, 2, 6, 48, 160), (128, 256, 2, 2, 24, 80)],
+                         ids=lambda c: "x".join(map(str, c)))
+def test_fused_stage_matches_fp64(case, all_sites):
+    """extractor.run_stage: the first block's output staged (and stored) by
+    the second block's conv1 (bn_add_relu_conv_stats), against fp64."""
+    cin, cout, stride, B, H, W = case
+    torch.manual_seed(9)
+    stage = extractor._stage(cin, cout, stride)
+    with torch.no_grad():
+        for m in stage.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.3, 0.3)
+    stage = stage.cuda().train()
+    for i in range(2):
+        for name in ("bn1", "bn2"):
+            object.__setattr__(getattr(stage[i], name), "_dro_tag", f"b{i}.{name}")
+    g = torch.Generator().manual_seed(10)
+    x = (0.5 + torch.randn(B, cin, H, W, generator=g)).cuda()
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    gout = torch.randn(B, cout, Ho, Wo, generator=g).cuda()
+    bufs0 = {n: t.clone() for n, t in stage.named_buffers()}
+    xd = x.clone().requires_grad_()
+    with record_bilinear_cells() as rec:
+        out = extractor.run_stage(stage, xd)
+    out.backward(gout)
+    masks = {tag[1]: m.bool().cpu() for tag, m in rec.calls if tag[0] == "relu"}
+    assert {"b0.bn1", "b0.bn2", "b1.bn1", "b1.bn2"} <= set(masks)
+    fused_bufs = {n: t.clone() for n, t in stage.named_buffers()}
+    with torch.no_grad():
+        for n, t in stage.named_buffers():
+            t.copy_(bufs0[n])
+    ref_out, ref_gx, ref_gp, ref_bufs = _stage_reference(stage, x, gout, masks)
+    torch.testing.assert_close(out.detach().double().cpu(), ref_out, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(xd.grad.double().cpu(), ref_gx, rtol=1e-4, atol=1e-4)
+    for n, t in stage.named_parameters():
+        scale = max(1.0, float(ref_gp[n].abs().max()))
+        torch.testing.assert_close(t.grad.double().cpu(), ref_gp[n], rtol=1e-4, atol=1e-4 * scale, msg=n)
+    for n, t in fused_bufs.items():
+        if "running" in n:
+            torch.testing.assert_close(t.double().cpu(), ref_bufs[n], rtol=1e-5, atol=1e-6, msg=n)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[4]], ids=lambda c: "x".join(map(str, c)))
 def test_fused_block_equals_unfused_hip(case):
@@ -145,7 +220,7 @@ def test_fused_block_equals_unfused_hip(case):
 
 
 @pytest.mark.gpu
-def test_fused_block_repeat_and_graph_replay():
+def test_fused_block_repeat_and_graph_replay(all_sites):
     """Repeated calls reuse the per-site states (counters reset by the kernels):
     every call equals the first, eager and replayed from a captured graph."""
     blk = _block(64, 64, 1, seed=7).cuda()
@@ -195,3 +270,17 @@ def test_bn_state_bytes_cpu():
     assert n >= 720 * 64 * 16 + 23 * 64 * 16 + 5 * 64 * 4
     assert lib.dro_bn_state_bytes(0, 48, 160, 64) == 0
     assert lib.dro_bn_state_bytes(6, 48, 160, 0) == 0
+
+
+def test_size_policy_cpu():
+    """Default policy: fused only where a channel holds > 16 K elements."""
+    blk = extractor.BasicBlock(64, 64, 1).train()
+    x = torch.empty(6, 64, 48, 160, device="meta")
+    conv, bn = blk.conv2, blk.bn2
+    assert not bnconv.supported(bn, conv, x)            # meta tensors are not CUDA
+    bnconv.set_bn_fusion(False)
+    try:
+        assert not bnconv.bn_fusion_enabled()
+    finally:
+        bnconv.set_bn_fusion(True)
+    assert bnconv.bn_fusion_enabled()
