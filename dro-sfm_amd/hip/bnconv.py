@@ -327,7 +327,6 @@ class _BnAddReluConvStats(torch.autograd.Function):
         ctx.site1, ctx.direct, ctx.scope = site1, direct, current_scope()
         ctx.need_w = w1.requires_grad
         ctx.skipsink = _sink_of(skip) if skip.requires_grad else None
-        ctx.y = y        # the parity tests' ReLU branch record
         return y, z1
 
     @staticmethod
