@@ -1596,6 +1596,155 @@ static void launch_wgrad_finish(const IgArgs& a, int splits, hipStream_t s) {
   else hipLaunchKernelGGL(wgrad_finish_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
 }
 
+// ------------------------------------------------------------------ 7x7 weight gradient
+// The encoders' 7x7 stems (stride 2, pad 3, 3 or 6 input channels;
+// extractor.py:59 via torchvision conv1) and the update blocks' 7x7 state
+// convs (stride 1, pad 3, 1 or 6 channels; update.py:77-124).  wgrad_kernel
+// gathered every (tap, channel) column from global memory per 64-pixel chunk
+// (25-32 TF/s on the stems).  Here a block walks 8x8 output-pixel tiles
+// (tile = blockIdx.x + k * gridDim.x, rows o0 = 64 * blockIdx.y), staging per
+// tile G[64 o][64 px] and the Cin x PD x PD input patch the tile reads (PD =
+// 7 S + 7, zero outside the image) into LDS; the MFMA B operand of column n =
+// tap * Cin + c at pixel p is the patch value at (S py + ty, S px + tx) -- one
+// shifted LDS read per lane per MFMA pair (both 32-row halves of A share it).
+// Wave w owns 32-column subtiles w, w + NW, ... (J of them).  The bias column
+// (NK) is the per-block row sum of G.  Partials [split][Cout][NK + 1] for
+// wgrad_finish_kernel (fixed order: the same finish as wgrad_kernel's).
+template <int S, int CIN, int NW, int J>
+__global__ __launch_bounds__(64 * NW) void wgrad_k7_kernel(IgArgs a) {
+  constexpr int PD = 7 * S + 7, PDP = PD | 1, GS = 65, NK = CIN * 49, NSUB = (NK + 31) / 32;
+  constexpr int NTH = 64 * NW, PATCH = CIN * PD * PDP, NPE = CIN * PD * PD;
+  constexpr int GPER = (4096 + NTH - 1) / NTH, PPER = (NPE + NTH - 1) / NTH;
+  static_assert(NW * J >= NSUB && NW <= 8, "subtiles per wave");
+  __shared__ float Gs[64 * GS];
+  __shared__ float Ps[PATCH + 1];        // [CIN][PD][PDP], then one zero
+  const int Cout = a.g.Cout, B = a.g.B, Ho = a.g.H, Wo = a.g.W;
+  const int Hi = a.Hs, Wi = a.Ws;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int o0 = blockIdx.y * 64;
+  const int txs = (Wo + 7) / 8, tis = ((Ho + 7) / 8) * txs, tiles = B * tis;
+  const float* __restrict__ Gp = a.G;
+  const float* __restrict__ X = a.src[0].p;
+  // per lane and subtile: the B operand's patch offset (the zero slot past
+  // the patch for padded columns)
+  int boff[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int n = (wave + j * NW) * 32 + (lane & 31);
+    if (n < NK) {
+      const int tap = n / CIN, c = n - tap * CIN, ty = tap / 7, tx = tap - ty * 7;
+      boff[j] = (c * PD + ty) * PDP + tx;
+    } else {
+      boff[j] = -1;
+    }
+  }
+  const int h = lane >> 5;
+  f32x16 acc[J][2];
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][u][r] = 0.f;
+  float bsum = 0.f;                      // bias column: thread o < 64
+  if (tid == 0) Ps[PATCH] = 0.f;
+  // this thread's staging slots (compile-time counts): the next tile's G and
+  // patch are loaded into registers while the current one is multiplied
+  float gr[GPER], pr[PPER];
+  auto load_tile = [&](int t) {
+    const int b = t / tis, r0 = t - b * tis, tyi = r0 / txs, txi = r0 - tyi * txs;
+    const int oy0 = tyi * 8, ox0 = txi * 8, iy0 = S * oy0 - 3, ix0 = S * ox0 - 3;
+    const float* gb = Gp + ((size_t)b * Cout + o0) * Ho * Wo;
+    const float* xb = X + (size_t)b * CIN * Hi * Wi;
+#pragma unroll
+    for (int i = 0; i < GPER; ++i) {
+      const int e = tid + i * NTH;
+      const int o = e >> 6, p = e & 63, oy = oy0 + (p >> 3), ox = ox0 + (p & 7);
+      const bool ok = (GPER * NTH == 4096 || e < 4096) && o0 + o < Cout && oy < Ho && ox < Wo;
+      gr[i] = ok ? gb[((size_t)o * Ho + oy) * Wo + ox] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PPER; ++i) {
+      const int e = tid + i * NTH;
+      const int c = e / (PD * PD), rem = e - c * (PD * PD), yy = rem / PD, xx = rem - yy * PD;
+      const int iy = iy0 + yy, ix = ix0 + xx;
+      const bool ok = e < NPE && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+      pr[i] = ok ? xb[((size_t)c * Hi + iy) * Wi + ix] : 0.f;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < GPER; ++i) {
+      const int e = tid + i * NTH;
+      if (GPER * NTH == 4096 || e < 4096) Gs[(e >> 6) * GS + (e & 63)] = gr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < PPER; ++i) {
+      const int e = tid + i * NTH;
+      if (e < NPE) {
+        const int c = e / (PD * PD), rem = e - c * (PD * PD), yy = rem / PD, xx = rem - yy * PD;
+        Ps[(c * PD + yy) * PDP + xx] = pr[i];
+      }
+    }
+  };
+  if ((int)blockIdx.x < tiles) {
+    load_tile(blockIdx.x);
+    store_tile();
+  }
+  __syncthreads();
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    if (tn < tiles) load_tile(tn);
+    if (a.gbias && tid < 64) {
+      float sb = 0.f;
+      for (int p = 0; p < 64; ++p) sb += Gs[tid * GS + p];
+      bsum += sb;
+    }
+    // LDS operands one step ahead of the MFMAs
+    float a0n = Gs[(lane & 31) * GS + h], a1n = Gs[(32 + (lane & 31)) * GS + h];
+    float bn[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) bn[j] = Ps[boff[j] < 0 ? PATCH : boff[j] + S * h];
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const float a0 = a0n, a1 = a1n;
+      float bv[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) bv[j] = bn[j];
+      if (k + 1 < 32) {
+        const int p = 2 * (k + 1) + h, po = S * (p >> 3) * PDP + S * (p & 7);
+        a0n = Gs[(lane & 31) * GS + p];
+        a1n = Gs[(32 + (lane & 31)) * GS + p];
+#pragma unroll
+        for (int j = 0; j < J; ++j) bn[j] = Ps[boff[j] < 0 ? PATCH : boff[j] + po];
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        acc[j][0] = mfma32(a0, bv[j], acc[j][0]);
+        acc[j][1] = mfma32(a1, bv[j], acc[j][1]);
+      }
+    }
+    __syncthreads();                     // every wave is done with this tile
+    if (tn < tiles) store_tile();
+    __syncthreads();
+  }
+  const int NKr = NK;
+  float* part = a.part + (size_t)blockIdx.x * Cout * (NKr + 1);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int n = (wave + j * NW) * 32 + (lane & 31);
+    if (n >= NK) continue;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < Cout) part[(size_t)o * (NK + 1) + n] = acc[j][u][r];
+      }
+  }
+  if (a.gbias && tid < 64 && o0 + tid < Cout) part[(size_t)(o0 + tid) * (NK + 1) + NK] = bsum;
+}
+
 // G = alpha * dout * act'(y) (only when act != none or alpha != 1)
 // grid (pixel blocks, B * Cout planes): no 64-bit division per element
 __global__ __launch_bounds__(256) void grad_pre_kernel(int act, float alpha, int Cout, int HW,
@@ -2118,6 +2267,56 @@ void conv_logf(double flops, const char* fmt, Ts... args) {
   snprintf(buf, sizeof(buf), fmt, args...);
   conv_log(buf, flops);
 }
+
+// the 7x7 path applies (weights of < 4096 floats per row, 64-row tiles)
+bool k7_ok(int KH, int KW, int Cin, int pad, int stride) {
+  static const bool off = getenv("DRO_K7_WGRAD_OFF") != nullptr;   // A/B: wgrad_kernel for them
+  return !off && KH == 7 && KW == 7 && pad == 3 &&
+         ((stride == 2 && (Cin == 3 || Cin == 6)) || (stride == 1 && (Cin == 1 || Cin == 6)));
+}
+
+// launches wgrad_k7_kernel + the finish with `splits` <= the caller's
+// wgrad_kernel plan (same partial workspace)
+// blocks (= partials) of the 7x7 weight gradient: >= 4 tiles per block, at
+// most 256 (measured at the stems, tools/bench_k7.py: 256 blocks of 11 tiles
+// 88 us for fnet's; 720 of 4 108 us -- the partials' traffic grows faster
+// than the SIMD balance improves)
+int k7_splits(int B, int Ho, int Wo) {
+  static const int per = (int)env_int("DRO_K7_TILES_PER_BLOCK", 4);
+  static const int cap = (int)env_int("DRO_K7_MAX_BLOCKS", 256);
+  const int tiles = B * ((Ho + 7) / 8) * ((Wo + 7) / 8);
+  int sp = (tiles + per - 1) / per;
+  if (sp > cap) sp = cap;
+  return sp < 1 ? 1 : sp;
+}
+
+size_t k7_part_bytes(int B, int Ho, int Wo, int Cin, int Cout) {
+  return align256((size_t)k7_splits(B, Ho, Wo) * Cout * (Cin * 49 + 1) * sizeof(float));
+}
+
+int launch_wgrad_k7(IgArgs& a, int stride, int splits, hipStream_t s) {
+  const int Cin = a.g.Cin, NK = Cin * 49;
+  const int tiles = a.g.B * ((a.g.H + 7) / 8) * ((a.g.W + 7) / 8);
+  if (splits > tiles) splits = tiles;
+  if (splits < 1) splits = 1;
+  const dim3 grid((unsigned)splits, (unsigned)((a.g.Cout + 63) / 64));
+  conv_logf(2.0 * a.g.Cout * NK * (double)a.g.B * a.g.H * a.g.W, "wgrad_k7_kernel<%d, %d>", stride, Cin);
+  // (S, CIN, waves, subtiles per wave): 32-column subtiles of the 49 Cin columns
+  if (stride == 2 && Cin == 3) hipLaunchKernelGGL((wgrad_k7_kernel<2, 3, 5, 1>), grid, dim3(320), 0, s, a);
+  else if (stride == 2 && Cin == 6) hipLaunchKernelGGL((wgrad_k7_kernel<2, 6, 5, 2>), grid, dim3(320), 0, s, a);
+  else if (stride == 1 && Cin == 1) hipLaunchKernelGGL((wgrad_k7_kernel<1, 1, 2, 1>), grid, dim3(128), 0, s, a);
+  else if (stride == 1 && Cin == 6) hipLaunchKernelGGL((wgrad_k7_kernel<1, 6, 5, 2>), grid, dim3(320), 0, s, a);
+  else {
+    set_error("wgrad_k7: unsupported channel count");
+    return DRO_E_SHAPE;
+  }
+  int st = launch_status("wgrad_k7_kernel launch failed");
+  if (st) return st;
+  a.K = NK;
+  launch_wgrad_finish(a, splits, s);
+  return launch_status("wgrad_finish_kernel launch failed");
+}
+
 
 template <int MODE, int EPI>
 bool thin_ok(const IgArgs& a) {
@@ -2929,6 +3128,13 @@ static int conv2d_backward_impl(const dro_slice* srcs, int nsrc, const float* we
     a.otiles = pl.otiles;
     a.pchunk = pl.pchunk;
     a.part = reinterpret_cast<float*>(ws_wg);
+    if (nsrc == 1 && !srcs[0].broadcast && srcs[0].channel_offset == 0 && srcs[0].total_channels == srcs[0].channels &&
+        k7_ok(KH, KW, a.g.Cin, KH / 2, 1)) {
+      // the update blocks' 7x7 state convs (stride 1, one dense source)
+      a.Hs = H;
+      a.Ws = W;
+      return launch_wgrad_k7(a, 1, pl.splits, s);
+    }
     conv_log("wgrad_kernel(", 2.0 * Cout * a.g.Cin * T * (double)P);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits),
                        dim3(256), 0, s, a);
@@ -3102,7 +3308,8 @@ extern "C" size_t dro_conv2d_strided_workspace_bytes(int B, int Hi, int Wi, int 
   const size_t fwd = plan_igemm_flat(Cout, Cin, KH, KW, B, Ho, Wo).part_bytes;
   const size_t dg = std::max(plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes,
                              stride == 2 ? plan_class_dgrad(B, Hi, Wi, Cin, Cout, KH, KW).part_bytes : (size_t)0);
-  const size_t wg = plan_wgrad(Cin, Cout, KH * KW, (long long)B * Ho * Wo).part_bytes;
+  size_t wg = plan_wgrad(Cin, Cout, KH * KW, (long long)B * Ho * Wo).part_bytes;
+  if (k7_ok(KH, KW, Cin, pad, stride)) wg = std::max(wg, k7_part_bytes(B, Ho, Wo, Cin, Cout));
   return std::max(fwd, align256(dg) + wg);
 }
 
@@ -3216,6 +3423,7 @@ extern "C" int dro_conv2d_strided_backward(const float* x, const float* weight, 
     a.part = reinterpret_cast<float*>(
         ws + align256(std::max(plan_igemm_flat(Cin, Cout, KH, KW, B, Hi, Wi).part_bytes,
                                stride == 2 ? plan_class_dgrad(B, Hi, Wi, Cin, Cout, KH, KW).part_bytes : (size_t)0)));
+    if (k7_ok(KH, KW, Cin, pad, stride)) return launch_wgrad_k7(a, stride, k7_splits(B, Ho, Wo), s);   // the stems
     conv_log("wgrad_kernel(", 2.0 * Cout * Cin * T * (double)P);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(pl.otiles * pl.ntiles), (unsigned)pl.splits), dim3(256), 0,
                        s, a);

@@ -332,6 +332,7 @@ def test_weight_split_exact(hip):
     (2, 64, 128, 48, 160, 1, 2, 0, False, None),     # 1x1/s2 downsample
     (2, 3, 64, 64, 96, 7, 2, 3, False, None),        # 7x7/s2 stem (3 channels)
     (1, 6, 64, 47, 81, 7, 2, 3, False, None),        # cnet_pose stem, odd input size
+    (2, 6, 64, 192, 640, 7, 2, 3, False, None),      # KITTI-size stem (wgrad_k7_kernel: 240 tiles per image)
     (2, 20, 24, 17, 23, 3, 2, 1, True, "relu"),      # odd sizes, bias + relu forward
     (2, 16, 40, 12, 20, 3, 1, 0, True, None),        # stride 1, no padding
     (2, 20, 24, 17, 23, 3, 2, 1, True, None),        # odd sizes: parity classes of unequal size
