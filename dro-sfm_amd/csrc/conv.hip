@@ -1745,6 +1745,103 @@ __global__ __launch_bounds__(64 * NW) void wgrad_k7_kernel(IgArgs a) {
   if (a.gbias && tid < 64 && o0 + tid < Cout) part[(size_t)(o0 + tid) * (NK + 1) + NK] = bsum;
 }
 
+// The stems' forward (7x7, stride 2, pad 3, 3 or 6 input channels, no bias
+// or activation: BN follows): out[o, p] = sum_k W[o, k] Xpatch[k, p], k = tap
+// * Cin + c.  The weights (64 x 49 Cin) are staged in LDS once per block, a
+// block walks 8x8 output tiles with the next tile's input patch loaded into
+// registers while the current one is multiplied; the four waves take the
+// four 32 x 32 quadrants (output-channel half x pixel half) of the tile --
+// balanced over the SIMDs -- and the B operand is the patch value at
+// (2 py + ty, 2 px + tx): one shifted LDS read per MFMA.  igemm_kernel
+// gathered every (tap, channel) row from global memory (30 TF/s).
+template <int CIN>
+__global__ __launch_bounds__(256) void fwd_k7s2_kernel(IgArgs a) {
+  constexpr int S = 2, PD = 7 * S + 7, PDP = PD | 1, NK = CIN * 49, KP = NK + 1;   // odd row stride
+  constexpr int KSTEPS = (NK + 1) / 2, NPE = CIN * PD * PD, PPER = (NPE + 255) / 256;
+  __shared__ float Ws[64 * KP];
+  __shared__ float Ps[CIN * PD * PDP + 1];
+  __shared__ int koff[2 * KSTEPS];      // patch offset of column k (the zero slot past NK)
+  const int Cout = a.g.Cout, B = a.g.B, Ho = a.g.H, Wo = a.g.W, Hi = a.Hs, Wi = a.Ws;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int oh = wave & 1, ph = wave >> 1, h = lane >> 5;
+  const int o0 = blockIdx.y * 64;
+  const int txs = (Wo + 7) / 8, tis = ((Ho + 7) / 8) * txs, tiles = B * tis;
+  const float* __restrict__ X = a.src[0].p;
+  for (int e = tid; e < 64 * NK; e += 256) {
+    const int o = e / NK, k = e - o * NK;
+    // torch weight layout [o][c][ty][tx]; column k = tap * Cin + c
+    const int tap = k / CIN, c = k - tap * CIN;
+    Ws[o * KP + k] = o0 + o < Cout ? a.weight[((size_t)(o0 + o) * CIN + c) * 49 + tap] : 0.f;
+  }
+  if (tid < 64) Ws[tid * KP + NK] = 0.f;
+  for (int k = tid; k < 2 * KSTEPS; k += 256) {
+    const int tap = k / CIN, c = k - tap * CIN, ty = tap / 7, tx = tap - ty * 7;
+    koff[k] = k < NK ? (c * PD + ty) * PDP + tx : CIN * PD * PDP;
+  }
+  if (tid == 0) Ps[CIN * PD * PDP] = 0.f;
+  const int pl = ph * 32 + (lane & 31), py = pl >> 3, px = pl & 7;
+  const int poff = S * py * PDP + S * px;
+  float pr[PPER];
+  auto load_tile = [&](int t) {
+    const int b = t / tis, r0 = t - b * tis, tyi = r0 / txs, txi = r0 - tyi * txs;
+    const int iy0 = S * tyi * 8 - 3, ix0 = S * txi * 8 - 3;
+    const float* xb = X + (size_t)b * CIN * Hi * Wi;
+#pragma unroll
+    for (int i = 0; i < PPER; ++i) {
+      const int e = tid + i * 256;
+      const int c = e / (PD * PD), rem = e - c * (PD * PD), yy = rem / PD, xx = rem - yy * PD;
+      const int iy = iy0 + yy, ix = ix0 + xx;
+      const bool ok = e < NPE && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+      pr[i] = ok ? xb[((size_t)c * Hi + iy) * Wi + ix] : 0.f;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < PPER; ++i) {
+      const int e = tid + i * 256;
+      if (e < NPE) {
+        const int c = e / (PD * PD), rem = e - c * (PD * PD), yy = rem / PD, xx = rem - yy * PD;
+        Ps[(c * PD + yy) * PDP + xx] = pr[i];
+      }
+    }
+  };
+  if ((int)blockIdx.x < tiles) {
+    load_tile(blockIdx.x);
+    store_tile();
+  }
+  __syncthreads();
+  const float* wrow = Ws + (oh * 32 + (lane & 31)) * KP + h;
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    if (tn < tiles) load_tile(tn);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    float an = wrow[0], bn = Ps[koff[h] + poff];
+#pragma unroll 8
+    for (int s2 = 0; s2 < KSTEPS; ++s2) {
+      const float av = an, bv = bn;
+      if (s2 + 1 < KSTEPS) {
+        an = wrow[2 * (s2 + 1)];
+        bn = Ps[koff[2 * (s2 + 1) + h] + poff];
+      }
+      acc = mfma32(av, bv, acc);
+    }
+    const int b = t / tis, r0 = t - b * tis, tyi = r0 / txs, txi = r0 - tyi * txs;
+    const int oy = tyi * 8 + py, ox = txi * 8 + px;
+    if (oy < Ho && ox < Wo) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + oh * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < Cout) a.out[(((size_t)b * a.out_ctot + a.out_coff + o) * Ho + oy) * Wo + ox] = acc[r];
+      }
+    }
+    __syncthreads();                     // every wave is done with this patch
+    if (tn < tiles) store_tile();
+    __syncthreads();
+  }
+}
+
 // G = alpha * dout * act'(y) (only when act != none or alpha != 1)
 // grid (pixel blocks, B * Cout planes): no 64-bit division per element
 __global__ __launch_bounds__(256) void grad_pre_kernel(int act, float alpha, int Cout, int HW,
@@ -2315,6 +2412,24 @@ int launch_wgrad_k7(IgArgs& a, int stride, int splits, hipStream_t s) {
   a.K = NK;
   launch_wgrad_finish(a, splits, s);
   return launch_status("wgrad_finish_kernel launch failed");
+}
+
+// the stems' forward on fwd_k7s2_kernel (env DRO_K7_FWD_OFF=1: igemm_kernel, A/B)
+bool k7_fwd_ok(int KH, int KW, int Cin, int pad, int stride, int act, const float* bias) {
+  static const bool off = getenv("DRO_K7_FWD_OFF") != nullptr;
+  return !off && KH == 7 && KW == 7 && pad == 3 && stride == 2 && (Cin == 3 || Cin == 6) && act == 0 && !bias;
+}
+
+int launch_fwd_k7(IgArgs& a, hipStream_t s) {
+  const int tiles = a.g.B * ((a.g.H + 7) / 8) * ((a.g.W + 7) / 8);
+  static const int per = (int)env_int("DRO_K7_FWD_TILES_PER_BLOCK", 4);
+  int nb = (tiles + per - 1) / per;
+  if (nb < 1) nb = 1;
+  const dim3 grid((unsigned)nb, (unsigned)((a.g.Cout + 63) / 64));
+  conv_logf(2.0 * a.g.Cout * a.g.Cin * 49 * (double)a.g.B * a.g.H * a.g.W, "fwd_k7s2_kernel<%d>", a.g.Cin);
+  if (a.g.Cin == 3) hipLaunchKernelGGL((fwd_k7s2_kernel<3>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((fwd_k7s2_kernel<6>), grid, dim3(256), 0, s, a);
+  return launch_status("fwd_k7s2_kernel launch failed");
 }
 
 
@@ -3339,6 +3454,7 @@ extern "C" int dro_conv2d_strided_forward(const float* x, const float* weight, c
   a.kch = Cin;
   const long long P = (long long)B * Ho * Wo;
   hipStream_t s = (hipStream_t)stream;
+  if (k7_fwd_ok(KH, KW, Cin, pad, stride, act, bias)) return launch_fwd_k7(a, s);   // the stems
   DRO_ACT_SWITCH(act, st = (launch_igemm<0, A_, 0>(a, P, static_cast<char*>(workspace), s)));
   return st;
 }

@@ -30,18 +30,26 @@ def main():
             fn = lambda: torch.ops.dro.conv2d_strided_backward(x, w, gout, 2, 3, None, gw, None, 0)  # noqa: E731
         else:
             fn = lambda: _conv_bwd([x], w, None, gout, 0, 1.0, [None], [0], gw, gb, 0)  # noqa: E731
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(20):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / 20 * 1e3
         gf = 2.0 * Cout * Cin * 49 * B * Ho * Wo / 1e9
+        us = _time(fn)
         print(f"{tag:16s} {name:20s} {us:8.1f} us  {gf / us * 1e3:6.1f} TF/s (incl. finish)", flush=True)
+        if s == 2:
+            ftag = "igemm_kernel" if os.environ.get("DRO_K7_FWD_OFF") else "fwd_k7s2_kernel"
+            us = _time(lambda: torch.ops.dro.conv2d_strided(x, w, None, 2, 3, 0))
+            print(f"{ftag:16s} {name:20s} {us:8.1f} us  {gf / us * 1e3:6.1f} TF/s (forward)", flush=True)
+
+
+def _time(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
 
 
 if __name__ == "__main__":
