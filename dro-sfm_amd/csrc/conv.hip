@@ -2414,10 +2414,14 @@ int launch_wgrad_k7(IgArgs& a, int stride, int splits, hipStream_t s) {
   return launch_status("wgrad_finish_kernel launch failed");
 }
 
-// the stems' forward on fwd_k7s2_kernel (env DRO_K7_FWD_OFF=1: igemm_kernel, A/B)
+// the stems' forward on fwd_k7s2_kernel: opt-in (env DRO_K7_FWD=1).  Its
+// different (equally exact) summation order moves the golden flip step's
+// gradients past the reference-fixture check (depth_head.conv2.bias 0.23 %
+// from the reference's own fp32 value; the fp64-oracle check passes), so the
+// default keeps igemm_kernel's order
 bool k7_fwd_ok(int KH, int KW, int Cin, int pad, int stride, int act, const float* bias) {
-  static const bool off = getenv("DRO_K7_FWD_OFF") != nullptr;
-  return !off && KH == 7 && KW == 7 && pad == 3 && stride == 2 && (Cin == 3 || Cin == 6) && act == 0 && !bias;
+  static const bool on = env_int("DRO_K7_FWD", 0) != 0;
+  return on && KH == 7 && KW == 7 && pad == 3 && stride == 2 && (Cin == 3 || Cin == 6) && act == 0 && !bias;
 }
 
 int launch_fwd_k7(IgArgs& a, hipStream_t s) {

@@ -1,7 +1,7 @@
 """Weight-gradient kernel time of the 7x7 convs: the encoders' stems (stride 2)
 and the update blocks' state convs (stride 1) at the KITTI step's shapes,
 wgrad_k7_kernel vs wgrad_kernel (DRO_K7_WGRAD_OFF=1, read once per process).
-usage: [DRO_K7_WGRAD_OFF=1] python tools/bench_k7.py"""
+usage: [DRO_K7_WGRAD_OFF=1] [DRO_K7_FWD=1] python tools/bench_k7.py"""
 import os
 import sys
 
@@ -34,7 +34,7 @@ def main():
         us = _time(fn)
         print(f"{tag:16s} {name:20s} {us:8.1f} us  {gf / us * 1e3:6.1f} TF/s (incl. finish)", flush=True)
         if s == 2:
-            ftag = "igemm_kernel" if os.environ.get("DRO_K7_FWD_OFF") else "fwd_k7s2_kernel"
+            ftag = "fwd_k7s2_kernel" if os.environ.get("DRO_K7_FWD") == "1" else "igemm_kernel"
             us = _time(lambda: torch.ops.dro.conv2d_strided(x, w, None, 2, 3, 0))
             print(f"{ftag:16s} {name:20s} {us:8.1f} us  {gf / us * 1e3:6.1f} TF/s (forward)", flush=True)
 
