@@ -142,3 +142,26 @@ def test_conv_plans_within_kernel_limits(lib):
                 assert cps * ks >= nck and cps * (ks - 1) < nck
                 if ks > 1:
                     assert part >= ks * rows * B * H * W * 4
+
+
+def test_bn_fusion_arguments_rejected(lib):
+    """ABI 10 (BN inside the 3x3 convs): argument checks before any launch."""
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    assert lib.dro_bn_state_bytes(2, 8, 8, 16) > 0
+    assert lib.dro_bn_state_bytes(2, 8, 8, 5000) == 0                       # C >= 4096
+    # NULL x / weight / out
+    assert lib.dro_conv2d_bn_forward(None, 2, 8, 8, 4, p, 4, None, None, None, None, None, None, None, 0,
+                                     None) == -1
+    # in_state without in_y; skip without in_state
+    assert lib.dro_conv2d_bn_forward(p, 2, 8, 8, 4, p, 4, p, None, None, None, None, p, p, 1 << 20, None) == -1
+    assert lib.dro_conv2d_bn_forward(p, 2, 8, 8, 4, p, 4, None, p, None, None, None, p, p, 1 << 20, None) == -1
+    assert lib.dro_conv2d_bn_forward(p, 0, 8, 8, 4, p, 4, None, None, None, None, None, p, p, 1 << 20, None) == -2
+    # g with accumulation, and both gin_state and src_bn in one call
+    gp = (ctypes.c_void_p * 7)(p.value, p.value, None, p.value, p.value, None, None)
+    assert lib.dro_conv2d_bn_backward_data(p, 2, 8, 8, 4, 4, p, None, None, None, gp, p, p, 1, p, 1 << 20,
+                                           None) == -3
+    assert lib.dro_conv2d_bn_backward_data(p, 2, 8, 8, 4, 4, p, p, p, p, gp, p, p, 0, p, 1 << 20, None) == -3
+    assert lib.dro_bn_apply(None, None, 1, 2, 4, 8, 8, p, p, None) == -1
+    assert lib.dro_bn_apply(p, None, 2, 2, 4, 8, 8, p, p, None) == -3          # relu must be 0 / 1
+    assert lib.dro_bn_backward_apply(p, None, 2, 4, 8, 8, p, p, None) == -1
