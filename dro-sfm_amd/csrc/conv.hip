@@ -1610,17 +1610,25 @@ static void launch_wgrad_finish(const IgArgs& a, int splits, hipStream_t s) {
 // Wave w owns 32-column subtiles w, w + NW, ... (J of them).  The bias column
 // (NK) is the per-block row sum of G.  Partials [split][Cout][NK + 1] for
 // wgrad_finish_kernel (fixed order: the same finish as wgrad_kernel's).
-template <int S, int CIN, int NW, int J>
-__global__ __launch_bounds__(64 * NW) void wgrad_k7_kernel(IgArgs a) {
+template <int S, int CIN, int NW, int J, int GR>
+__global__ __launch_bounds__(64 * NW * GR) void wgrad_k7_kernel(IgArgs a) {
+  // GR wave groups per block (NW waves each) take alternate tiles of the
+  // block's list with their own LDS buffers, and their accumulators are
+  // summed (group order) before the one partial: more waves per CU without
+  // more partials
   constexpr int PD = 7 * S + 7, PDP = PD | 1, GS = 65, NK = CIN * 49, NSUB = (NK + 31) / 32;
   constexpr int NTH = 64 * NW, PATCH = CIN * PD * PDP, NPE = CIN * PD * PD;
   constexpr int GPER = (4096 + NTH - 1) / NTH, PPER = (NPE + NTH - 1) / NTH;
-  static_assert(NW * J >= NSUB && NW <= 8, "subtiles per wave");
-  __shared__ float Gs[64 * GS];
-  __shared__ float Ps[PATCH + 1];        // [CIN][PD][PDP], then one zero
+  static_assert(NW * J >= NSUB && NW * GR <= 16, "subtiles per wave");
+  __shared__ float Gs_all[GR][64 * GS];
+  __shared__ float Ps_all[GR][PATCH + 1];    // [CIN][PD][PDP], then one zero
+  __shared__ float cmb[GR > 1 ? NTH * 16 + 64 : 1];
   const int Cout = a.g.Cout, B = a.g.B, Ho = a.g.H, Wo = a.g.W;
   const int Hi = a.Hs, Wi = a.Ws;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = GR == 1 ? 0 : wave / NW, wv = wave - grp * NW, tid = threadIdx.x - grp * NTH;
+  float* Gs = Gs_all[grp];
+  float* Ps = Ps_all[grp];
   const int o0 = blockIdx.y * 64;
   const int txs = (Wo + 7) / 8, tis = ((Ho + 7) / 8) * txs, tiles = B * tis;
   const float* __restrict__ Gp = a.G;
@@ -1630,7 +1638,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_k7_kernel(IgArgs a) {
   int boff[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int n = (wave + j * NW) * 32 + (lane & 31);
+    const int n = (wv + j * NW) * 32 + (lane & 31);
     if (n < NK) {
       const int tap = n / CIN, c = n - tap * CIN, ty = tap / 7, tx = tap - ty * 7;
       boff[j] = (c * PD + ty) * PDP + tx;
@@ -1646,7 +1654,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_k7_kernel(IgArgs a) {
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[j][u][r] = 0.f;
-  float bsum = 0.f;                      // bias column: thread o < 64
+  float bsum = 0.f;                      // bias column: thread o < 64 of each group
   if (tid == 0) Ps[PATCH] = 0.f;
   // this thread's staging slots (compile-time counts): the next tile's G and
   // patch are loaded into registers while the current one is multiplied
@@ -1687,52 +1695,81 @@ __global__ __launch_bounds__(64 * NW) void wgrad_k7_kernel(IgArgs a) {
       }
     }
   };
-  if ((int)blockIdx.x < tiles) {
-    load_tile(blockIdx.x);
+  // the block's tiles blockIdx.x + i * gridDim.x; group g takes i = g, g + GR, ...
+  const int step = GR * gridDim.x;
+  const int nblk = (int)blockIdx.x < tiles ? (tiles - (int)blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+  const int iters = (nblk + GR - 1) / GR;
+  const int t0 = blockIdx.x + grp * gridDim.x;
+  if (t0 < tiles) {
+    load_tile(t0);
     store_tile();
   }
   __syncthreads();
-  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int tn = t + gridDim.x;
+  for (int m = 0, t = t0; m < iters; ++m, t += step) {
+    const int tn = t + step;
+    const bool has = t < tiles;
     if (tn < tiles) load_tile(tn);
-    if (a.gbias && tid < 64) {
-      float sb = 0.f;
-      for (int p = 0; p < 64; ++p) sb += Gs[tid * GS + p];
-      bsum += sb;
-    }
-    // LDS operands one step ahead of the MFMAs
-    float a0n = Gs[(lane & 31) * GS + h], a1n = Gs[(32 + (lane & 31)) * GS + h];
-    float bn[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) bn[j] = Ps[boff[j] < 0 ? PATCH : boff[j] + S * h];
-#pragma unroll 8
-    for (int k = 0; k < 32; ++k) {
-      const float a0 = a0n, a1 = a1n;
-      float bv[J];
-#pragma unroll
-      for (int j = 0; j < J; ++j) bv[j] = bn[j];
-      if (k + 1 < 32) {
-        const int p = 2 * (k + 1) + h, po = S * (p >> 3) * PDP + S * (p & 7);
-        a0n = Gs[(lane & 31) * GS + p];
-        a1n = Gs[(32 + (lane & 31)) * GS + p];
-#pragma unroll
-        for (int j = 0; j < J; ++j) bn[j] = Ps[boff[j] < 0 ? PATCH : boff[j] + po];
+    if (has) {
+      if (a.gbias && tid < 64) {
+        float sb = 0.f;
+        for (int p = 0; p < 64; ++p) sb += Gs[tid * GS + p];
+        bsum += sb;
       }
+      // LDS operands one step ahead of the MFMAs
+      float a0n = Gs[(lane & 31) * GS + h], a1n = Gs[(32 + (lane & 31)) * GS + h];
+      float bn[J];
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        acc[j][0] = mfma32(a0, bv[j], acc[j][0]);
-        acc[j][1] = mfma32(a1, bv[j], acc[j][1]);
+      for (int j = 0; j < J; ++j) bn[j] = Ps[boff[j] < 0 ? PATCH : boff[j] + S * h];
+#pragma unroll 8
+      for (int k = 0; k < 32; ++k) {
+        const float a0 = a0n, a1 = a1n;
+        float bv[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) bv[j] = bn[j];
+        if (k + 1 < 32) {
+          const int p = 2 * (k + 1) + h, po = S * (p >> 3) * PDP + S * (p & 7);
+          a0n = Gs[(lane & 31) * GS + p];
+          a1n = Gs[(32 + (lane & 31)) * GS + p];
+#pragma unroll
+          for (int j = 0; j < J; ++j) bn[j] = Ps[boff[j] < 0 ? PATCH : boff[j] + po];
+        }
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          acc[j][0] = mfma32(a0, bv[j], acc[j][0]);
+          acc[j][1] = mfma32(a1, bv[j], acc[j][1]);
+        }
       }
     }
     __syncthreads();                     // every wave is done with this tile
     if (tn < tiles) store_tile();
     __syncthreads();
   }
-  const int NKr = NK;
-  float* part = a.part + (size_t)blockIdx.x * Cout * (NKr + 1);
+  if constexpr (GR > 1) {
+    // group 1's sums into group 0's (one (j, u) accumulator at a time)
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (grp == 1) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cmb[(wv * 64 + lane) * 16 + r] = acc[j][u][r];
+        }
+        __syncthreads();
+        if (grp == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[j][u][r] += cmb[(wv * 64 + lane) * 16 + r];
+        }
+        __syncthreads();
+      }
+    if (grp == 1 && tid < 64) cmb[NTH * 16 + tid] = bsum;
+    __syncthreads();
+    if (grp == 0 && tid < 64) bsum += cmb[NTH * 16 + tid];
+    if (grp != 0) return;
+  }
+  float* part = a.part + (size_t)blockIdx.x * Cout * (NK + 1);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int n = (wave + j * NW) * 32 + (lane & 31);
+    const int n = (wv + j * NW) * 32 + (lane & 31);
     if (n >= NK) continue;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -2398,11 +2435,22 @@ int launch_wgrad_k7(IgArgs& a, int stride, int splits, hipStream_t s) {
   if (splits < 1) splits = 1;
   const dim3 grid((unsigned)splits, (unsigned)((a.g.Cout + 63) / 64));
   conv_logf(2.0 * a.g.Cout * NK * (double)a.g.B * a.g.H * a.g.W, "wgrad_k7_kernel<%d, %d>", stride, Cin);
-  // (S, CIN, waves, subtiles per wave): 32-column subtiles of the 49 Cin columns
-  if (stride == 2 && Cin == 3) hipLaunchKernelGGL((wgrad_k7_kernel<2, 3, 5, 1>), grid, dim3(320), 0, s, a);
-  else if (stride == 2 && Cin == 6) hipLaunchKernelGGL((wgrad_k7_kernel<2, 6, 5, 2>), grid, dim3(320), 0, s, a);
-  else if (stride == 1 && Cin == 1) hipLaunchKernelGGL((wgrad_k7_kernel<1, 1, 2, 1>), grid, dim3(128), 0, s, a);
-  else if (stride == 1 && Cin == 6) hipLaunchKernelGGL((wgrad_k7_kernel<1, 6, 5, 2>), grid, dim3(320), 0, s, a);
+  // (S, CIN, waves, subtiles per wave, wave groups): 32-column subtiles of the
+  // 49 Cin columns; two wave groups per block for the 3-channel stems (fnet
+  // 93 -> 78 us, cnet_depth 41 -> 37 us; the 6-channel variant spills and is
+  // no faster), DRO_K7_GROUPS=1|2 forces one (A/B)
+  static const int forced = env_int("DRO_K7_GROUPS", 0);
+  const int groups = forced == 1 || forced == 2 ? forced : (stride == 2 && Cin == 3 ? 2 : 1);
+#define DRO_K7(S_, C_, NW_, J_)                                                                         \
+  do {                                                                                                  \
+    if (groups == 2) hipLaunchKernelGGL((wgrad_k7_kernel<S_, C_, NW_, J_, 2>), grid, dim3(128 * NW_), 0, s, a); \
+    else hipLaunchKernelGGL((wgrad_k7_kernel<S_, C_, NW_, J_, 1>), grid, dim3(64 * NW_), 0, s, a);     \
+  } while (0)
+  if (stride == 2 && Cin == 3) DRO_K7(2, 3, 5, 1);
+  else if (stride == 2 && Cin == 6) DRO_K7(2, 6, 5, 2);
+  else if (stride == 1 && Cin == 1) DRO_K7(1, 1, 2, 1);
+  else if (stride == 1 && Cin == 6) DRO_K7(1, 6, 5, 2);
+#undef DRO_K7
   else {
     set_error("wgrad_k7: unsupported channel count");
     return DRO_E_SHAPE;
